@@ -1,0 +1,205 @@
+/*
+ * och_gpu.h -- C ABI of the MI355X (gfx950) sparse-voxel-octree ray caster.
+ *
+ * Drop-in boundary for the reference's hot path (ORT/ = Octree_Ray_Tracing/):
+ *
+ *   void h_octree<L,D>::sse_trace(float ox, float oy, float oz,
+ *                                 float dx, float dy, float dz,
+ *                                 och::direction& hit_direction,
+ *                                 uint32_t& hit_voxel, float& hit_time) const;
+ *                                                   ORT/och_h_octree.h:292, :449
+ *   void octree::sse_trace(...)                     ORT/och_octree.h:56-58, ORT/och_octree.cpp:167
+ *   tree_camera::update_position()  (ray generator) ORT/test_och_h_octree.cpp:87-138
+ *   tree_window::update_image() + trace_pixel()     ORT/test_och_h_octree.cpp:437-457, :64-85
+ *
+ * Every entry point returns an och_status (0 = OK).  Host buffers belong to
+ * the caller; device memory belongs to the pool.  Functions suffixed _dev take
+ * device pointers and enqueue on the pool's HIP stream without synchronising.
+ * Results are bit-identical to the reference CPU tracer run with the same
+ * RCPPS table (och_gpu_set_rcp_lut / och_host_rcp_lut).
+ */
+#ifndef OCH_GPU_H
+#define OCH_GPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define OCH_GPU_ABI_VERSION 1
+
+#if defined(__GNUC__)
+#define OCH_API __attribute__((visibility("default")))
+#else
+#define OCH_API
+#endif
+
+typedef enum och_status {
+    OCH_OK = 0,
+    OCH_E_INVALID = -1,     /* bad argument / precondition */
+    OCH_E_HIP = -2,         /* HIP runtime error (see och_last_error) */
+    OCH_E_NODEV = -3,       /* no gfx950 device visible */
+    OCH_E_RCP_MODEL = -4,   /* host RCPPS is not representable as a mantissa table */
+    OCH_E_NOMEM = -5,
+    OCH_E_CAPACITY = -6     /* builder: node table full (reference: exit(0), ORT/och_h_octree.h:112-116) */
+} och_status;
+
+/* och::direction, ORT/och_tree_helper.h:7-18: the ray-travel sign on the
+ * axis whose face was crossed last; exit = miss, inside = origin in a voxel. */
+typedef enum och_direction {
+    OCH_X_POS = 0, OCH_Y_POS = 1, OCH_Z_POS = 2,
+    OCH_X_NEG = 3, OCH_Y_NEG = 4, OCH_Z_NEG = 5,
+    OCH_EXIT = 6, OCH_INSIDE = 7, OCH_ERROR = 8
+} och_direction;
+
+typedef struct och_gpu_pool och_gpu_pool;
+
+/* Camera uniforms of tree_camera::update_position (ORT/test_och_h_octree.cpp:87-115),
+ * computed ONCE per frame on the host (sinf/cosf/tanf of this host's libm)
+ * by och_camera_setup; the per-pixel part runs on the GPU. */
+typedef struct och_camera {
+    float pos[3];        /* ray origin, tree occupies [1,2)^3 (ORT/test_och_h_octree.cpp:55) */
+    float rot[9];        /* t_x_fx, t_x_fy, t_x_fz, t_y_fx, ..., t_z_fz (:107-115) */
+    float fov_factor;    /* 1 / tanf(fov / 2) (:97) */
+    float aspect;        /* (float)W / (float)H (:89) */
+    float view_x;        /* 2.0F / (float)W (:91) */
+    float view_y;        /* 2.0F / (float)H (:93) */
+    int32_t width, height;
+} och_camera;
+
+typedef struct och_pool_info {
+    uint64_t device_bytes;   /* node pool bytes resident in HBM */
+    uint32_t n_nodes;        /* nodes uploaded (incl. the padding slot of 1-based pools) */
+    uint32_t root;
+    int32_t depth;
+    int32_t index_base;
+    float miss_t;
+    int32_t rcp_log2_entries;
+    int32_t device;
+} och_pool_info;
+
+/* ------------------------------------------------------------ runtime */
+OCH_API int och_abi_version(void);
+OCH_API const char *och_last_error(void);      /* thread-local message of the last failure */
+OCH_API int och_device_count(int *count);       /* visible gfx950 devices */
+
+/* ------------------------------------------------------------ RCPPS model */
+/* Capture this host CPU's _mm_rcp_ps (the reference's reciprocal,
+ * ORT/och_h_octree.h:316) as a 2^k table over the mantissa of inputs in [-2,-1),
+ * after checking that the result depends only on the top k mantissa bits and
+ * that other exponents shift the result exponent.  lut must hold 1<<23 entries
+ * (worst case); *log2_entries receives k.  Returns OCH_E_RCP_MODEL if the host
+ * instruction does not follow the model (then pass an explicit table). */
+OCH_API int och_host_rcp_lut(uint32_t *lut, int *log2_entries);
+/* Same model evaluated on the host, for a single input bit pattern. */
+OCH_API uint32_t och_rcp_from_lut(uint32_t xbits, const uint32_t *lut, int log2_entries);
+
+/* ------------------------------------------------------------ node pools */
+/* Upload a node pool.  nodes = n_nodes x 8 uint32 child slots exactly as the
+ * reference lays them out (ORT/och_h_octree.h:38-40): interior slots hold node
+ * indices, the leaf level holds voxel ids, 0 = empty.
+ *   index_base 1: h_octree -- indices are 1-based into nodes[] (the
+ *                 reference's table->nodes with root_idx, ORT/och_h_octree.h:93-95);
+ *   index_base 0: octree   -- 0-based, root = 0 (ORT/och_octree.cpp:207).
+ * miss_t: hit_time reported for a miss (+INF for h_octree, :429; 0.0F for
+ * octree, ORT/och_octree.cpp:302).  depth = number of levels (1..22).
+ * The pool starts with this host's RCPPS table (och_host_rcp_lut); override
+ * with och_gpu_set_rcp_lut.  device < 0 selects the current HIP device. */
+OCH_API int och_gpu_pool_create(const uint32_t *nodes, uint32_t n_nodes, uint32_t root, int depth,
+                                int index_base, float miss_t, int device, och_gpu_pool **out);
+OCH_API int och_gpu_pool_destroy(och_gpu_pool *pool);
+OCH_API int och_gpu_pool_info(const och_gpu_pool *pool, och_pool_info *info);
+/* Re-upload nodes [first, first+count) (pool numbering) and set a new root --
+ * mirrors h_octree::set's path copy (ORT/och_h_octree.h:176-237) after an edit. */
+OCH_API int och_gpu_pool_update(och_gpu_pool *pool, uint32_t first, uint32_t count,
+                                const uint32_t *nodes, uint32_t root);
+OCH_API int och_gpu_set_rcp_lut(och_gpu_pool *pool, const uint32_t *lut, int log2_entries);
+/* Palette: n_voxels x 6 RGBA8 colours (olc::Pixel layout, r in the low byte),
+ * ordered x_pos..z_neg per voxel id 1..n (ORT/och_voxel.cpp:195-305). */
+OCH_API int och_gpu_set_palette(och_gpu_pool *pool, const uint32_t *rgba, uint32_t n_voxels);
+/* Use a caller-owned HIP stream (hipStream_t) for all _dev calls; NULL = the pool's own. */
+OCH_API int och_gpu_set_stream(och_gpu_pool *pool, void *hip_stream);
+OCH_API int och_gpu_synchronize(och_gpu_pool *pool);
+/* Duration of the most recent trace/render kernel launched on the pool,
+ * measured with HIP events on the stream it ran on (blocks until it ends). */
+OCH_API int och_gpu_last_kernel_ms(och_gpu_pool *pool, float *ms);
+
+/* ------------------------------------------------------------ tracing */
+/* Reference signature: one ray, synchronous (the pick ray of
+ * ORT/test_och_h_octree.cpp:536).  Requires origin in (1,2)^3. */
+OCH_API int och_gpu_trace(och_gpu_pool *pool, float ox, float oy, float oz, float dx, float dy, float dz,
+                          int32_t *hit_direction, uint32_t *hit_voxel, float *hit_time);
+/* Batch of n rays, host buffers, synchronous.  origin_stride 0 = one shared
+ * origin (3 floats), 3 = one origin per ray.  dirs: n x 3 floats (och::float3
+ * AoS, ORT/test_och_h_octree.cpp:49).  Outputs: n each. */
+OCH_API int och_gpu_trace_batch(och_gpu_pool *pool, const float *origin, int origin_stride,
+                                const float *dirs, uint32_t n,
+                                int32_t *hit_direction, uint32_t *hit_voxel, float *hit_time);
+/* Same with device buffers, asynchronous on the pool stream.  push_count
+ * (optional, may be NULL) receives the PUSH iterations (child fetches) per ray. */
+OCH_API int och_gpu_trace_batch_dev(och_gpu_pool *pool, const float *origin, int origin_stride,
+                                    const float *dirs, uint32_t n,
+                                    int32_t *hit_direction, uint32_t *hit_voxel, float *hit_time,
+                                    uint32_t *push_count);
+
+/* ------------------------------------------------------------ camera / frame */
+/* tree_camera::update_position's per-frame constants (ORT/test_och_h_octree.cpp:89-115):
+ * yaw = camera.dir.x, pitch = camera.dir.y, fov = 1.25F in the reference. */
+OCH_API int och_camera_setup(float px, float py, float pz, float yaw, float pitch, float fov,
+                             int width, int height, och_camera *cam);
+/* Per-pixel ray directions (row-major, x + y*W) into a device buffer of W*H*3 floats. */
+OCH_API int och_gpu_raygen_dev(och_gpu_pool *pool, const och_camera *cam, float *dirs);
+/* One frame of update_position + update_image (ORT/test_och_h_octree.cpp:437-457):
+ * raygen, trace and shade fused, RGBA8 into a host W*H buffer. */
+OCH_API int och_gpu_render(och_gpu_pool *pool, const och_camera *cam, uint32_t *rgba);
+/* Sharded device render: rows are dealt in chunks of row_chunk rows round-robin
+ * over n_shards; this call renders shard `shard` into `rgba_slice`, a compact
+ * buffer of och_shard_rows(H, row_chunk, n_shards) x W pixels. n_shards = 1,
+ * row_chunk = H renders the whole frame. */
+OCH_API int och_gpu_render_dev(och_gpu_pool *pool, const och_camera *cam, uint32_t *rgba_slice,
+                               int row_chunk, int shard, int n_shards);
+OCH_API int och_shard_rows(int height, int row_chunk, int n_shards);
+/* Reassemble n_shards gathered slices (slice s at gathered + s*rows*W) into a
+ * full W*H frame on the device. */
+OCH_API int och_gpu_unshard_dev(och_gpu_pool *pool, const uint32_t *gathered, uint32_t *frame,
+                                int width, int height, int row_chunk, int n_shards);
+
+/* ------------------------------------------------------------ builder */
+/* The demo terrain (ORT/test_och_h_octree.cpp:561-787) built in parallel
+ * bottom-up, hash-consed to the same canonical DAG h_octree produces.
+ * Output pool is breadth-first (root first, levels contiguous), 1-based with
+ * slot 0 unused when dedup = 1 (an h_octree pool), or an expanded 0-based tree
+ * with root 0 when dedup = 0 (an och::octree pool). */
+typedef struct och_terrain_params {
+    int32_t depth;          /* 1..12: dim = 1 << depth */
+    int32_t tunnels;        /* apply the remove(tree, tunnels) pass (:786) */
+    int32_t dedup;          /* 1 = h_octree DAG, 0 = pointer octree */
+    int32_t rand_kind;      /* 0 = glibc rand() default seed, 1 = MSVC rand() */
+    int32_t threads;        /* 0 = all hardware threads */
+    int32_t use_gpu;        /* evaluate voxels on the GPU when one is present */
+} och_terrain_params;
+
+typedef struct och_host_pool {
+    uint32_t *nodes;        /* n_nodes x 8 */
+    uint32_t n_nodes;
+    uint32_t root;
+    int32_t depth;
+    int32_t index_base;
+    uint64_t solid_voxels;  /* statistics */
+    uint64_t voxel_hist[8]; /* count per voxel id 0..7 (solid ids) */
+    uint64_t tree_nodes;    /* nodes of the expanded tree (h_octree nodecnt) */
+    double build_seconds;
+} och_host_pool;
+
+OCH_API int och_build_terrain(const och_terrain_params *params, och_host_pool *out);
+OCH_API void och_host_pool_free(och_host_pool *pool);
+/* h_octree::at over any pool (ORT/och_h_octree.h:239-258). */
+OCH_API uint32_t och_pool_at(const uint32_t *nodes, uint32_t root, int depth, int index_base,
+                             int x, int y, int z);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* OCH_GPU_H */

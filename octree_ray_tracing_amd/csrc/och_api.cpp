@@ -1,0 +1,567 @@
+// och_api.cpp -- the C ABI (include/och_gpu.h): pools, RCPPS capture, camera
+// constants, synchronous and asynchronous trace / render entry points.
+#include <hip/hip_runtime.h>
+#include <immintrin.h>
+
+#include <atomic>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "och_internal.h"
+
+namespace {
+
+thread_local std::string g_error;
+
+int fail(int status, const char *fmt, ...)
+{
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    g_error = buf;
+    return status;
+}
+
+#define OCH_HIP(expr)                                                                        \
+    do {                                                                                     \
+        const hipError_t e_ = (expr);                                                        \
+        if (e_ != hipSuccess) return fail(OCH_E_HIP, "%s: %s", #expr, hipGetErrorString(e_)); \
+    } while (0)
+
+// Keep the caller's current device (torch sets one per rank) across calls.
+struct DeviceGuard {
+    int prev = -1;
+    bool ok = true;
+    explicit DeviceGuard(int dev)
+    {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        if (dev >= 0 && dev != prev) ok = hipSetDevice(dev) == hipSuccess;
+    }
+    ~DeviceGuard()
+    {
+        int cur = -1;
+        if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+    }
+};
+
+// ------------------------------------------------------------ RCPPS capture
+
+inline uint32_t rcpps_native(uint32_t x)
+{
+    const __m128 r = _mm_rcp_ps(_mm_castsi128_ps(_mm_set1_epi32((int)x)));
+    return (uint32_t)_mm_cvtsi128_si32(_mm_castps_si128(r));
+}
+
+struct HostRcp {
+    int status = OCH_OK;
+    int log2_entries = 0;
+    std::vector<uint32_t> lut;
+    std::string error;
+};
+
+const HostRcp &host_rcp()
+{
+    static HostRcp cap;
+    static std::once_flag once;
+    std::call_once(once, [] {
+        const uint32_t n = 1u << 23;
+        std::vector<uint32_t> full(n);
+        for (uint32_t m = 0; m < n; m += 4) {
+            const __m128i x = _mm_set_epi32((int)(0xBF800000u | (m + 3)), (int)(0xBF800000u | (m + 2)),
+                                            (int)(0xBF800000u | (m + 1)), (int)(0xBF800000u | m));
+            _mm_storeu_si128((__m128i *)&full[m], _mm_castps_si128(_mm_rcp_ps(_mm_castsi128_ps(x))));
+        }
+        // Smallest k such that the result only depends on the top k mantissa bits.
+        int k = 23;
+        for (int cand = 8; cand <= 23; ++cand) {
+            const uint32_t block = 1u << (23 - cand);
+            bool ok = true;
+            for (uint32_t m = 0; m < n && ok; ++m) ok = full[m] == full[m & ~(block - 1)];
+            if (ok) { k = cand; break; }
+        }
+        cap.log2_entries = k;
+        cap.lut.resize(1u << k);
+        for (uint32_t i = 0; i < (1u << k); ++i) cap.lut[i] = full[(size_t)i << (23 - k)];
+        // Check the exponent model on every exponent (negative inputs, as the tracer uses).
+        for (uint32_t e = 0; e < 256 && cap.status == OCH_OK; ++e)
+            for (uint32_t m = 0; m < n; m += (e == 127 ? 1u : 997u)) {
+                const uint32_t x = 0x80000000u | (e << 23) | m;
+                if (e == 255 && m) continue;   // NaN payload handling is not used by the tracer
+                const uint32_t want = rcpps_native(x);
+                const uint32_t got = och_rcp_from_lut(x, cap.lut.data(), k);
+                if (want != got) {
+                    cap.status = OCH_E_RCP_MODEL;
+                    char buf[160];
+                    snprintf(buf, sizeof buf, "host RCPPS(0x%08x) = 0x%08x, table model gives 0x%08x", x, want, got);
+                    cap.error = buf;
+                    break;
+                }
+            }
+    });
+    return cap;
+}
+
+}  // namespace
+
+// ------------------------------------------------------------ pool object
+
+struct och_gpu_pool {
+    int device = 0;
+    uint32_t *d_nodes = nullptr;    // with one padding node in front for 1-based pools
+    uint32_t n_nodes = 0;           // nodes in d_nodes
+    uint32_t root = 0;
+    int depth = 0;
+    int index_base = 1;
+    float miss_t = INFINITY;
+    uint32_t *d_lut = nullptr;
+    int lut_log2 = 0;
+    uint32_t *d_palette = nullptr;
+    uint32_t n_voxels = 0;
+    hipStream_t own_stream = nullptr;
+    hipStream_t ext_stream = nullptr;
+    hipEvent_t ev_start = nullptr, ev_stop = nullptr;
+    bool timed = false;
+    // host mirror of the uploaded nodes (user numbering), for validating edits
+    std::vector<uint32_t> mirror;
+    // host-call staging
+    void *d_scratch = nullptr;
+    size_t scratch_bytes = 0;
+
+    hipStream_t stream() const { return ext_stream ? ext_stream : own_stream; }
+
+    och::DevPool dev() const
+    {
+        och::DevPool p;
+        p.nodes = d_nodes;
+        p.lut = d_lut;
+        p.root = root;
+        p.depth = depth;
+        p.lut_shift = 23 - lut_log2;
+        uint32_t mb;
+        std::memcpy(&mb, &miss_t, 4);
+        p.miss_bits = mb;
+        return p;
+    }
+};
+
+namespace {
+
+int ensure_scratch(och_gpu_pool *p, size_t bytes)
+{
+    if (bytes <= p->scratch_bytes) return OCH_OK;
+    if (p->d_scratch) OCH_HIP(hipFree(p->d_scratch));
+    p->d_scratch = nullptr;
+    p->scratch_bytes = 0;
+    OCH_HIP(hipMalloc(&p->d_scratch, bytes));
+    p->scratch_bytes = bytes;
+    return OCH_OK;
+}
+
+// Walk every reachable (node, level) pair once and check that interior slots
+// name nodes inside the pool, so no kernel can read out of bounds.
+int validate_pool(const uint32_t *nodes, uint32_t n_nodes, uint32_t root, int depth, int base)
+{
+    if (depth < 1 || depth > 22) return fail(OCH_E_INVALID, "depth %d outside 1..22", depth);
+    if (n_nodes == 0) return fail(OCH_E_INVALID, "empty node array");
+    if ((uint64_t)n_nodes + 1 >= (1ull << 29)) return fail(OCH_E_INVALID, "pool of %u nodes exceeds 2^29", n_nodes);
+    auto in_range = [&](uint32_t v) { return base == 1 ? (v >= 1 && v <= n_nodes) : (v < n_nodes); };
+    if (base == 1 && root == 0) return OCH_OK;   // empty h_octree: every ray misses
+    if (!in_range(root)) return fail(OCH_E_INVALID, "root %u outside the pool", root);
+    std::vector<uint32_t> seen(n_nodes, 0);
+    std::vector<uint32_t> cur{root}, next;
+    seen[root - base] |= 1u << 1;
+    for (int level = 1; level < depth; ++level) {
+        next.clear();
+        for (uint32_t v : cur) {
+            const uint32_t *c = nodes + (size_t)(v - base) * 8;
+            for (int k = 0; k < 8; ++k) {
+                if (!c[k]) continue;
+                if (!in_range(c[k]) || (base == 0 && c[k] == 0))
+                    return fail(OCH_E_INVALID, "node %u (level %d) slot %d names %u, outside the pool", v, level, k, c[k]);
+                uint32_t &s = seen[c[k] - base];
+                if (!(s & (1u << (level + 1)))) {
+                    s |= 1u << (level + 1);
+                    next.push_back(c[k]);
+                }
+            }
+        }
+        cur.swap(next);
+    }
+    return OCH_OK;
+}
+
+int upload_lut(och_gpu_pool *p, const uint32_t *lut, int log2_entries)
+{
+    if (!lut || log2_entries < 1 || log2_entries > 23) return fail(OCH_E_INVALID, "bad RCPPS table");
+    if (p->d_lut) OCH_HIP(hipFree(p->d_lut));
+    p->d_lut = nullptr;
+    const size_t bytes = sizeof(uint32_t) << log2_entries;
+    OCH_HIP(hipMalloc(&p->d_lut, bytes));
+    OCH_HIP(hipMemcpy(p->d_lut, lut, bytes, hipMemcpyHostToDevice));
+    p->lut_log2 = log2_entries;
+    return OCH_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+OCH_API int och_abi_version(void) { return OCH_GPU_ABI_VERSION; }
+
+OCH_API const char *och_last_error(void) { return g_error.c_str(); }
+
+OCH_API int och_device_count(int *count)
+{
+    if (!count) return fail(OCH_E_INVALID, "count is NULL");
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) n = 0;
+    int gfx950 = 0;
+    for (int i = 0; i < n; ++i) {
+        hipDeviceProp_t prop;
+        if (hipGetDeviceProperties(&prop, i) == hipSuccess && std::strncmp(prop.gcnArchName, "gfx950", 6) == 0)
+            ++gfx950;
+    }
+    *count = gfx950;
+    return OCH_OK;
+}
+
+OCH_API uint32_t och_rcp_from_lut(uint32_t x, const uint32_t *lut, int log2_entries)
+{
+    const uint32_t sign = x & 0x80000000u, e = (x >> 23) & 0xFFu;
+    if (e == 0) return sign | 0x7F800000u;
+    if (e == 0xFFu) return (x & 0x7FFFFFu) ? (x | 0x400000u) : sign;
+    const uint32_t ent = lut[(x & 0x7FFFFFu) >> (23 - log2_entries)];
+    const int ne = (int)((ent >> 23) & 0xFFu) + 127 - (int)e;
+    return ne <= 0 ? sign : (sign | ((uint32_t)ne << 23) | (ent & 0x7FFFFFu));
+}
+
+OCH_API int och_host_rcp_lut(uint32_t *lut, int *log2_entries)
+{
+    const HostRcp &c = host_rcp();
+    if (c.status != OCH_OK) return fail(c.status, "%s", c.error.c_str());
+    if (lut) std::memcpy(lut, c.lut.data(), c.lut.size() * sizeof(uint32_t));
+    if (log2_entries) *log2_entries = c.log2_entries;
+    return OCH_OK;
+}
+
+OCH_API int och_gpu_pool_create(const uint32_t *nodes, uint32_t n_nodes, uint32_t root, int depth, int index_base,
+                                float miss_t, int device, och_gpu_pool **out)
+{
+    if (!nodes || !out) return fail(OCH_E_INVALID, "nodes/out is NULL");
+    if (index_base != 0 && index_base != 1) return fail(OCH_E_INVALID, "index_base must be 0 or 1");
+    *out = nullptr;
+    int st = validate_pool(nodes, n_nodes, root, depth, index_base);
+    if (st != OCH_OK) return st;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(OCH_E_NODEV, "no HIP device visible");
+    if (device < 0) OCH_HIP(hipGetDevice(&device));
+    if (device >= ndev) return fail(OCH_E_NODEV, "device %d of %d", device, ndev);
+    DeviceGuard g(device);
+    if (!g.ok) return fail(OCH_E_HIP, "hipSetDevice(%d) failed", device);
+
+    och_gpu_pool *p = new och_gpu_pool;
+    p->device = device;
+    p->depth = depth;
+    p->index_base = index_base;
+    p->miss_t = miss_t;
+    p->root = root;
+    p->n_nodes = n_nodes + (uint32_t)index_base;   // padding node 0 for 1-based pools
+    const size_t bytes = (size_t)p->n_nodes * 32;
+    auto bail = [&](int s) { och_gpu_pool_destroy(p); return s; };
+    if (hipMalloc(&p->d_nodes, bytes) != hipSuccess) return bail(fail(OCH_E_NOMEM, "hipMalloc(%zu) failed", bytes));
+    if (index_base == 1 && hipMemset(p->d_nodes, 0, 32) != hipSuccess) return bail(fail(OCH_E_HIP, "hipMemset failed"));
+    if (hipMemcpy(p->d_nodes + 8 * index_base, nodes, (size_t)n_nodes * 32, hipMemcpyHostToDevice) != hipSuccess)
+        return bail(fail(OCH_E_HIP, "node upload failed"));
+    p->mirror.assign(nodes, nodes + (size_t)n_nodes * 8);
+    if (hipStreamCreateWithFlags(&p->own_stream, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreate(&p->ev_start) != hipSuccess || hipEventCreate(&p->ev_stop) != hipSuccess)
+        return bail(fail(OCH_E_HIP, "stream/event creation failed"));
+    const HostRcp &rc = host_rcp();
+    if (rc.status == OCH_OK) {
+        st = upload_lut(p, rc.lut.data(), rc.log2_entries);
+        if (st != OCH_OK) return bail(st);
+    }
+    // A host whose RCPPS does not fit the model leaves the pool without a table:
+    // tracing then fails with OCH_E_RCP_MODEL until och_gpu_set_rcp_lut is called.
+    *out = p;
+    return OCH_OK;
+}
+
+OCH_API int och_gpu_pool_destroy(och_gpu_pool *p)
+{
+    if (!p) return OCH_OK;
+    DeviceGuard g(p->device);
+    if (p->own_stream) (void)hipStreamSynchronize(p->own_stream);
+    if (p->ext_stream) (void)hipStreamSynchronize(p->ext_stream);
+    if (p->d_nodes) (void)hipFree(p->d_nodes);
+    if (p->d_lut) (void)hipFree(p->d_lut);
+    if (p->d_palette) (void)hipFree(p->d_palette);
+    if (p->d_scratch) (void)hipFree(p->d_scratch);
+    if (p->ev_start) (void)hipEventDestroy(p->ev_start);
+    if (p->ev_stop) (void)hipEventDestroy(p->ev_stop);
+    if (p->own_stream) (void)hipStreamDestroy(p->own_stream);
+    delete p;
+    return OCH_OK;
+}
+
+OCH_API int och_gpu_pool_info(const och_gpu_pool *p, och_pool_info *info)
+{
+    if (!p || !info) return fail(OCH_E_INVALID, "pool/info is NULL");
+    info->device_bytes = (uint64_t)p->n_nodes * 32;
+    info->n_nodes = p->n_nodes;
+    info->root = p->root;
+    info->depth = p->depth;
+    info->index_base = p->index_base;
+    info->miss_t = p->miss_t;
+    info->rcp_log2_entries = p->d_lut ? p->lut_log2 : 0;
+    info->device = p->device;
+    return OCH_OK;
+}
+
+OCH_API int och_gpu_pool_update(och_gpu_pool *p, uint32_t first, uint32_t count, const uint32_t *nodes, uint32_t root)
+{
+    if (!p || (count && !nodes)) return fail(OCH_E_INVALID, "pool/nodes is NULL");
+    const uint32_t n_user = p->n_nodes - (uint32_t)p->index_base;
+    const uint32_t lo = p->index_base == 1 ? 1u : 0u;
+    if (count && (first < lo || (uint64_t)first - lo + count > n_user))
+        return fail(OCH_E_INVALID, "update [%u, +%u) outside the pool", first, count);
+    // Apply to the host mirror and re-validate everything reachable from the
+    // new root before any byte reaches the device (h_octree::set keeps the
+    // pool consistent, ORT/och_h_octree.h:176-237; a bad edit must not fault).
+    const size_t off = (size_t)(first - lo) * 8;
+    std::vector<uint32_t> saved(p->mirror.begin() + off, p->mirror.begin() + off + (size_t)count * 8);
+    std::memcpy(p->mirror.data() + off, nodes, (size_t)count * 32);
+    const int st = validate_pool(p->mirror.data(), n_user, root, p->depth, p->index_base);
+    if (st != OCH_OK) {
+        std::memcpy(p->mirror.data() + off, saved.data(), saved.size() * 4);
+        return st;
+    }
+    DeviceGuard g(p->device);
+    if (count)
+        OCH_HIP(hipMemcpyAsync(p->d_nodes + 8 * (size_t)(first - lo + p->index_base), p->mirror.data() + off,
+                               (size_t)count * 32, hipMemcpyHostToDevice, p->stream()));
+    OCH_HIP(hipStreamSynchronize(p->stream()));
+    p->root = root;
+    return OCH_OK;
+}
+
+OCH_API int och_gpu_set_rcp_lut(och_gpu_pool *p, const uint32_t *lut, int log2_entries)
+{
+    if (!p) return fail(OCH_E_INVALID, "pool is NULL");
+    DeviceGuard g(p->device);
+    OCH_HIP(hipStreamSynchronize(p->stream()));
+    return upload_lut(p, lut, log2_entries);
+}
+
+OCH_API int och_gpu_set_palette(och_gpu_pool *p, const uint32_t *rgba, uint32_t n_voxels)
+{
+    if (!p || (n_voxels && !rgba)) return fail(OCH_E_INVALID, "pool/palette is NULL");
+    DeviceGuard g(p->device);
+    OCH_HIP(hipStreamSynchronize(p->stream()));
+    if (p->d_palette) OCH_HIP(hipFree(p->d_palette));
+    p->d_palette = nullptr;
+    p->n_voxels = 0;
+    if (!n_voxels) return OCH_OK;
+    OCH_HIP(hipMalloc(&p->d_palette, (size_t)n_voxels * 6 * 4));
+    OCH_HIP(hipMemcpy(p->d_palette, rgba, (size_t)n_voxels * 6 * 4, hipMemcpyHostToDevice));
+    p->n_voxels = n_voxels;
+    return OCH_OK;
+}
+
+OCH_API int och_gpu_set_stream(och_gpu_pool *p, void *stream)
+{
+    if (!p) return fail(OCH_E_INVALID, "pool is NULL");
+    p->ext_stream = (hipStream_t)stream;
+    return OCH_OK;
+}
+
+OCH_API int och_gpu_synchronize(och_gpu_pool *p)
+{
+    if (!p) return fail(OCH_E_INVALID, "pool is NULL");
+    DeviceGuard g(p->device);
+    OCH_HIP(hipStreamSynchronize(p->stream()));
+    return OCH_OK;
+}
+
+OCH_API int och_gpu_last_kernel_ms(och_gpu_pool *p, float *ms)
+{
+    if (!p || !ms) return fail(OCH_E_INVALID, "pool/ms is NULL");
+    if (!p->timed) return fail(OCH_E_INVALID, "no kernel has been launched on this pool");
+    DeviceGuard g(p->device);
+    OCH_HIP(hipEventSynchronize(p->ev_stop));
+    OCH_HIP(hipEventElapsedTime(ms, p->ev_start, p->ev_stop));
+    return OCH_OK;
+}
+
+OCH_API int och_gpu_trace_batch_dev(och_gpu_pool *p, const float *origin, int origin_stride, const float *dirs,
+                                    uint32_t n, int32_t *hit_dir, uint32_t *hit_voxel, float *hit_time,
+                                    uint32_t *push_count)
+{
+    if (!p || (n && (!origin || !dirs || !hit_dir || !hit_voxel || !hit_time)))
+        return fail(OCH_E_INVALID, "NULL argument");
+    if (origin_stride != 0 && origin_stride != 3) return fail(OCH_E_INVALID, "origin_stride must be 0 or 3");
+    if (!p->d_lut) return fail(OCH_E_RCP_MODEL, "no RCPPS table on this pool (call och_gpu_set_rcp_lut)");
+    DeviceGuard g(p->device);
+    OCH_HIP(hipEventRecord(p->ev_start, p->stream()));
+    OCH_HIP(och::launch_trace_batch(p->dev(), origin, origin_stride, dirs, n, hit_dir, hit_voxel,
+                                    reinterpret_cast<uint32_t *>(hit_time), push_count, p->stream()));
+    OCH_HIP(hipEventRecord(p->ev_stop, p->stream()));
+    p->timed = true;
+    return OCH_OK;
+}
+
+OCH_API int och_gpu_trace_batch(och_gpu_pool *p, const float *origin, int origin_stride, const float *dirs,
+                                uint32_t n, int32_t *hit_dir, uint32_t *hit_voxel, float *hit_time)
+{
+    if (!p || (n && (!origin || !dirs || !hit_dir || !hit_voxel || !hit_time)))
+        return fail(OCH_E_INVALID, "NULL argument");
+    if (origin_stride != 0 && origin_stride != 3) return fail(OCH_E_INVALID, "origin_stride must be 0 or 3");
+    if (n == 0) return OCH_OK;
+    DeviceGuard g(p->device);
+    const size_t n_orig = origin_stride ? (size_t)n * 3 : 3;
+    const size_t b_orig = (n_orig * 4 + 255) & ~(size_t)255;
+    const size_t b_dirs = ((size_t)n * 12 + 255) & ~(size_t)255;
+    const size_t b_out = ((size_t)n * 4 + 255) & ~(size_t)255;
+    int st = ensure_scratch(p, b_orig + b_dirs + 3 * b_out);
+    if (st != OCH_OK) return st;
+    char *base = static_cast<char *>(p->d_scratch);
+    float *d_orig = reinterpret_cast<float *>(base);
+    float *d_dirs = reinterpret_cast<float *>(base + b_orig);
+    int32_t *d_dir = reinterpret_cast<int32_t *>(base + b_orig + b_dirs);
+    uint32_t *d_vox = reinterpret_cast<uint32_t *>(base + b_orig + b_dirs + b_out);
+    float *d_t = reinterpret_cast<float *>(base + b_orig + b_dirs + 2 * b_out);
+    hipStream_t s = p->stream();
+    OCH_HIP(hipMemcpyAsync(d_orig, origin, n_orig * 4, hipMemcpyHostToDevice, s));
+    OCH_HIP(hipMemcpyAsync(d_dirs, dirs, (size_t)n * 12, hipMemcpyHostToDevice, s));
+    st = och_gpu_trace_batch_dev(p, d_orig, origin_stride, d_dirs, n, d_dir, d_vox, d_t, nullptr);
+    if (st != OCH_OK) return st;
+    OCH_HIP(hipMemcpyAsync(hit_dir, d_dir, (size_t)n * 4, hipMemcpyDeviceToHost, s));
+    OCH_HIP(hipMemcpyAsync(hit_voxel, d_vox, (size_t)n * 4, hipMemcpyDeviceToHost, s));
+    OCH_HIP(hipMemcpyAsync(hit_time, d_t, (size_t)n * 4, hipMemcpyDeviceToHost, s));
+    OCH_HIP(hipStreamSynchronize(s));
+    return OCH_OK;
+}
+
+OCH_API int och_gpu_trace(och_gpu_pool *p, float ox, float oy, float oz, float dx, float dy, float dz,
+                          int32_t *hit_direction, uint32_t *hit_voxel, float *hit_time)
+{
+    if (!hit_direction || !hit_voxel || !hit_time) return fail(OCH_E_INVALID, "NULL output");
+    const float o[3] = {ox, oy, oz}, d[3] = {dx, dy, dz};
+    return och_gpu_trace_batch(p, o, 0, d, 1, hit_direction, hit_voxel, hit_time);
+}
+
+OCH_API int och_camera_setup(float px, float py, float pz, float yaw, float pitch, float fov, int width, int height,
+                             och_camera *cam)
+{
+    if (!cam || width <= 0 || height <= 0) return fail(OCH_E_INVALID, "bad camera arguments");
+    // ORT/test_och_h_octree.cpp:89-115, evaluated in float exactly as written.
+    cam->pos[0] = px;
+    cam->pos[1] = py;
+    cam->pos[2] = pz;
+    cam->aspect = (float)width / (float)height;
+    cam->view_x = 2.0F / (float)width;
+    cam->view_y = 2.0F / (float)height;
+    cam->fov_factor = 1 / tanf(fov / 2);
+    const float sin_a = 0, cos_a = 1;
+    const float sin_b = sinf(yaw), cos_b = cosf(yaw);
+    const float sin_c = sinf(pitch), cos_c = cosf(pitch);
+    cam->rot[0] = cos_a * cos_b;
+    cam->rot[1] = cos_a * sin_b * sin_c - sin_a * cos_c;
+    cam->rot[2] = cos_a * sin_b * cos_c + sin_a * sin_c;
+    cam->rot[3] = sin_a * cos_b;
+    cam->rot[4] = sin_a * sin_b * sin_c + cos_a * cos_c;
+    cam->rot[5] = sin_a * sin_b * cos_c - cos_a * sin_c;
+    cam->rot[6] = -sin_b;
+    cam->rot[7] = cos_b * sin_c;
+    cam->rot[8] = cos_b * cos_c;
+    cam->width = width;
+    cam->height = height;
+    return OCH_OK;
+}
+
+OCH_API int och_gpu_raygen_dev(och_gpu_pool *p, const och_camera *cam, float *dirs)
+{
+    if (!p || !cam || !dirs) return fail(OCH_E_INVALID, "NULL argument");
+    DeviceGuard g(p->device);
+    OCH_HIP(och::launch_raygen(*cam, dirs, p->stream()));
+    return OCH_OK;
+}
+
+OCH_API int och_shard_rows(int height, int row_chunk, int n_shards)
+{
+    if (height <= 0 || row_chunk <= 0 || n_shards <= 0) return 0;
+    const int chunks = (height + row_chunk - 1) / row_chunk;
+    return ((chunks + n_shards - 1) / n_shards) * row_chunk;
+}
+
+OCH_API int och_gpu_render_dev(och_gpu_pool *p, const och_camera *cam, uint32_t *rgba_slice, int row_chunk, int shard,
+                               int n_shards)
+{
+    if (!p || !cam || !rgba_slice) return fail(OCH_E_INVALID, "NULL argument");
+    if (row_chunk <= 0 || n_shards <= 0 || shard < 0 || shard >= n_shards)
+        return fail(OCH_E_INVALID, "bad sharding (%d, %d, %d)", row_chunk, shard, n_shards);
+    if (!p->d_lut) return fail(OCH_E_RCP_MODEL, "no RCPPS table on this pool (call och_gpu_set_rcp_lut)");
+    DeviceGuard g(p->device);
+    och::DevFrame f;
+    f.cam = *cam;
+    f.palette = p->d_palette;
+    f.n_voxels = p->n_voxels;
+    f.out = rgba_slice;
+    f.row_chunk = row_chunk;
+    f.shard = shard;
+    f.n_shards = n_shards;
+    f.slice_rows = och_shard_rows(cam->height, row_chunk, n_shards);
+    OCH_HIP(hipEventRecord(p->ev_start, p->stream()));
+    OCH_HIP(och::launch_render(p->dev(), f, p->stream()));
+    OCH_HIP(hipEventRecord(p->ev_stop, p->stream()));
+    p->timed = true;
+    return OCH_OK;
+}
+
+OCH_API int och_gpu_unshard_dev(och_gpu_pool *p, const uint32_t *gathered, uint32_t *frame, int width, int height,
+                                int row_chunk, int n_shards)
+{
+    if (!p || !gathered || !frame || width <= 0 || height <= 0 || row_chunk <= 0 || n_shards <= 0)
+        return fail(OCH_E_INVALID, "bad unshard arguments");
+    DeviceGuard g(p->device);
+    OCH_HIP(och::launch_unshard(gathered, frame, width, height, row_chunk, n_shards,
+                                och_shard_rows(height, row_chunk, n_shards), p->stream()));
+    return OCH_OK;
+}
+
+OCH_API int och_gpu_render(och_gpu_pool *p, const och_camera *cam, uint32_t *rgba)
+{
+    if (!p || !cam || !rgba) return fail(OCH_E_INVALID, "NULL argument");
+    DeviceGuard g(p->device);
+    const size_t bytes = (size_t)cam->width * cam->height * 4;
+    int st = ensure_scratch(p, bytes);
+    if (st != OCH_OK) return st;
+    st = och_gpu_render_dev(p, cam, static_cast<uint32_t *>(p->d_scratch), cam->height, 0, 1);
+    if (st != OCH_OK) return st;
+    OCH_HIP(hipMemcpyAsync(rgba, p->d_scratch, bytes, hipMemcpyDeviceToHost, p->stream()));
+    OCH_HIP(hipStreamSynchronize(p->stream()));
+    return OCH_OK;
+}
+
+OCH_API uint32_t och_pool_at(const uint32_t *nodes, uint32_t root, int depth, int index_base, int x, int y, int z)
+{
+    // h_octree::at (ORT/och_h_octree.h:239-258) with the child digit of z_encode_16.
+    if (!nodes || (index_base == 1 && root == 0)) return 0;
+    uint32_t cur = root;
+    for (int l = depth - 1; l >= 0; --l) {
+        const int c = ((x >> l) & 1) | (((y >> l) & 1) << 1) | (((z >> l) & 1) << 2);
+        const uint32_t nx = nodes[(size_t)(cur - index_base) * 8 + c];
+        if (l == 0 || !nx) return nx;
+        cur = nx;
+    }
+    return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,77 @@
+"""Multi-GPU frames: row-chunk sharding + all-gather of the RGBA8 framebuffer.
+
+The reference renders one frame on one core (ORT/test_och_h_octree.cpp:448-450).
+Here each rank (one process per GPU, torch.distributed over RCCL/xGMI) renders
+the rows dealt to it -- chunks of `row_chunk` rows round-robin over ranks, so
+sky and terrain cost is balanced -- into a compact slice, then one all-gather
+assembles the slices and a tiny device kernel restores row order.  The node
+pool is replicated (read-only, uploaded once per rank); the only data-path
+collective is the framebuffer exchange.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from .tracer import GpuPool, shard_rows
+
+
+def slice_row_map(height: int, row_chunk: int, n_shards: int, shard: int) -> np.ndarray:
+    """Global row of each row of `shard`'s compact slice (-1 = padding)."""
+    rows = shard_rows(height, row_chunk, n_shards)
+    local = np.arange(rows)
+    gchunk = (local // row_chunk) * n_shards + shard
+    g = gchunk * row_chunk + local % row_chunk
+    return np.where(g < height, g, -1)
+
+
+def unshard_host(gathered: np.ndarray, height: int, row_chunk: int) -> np.ndarray:
+    """Host restatement of the unshard kernel: (n, rows, W) slices -> (H, W) frame."""
+    n, rows, width = gathered.shape
+    frame = np.zeros((height, width), gathered.dtype)
+    for s in range(n):
+        m = slice_row_map(height, row_chunk, n, s)
+        ok = m >= 0
+        frame[m[ok]] = gathered[s][ok]
+    return frame
+
+
+class ShardedFrame:
+    """Renders frames across the ranks of the default process group.
+
+    pool: this rank's GpuPool (same tree on every rank).  The all-gather runs
+    on the current torch stream, which the pool is bound to, so render ->
+    all-gather -> unshard are ordered without host synchronisation.
+    """
+
+    def __init__(self, pool: GpuPool, width: int, height: int, row_chunk: int = 8, group=None):
+        import torch
+        import torch.distributed as dist
+
+        self.pool, self.width, self.height, self.row_chunk = pool, width, height, row_chunk
+        self.group = group
+        self.rank = dist.get_rank(group) if dist.is_initialized() else 0
+        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.rows = shard_rows(height, row_chunk, self.world)
+        dev = torch.device("cuda", torch.cuda.current_device())
+        self.slice = torch.empty((self.rows, width), dtype=torch.int32, device=dev)
+        self.gathered = torch.empty((self.world, self.rows, width), dtype=torch.int32, device=dev)
+        self.frame = torch.empty((height, width), dtype=torch.int32, device=dev)
+        pool.set_stream(torch.cuda.current_stream())
+
+    def render_local(self, cam):
+        self.pool.render_dev(cam, self.slice, self.row_chunk, self.rank, self.world)
+        return self.slice
+
+    def exchange(self):
+        import torch.distributed as dist
+
+        if self.world > 1:
+            dist.all_gather_into_tensor(self.gathered, self.slice, group=self.group)
+            self.pool.unshard_dev(self.gathered, self.frame, self.width, self.height, self.row_chunk, self.world)
+        else:
+            self.pool.unshard_dev(self.slice, self.frame, self.width, self.height, self.row_chunk, 1)
+        return self.frame
+
+    def render(self, cam):
+        self.render_local(cam)
+        return self.exchange()

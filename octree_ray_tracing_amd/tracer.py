@@ -1,0 +1,216 @@
+"""Host-side mirror of the reference's tracer interface over the C ABI.
+
+Reference (ORT/ = Octree_Ray_Tracing/):
+  och::h_octree<L, D>::sse_trace(ox, oy, oz, dx, dy, dz, dir&, voxel&, t&)   ORT/och_h_octree.h:292-452
+  och::octree::sse_trace(...)                                              ORT/och_octree.cpp:167-325
+  tree_camera::update_position / trace_pixel                               ORT/test_och_h_octree.cpp:64-138
+  tree_window::update_image                                                ORT/test_och_h_octree.cpp:437-457
+
+`HOctree` / `Octree` wrap a device-resident node pool (`och_gpu_pool`).  Every
+compute call runs the gfx950 kernels in liboch_gpu.so; nothing here computes
+a hit on the CPU.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import enum
+import math
+
+import numpy as np
+
+from . import _lib
+from ._lib import Camera, OchError, call
+
+
+class Direction(enum.IntEnum):
+    """och::direction (ORT/och_tree_helper.h:7-18)."""
+    x_pos = 0
+    y_pos = 1
+    z_pos = 2
+    x_neg = 3
+    y_neg = 4
+    z_neg = 5
+    exit = 6
+    inside = 7
+    error = 8
+
+
+def _np_ptr(a: np.ndarray) -> int:
+    return a.ctypes.data
+
+
+def _dev_ptr(t) -> int:
+    """Device pointer of a torch tensor (or an int already)."""
+    if isinstance(t, int):
+        return t
+    if not t.is_cuda:
+        raise ValueError("expected a device tensor")
+    if not t.is_contiguous():
+        raise ValueError("expected a contiguous tensor")
+    return t.data_ptr()
+
+
+def host_rcp_lut() -> np.ndarray:
+    """This host's RCPPS (_mm_rcp_ps, ORT/och_h_octree.h:316) as a 2^k table."""
+    buf = np.empty(1 << 23, np.uint32)
+    k = C.c_int()
+    call("och_host_rcp_lut", _np_ptr(buf), C.byref(k))
+    return buf[: 1 << k.value].copy()
+
+
+def rcp_from_lut(xbits: int, lut: np.ndarray) -> int:
+    lut = np.ascontiguousarray(lut, np.uint32)
+    return call("och_rcp_from_lut", xbits, _np_ptr(lut), int(round(math.log2(lut.size))))
+
+
+def device_count() -> int:
+    n = C.c_int()
+    call("och_device_count", C.byref(n))
+    return n.value
+
+
+def camera(pos=(1.5, 1.5, 1.5), yaw: float = 0.0, pitch: float = 0.0, fov: float = 1.25,
+           width: int = 640, height: int = 360) -> Camera:
+    """tree_camera state -> per-frame uniforms (ORT/test_och_h_octree.cpp:53-55, :87-115).
+    yaw = camera.dir.x, pitch = camera.dir.y."""
+    cam = Camera()
+    call("och_camera_setup", float(pos[0]), float(pos[1]), float(pos[2]), float(yaw), float(pitch),
+         float(fov), int(width), int(height), C.byref(cam))
+    return cam
+
+
+class GpuPool:
+    """A node pool resident in HBM on one device, traced by the gfx950 kernels."""
+
+    def __init__(self, nodes: np.ndarray, root: int, depth: int, index_base: int = 1,
+                 miss_t: float | None = None, device: int = -1):
+        nodes = np.ascontiguousarray(nodes, dtype=np.uint32).reshape(-1, 8)
+        if miss_t is None:
+            miss_t = math.inf if index_base == 1 else 0.0
+        self.depth, self.index_base, self.miss_t = int(depth), int(index_base), float(miss_t)
+        self._h = C.c_void_p()
+        call("och_gpu_pool_create", _np_ptr(nodes), nodes.shape[0], int(root), int(depth),
+             int(index_base), float(miss_t), int(device), C.byref(self._h))
+        self._palette_n = 0
+
+    # -- lifetime
+    def close(self):
+        if getattr(self, "_h", None) and self._h.value:
+            call("och_gpu_pool_destroy", self._h)
+            self._h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    # -- configuration
+    def info(self) -> dict:
+        inf = _lib.PoolInfo()
+        call("och_gpu_pool_info", self._h, C.byref(inf))
+        return {f: getattr(inf, f) for f, _ in _lib.PoolInfo._fields_}
+
+    def get_root(self) -> int:
+        return self.info()["root"]
+
+    def set_rcp_lut(self, lut: np.ndarray):
+        lut = np.ascontiguousarray(lut, np.uint32)
+        call("och_gpu_set_rcp_lut", self._h, _np_ptr(lut), int(round(math.log2(lut.size))))
+
+    def set_palette(self, rgba: np.ndarray):
+        rgba = np.ascontiguousarray(rgba, np.uint32).reshape(-1)
+        if rgba.size % 6:
+            raise ValueError("palette must hold 6 colours per voxel id")
+        call("och_gpu_set_palette", self._h, _np_ptr(rgba), rgba.size // 6)
+        self._palette_n = rgba.size // 6
+
+    def set_stream(self, stream):
+        """Enqueue _dev work on a caller stream (torch.cuda.Stream or raw handle)."""
+        handle = getattr(stream, "cuda_stream", stream)
+        call("och_gpu_set_stream", self._h, C.c_void_p(handle))
+
+    def update(self, first: int, nodes: np.ndarray, root: int):
+        nodes = np.ascontiguousarray(nodes, np.uint32).reshape(-1, 8)
+        call("och_gpu_pool_update", self._h, int(first), nodes.shape[0], _np_ptr(nodes), int(root))
+
+    def synchronize(self):
+        call("och_gpu_synchronize", self._h)
+
+    def last_kernel_ms(self) -> float:
+        ms = C.c_float()
+        call("och_gpu_last_kernel_ms", self._h, C.byref(ms))
+        return ms.value
+
+    # -- tracing (reference signature)
+    def sse_trace(self, ox, oy, oz, dx, dy, dz):
+        """h_octree::sse_trace: returns (Direction, voxel, t)."""
+        d, v, t = C.c_int32(), C.c_uint32(), C.c_float()
+        call("och_gpu_trace", self._h, float(ox), float(oy), float(oz), float(dx), float(dy), float(dz),
+             C.byref(d), C.byref(v), C.byref(t))
+        return Direction(d.value), v.value, t.value
+
+    def trace_batch(self, origins, dirs):
+        """Host arrays in, host arrays out (synchronous).  origins (3,) or (n,3)."""
+        dirs = np.ascontiguousarray(dirs, np.float32).reshape(-1, 3)
+        origins = np.ascontiguousarray(origins, np.float32)
+        stride = 0 if origins.size == 3 else 3
+        n = dirs.shape[0]
+        hd, hv, ht = np.empty(n, np.int32), np.empty(n, np.uint32), np.empty(n, np.float32)
+        call("och_gpu_trace_batch", self._h, _np_ptr(origins), stride, _np_ptr(dirs), n,
+             _np_ptr(hd), _np_ptr(hv), _np_ptr(ht))
+        return hd, hv, ht
+
+    def trace_batch_dev(self, origins, dirs, hit_dir, hit_voxel, hit_time, push=None, n=None):
+        """Device buffers (torch tensors), asynchronous on the pool's stream."""
+        if n is None:
+            n = dirs.numel() // 3
+        stride = 0 if origins.numel() == 3 else 3
+        call("och_gpu_trace_batch_dev", self._h, _dev_ptr(origins), stride, _dev_ptr(dirs), int(n),
+             _dev_ptr(hit_dir), _dev_ptr(hit_voxel), _dev_ptr(hit_time),
+             None if push is None else _dev_ptr(push))
+
+    # -- frame path
+    def raygen_dev(self, cam: Camera, dirs):
+        call("och_gpu_raygen_dev", self._h, C.byref(cam), _dev_ptr(dirs))
+
+    def render(self, cam: Camera) -> np.ndarray:
+        """update_position + update_image: RGBA8 (olc::Pixel) frame, H x W uint32."""
+        out = np.empty((cam.height, cam.width), np.uint32)
+        call("och_gpu_render", self._h, C.byref(cam), _np_ptr(out))
+        return out
+
+    def render_dev(self, cam: Camera, rgba_slice, row_chunk: int | None = None, shard: int = 0,
+                   n_shards: int = 1):
+        if row_chunk is None:
+            row_chunk = cam.height
+        call("och_gpu_render_dev", self._h, C.byref(cam), _dev_ptr(rgba_slice), int(row_chunk),
+             int(shard), int(n_shards))
+
+    def unshard_dev(self, gathered, frame, width: int, height: int, row_chunk: int, n_shards: int):
+        call("och_gpu_unshard_dev", self._h, _dev_ptr(gathered), _dev_ptr(frame), int(width), int(height),
+             int(row_chunk), int(n_shards))
+
+
+def shard_rows(height: int, row_chunk: int, n_shards: int) -> int:
+    return call("och_shard_rows", int(height), int(row_chunk), int(n_shards))
+
+
+class HOctree(GpuPool):
+    """och::h_octree's table on the GPU: 1-based, miss t = +INF (ORT/och_h_octree.h:429)."""
+
+    def __init__(self, nodes, root, depth, device: int = -1):
+        super().__init__(nodes, root, depth, index_base=1, miss_t=math.inf, device=device)
+
+
+class Octree(GpuPool):
+    """och::octree's table on the GPU: 0-based, root 0, miss t = 0 (ORT/och_octree.cpp:302)."""
+
+    def __init__(self, nodes, depth, device: int = -1):
+        super().__init__(nodes, 0, depth, index_base=0, miss_t=0.0, device=device)

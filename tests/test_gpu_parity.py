@@ -1,0 +1,250 @@
+"""GPU parity: the gfx950 kernels (through the C ABI) vs the CPU oracle, bit for bit.
+
+Hit records (direction, voxel id, t bit pattern) and PUSH counts must be
+identical.  Two RCPPS regimes: the committed Intel table (golden vectors made
+in the build container) and this host's own RCPPS (oracle in native mode vs
+GPU with the table captured from the same host)."""
+import math
+
+import numpy as np
+import pytest
+
+from conftest import GOLD
+
+pytestmark = pytest.mark.gpu
+
+ORIGIN = np.array([1.5, 1.5, 1.5], np.float32)
+
+
+def gpu_trace_dev(pool, origins, dirs, want_push=True):
+    import torch
+    dev = torch.device("cuda", 0)
+    dirs = np.ascontiguousarray(dirs, np.float32).reshape(-1, 3)
+    n = dirs.shape[0]
+    o = torch.from_numpy(np.ascontiguousarray(origins, np.float32).reshape(-1)).to(dev)
+    d = torch.from_numpy(dirs.reshape(-1)).to(dev)
+    hd = torch.empty(n, dtype=torch.int32, device=dev)
+    hv = torch.empty(n, dtype=torch.int32, device=dev)
+    ht = torch.empty(n, dtype=torch.float32, device=dev)
+    hp = torch.empty(n, dtype=torch.int32, device=dev) if want_push else None
+    pool.set_stream(torch.cuda.current_stream())
+    pool.trace_batch_dev(o, d, hd, hv, ht, hp, n=n)
+    torch.cuda.synchronize()
+    out = {"dir": hd.cpu().numpy(), "voxel": hv.cpu().numpy().view(np.uint32),
+           "t": ht.cpu().numpy().view(np.uint32)}
+    if want_push:
+        out["push"] = hp.cpu().numpy().view(np.uint32)
+    return out
+
+
+def assert_same(gpu, ref, push=True):
+    assert np.array_equal(gpu["dir"], ref["dir"]), _first_diff(gpu["dir"], ref["dir"])
+    assert np.array_equal(gpu["voxel"], ref["voxel"].view(np.uint32))
+    assert np.array_equal(np.asarray(gpu["t"]).view(np.uint32), np.asarray(ref["t"]).view(np.uint32))
+    if push and "push" in gpu and ref.get("push") is not None:
+        assert np.array_equal(gpu["push"], ref["push"])
+
+
+def _first_diff(a, b):
+    i = np.nonzero(a != b)[0]
+    return f"{i.size} mismatches, first at {i[:5]}: {a[i[:5]]} vs {b[i[:5]]}"
+
+
+@pytest.fixture(scope="module")
+def golden():
+    return np.load(GOLD / "trace_d6.npz")
+
+
+def test_golden_vectors_intel_table(ort, gpu_device, golden, intel_lut):
+    pool = ort.HOctree(golden["nodes"], int(golden["root"]), int(golden["depth"]), device=0)
+    pool.set_rcp_lut(intel_lut)
+    for name in ("cam", "rnd", "edge"):
+        want = {"dir": golden[f"{name}_dir"], "voxel": golden[f"{name}_vox"], "t": golden[f"{name}_t"],
+                "push": golden[f"{name}_push"]}
+        assert_same(gpu_trace_dev(pool, golden[f"{name}_o"], golden[f"{name}_d"]), want)
+        hd, hv, ht = pool.trace_batch(golden[f"{name}_o"], golden[f"{name}_d"])
+        assert_same({"dir": hd, "voxel": hv, "t": ht}, want, push=False)
+    pool.close()
+
+
+def test_zero_direction_quirk_reference_table(ort, O, gpu_device, known, intel_lut):
+    """SURVEY §7 known answer, traced on the reference's own hash-table layout."""
+    k = known["zero_direction_quirk"]
+    T = O.HRef(k["depth"], 10)
+    for x, y, z, v in k["voxels"]:
+        T.set(x, y, z, v)
+    pool = ort.HOctree(T.nodes(), T.root, k["depth"], device=0)
+    pool.set_rcp_lut(intel_lut)
+    for case in k["cases"]:
+        d, v, t = pool.sse_trace(*k["origin"], *case["dir"])
+        assert (int(d), v) == (case["direction"], case["voxel"])
+        assert float(np.float32(t)) == float.fromhex(case["t_hex"])
+    pool.close()
+
+
+@pytest.mark.parametrize("depth", [8, 10])
+def test_camera_frames_host_rcpps(ort, O, gpu_device, depth):
+    """Full 1920x1080 frames, both survey pitches, vs the oracle using this host's RCPPS."""
+    tree = ort.build_terrain(depth)
+    pool = ort.HOctree(tree.nodes, tree.root, depth, device=0)
+    ref_pool = O.OraclePool(tree.nodes, tree.root, depth, 1)
+    for pitch in (0.0, -0.6):
+        rays = O.raygen(0.3, pitch, 1.25, 1920, 1080)
+        ref = O.trace_batch(ref_pool, O.Rcp(None), ORIGIN, rays, nthreads=16, want_push=True)
+        assert_same(gpu_trace_dev(pool, ORIGIN, rays), ref)
+    pool.close()
+
+
+def test_reference_hash_table_layout(ort, O, gpu_device):
+    """The reference's table->nodes (1-based, hash-scattered, gravestones) uploaded as-is."""
+    T = O.HRef(8, 19)
+    T.fill_terrain()
+    nodes = T.nodes()
+    pool = ort.HOctree(nodes, T.root, 8, device=0)
+    rng = np.random.default_rng(9)
+    o = rng.uniform(1.01, 1.99, (100000, 3)).astype(np.float32)
+    d = rng.uniform(-1, 1, (100000, 3)).astype(np.float32)
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    ref = O.trace_batch(T.pool(), O.Rcp(None), o, d, nthreads=16, want_push=True)
+    assert_same(gpu_trace_dev(pool, o, d), ref)
+    rays = O.raygen(0.3, -0.6, 1.25, 640, 360)
+    assert_same(gpu_trace_dev(pool, ORIGIN, rays), O.trace_batch(T.pool(), O.Rcp(None), ORIGIN, rays, want_push=True))
+    pool.close()
+
+
+def test_octree_variant(ort, O, gpu_device):
+    """och::octree: 0-based pool, root 0, miss t = 0.0F (ORT/och_octree.cpp:302)."""
+    tree = ort.build_terrain(8, dedup=False)
+    pool = ort.Octree(tree.nodes, 8, device=0)
+    ref_pool = O.OraclePool(tree.nodes, 0, 8, 0)
+    rays = O.raygen(0.3, 0.0, 1.25, 512, 512)
+    ref = O.trace_batch(ref_pool, O.Rcp(None), ORIGIN, rays, want_push=True)
+    got = gpu_trace_dev(pool, ORIGIN, rays)
+    assert_same(got, ref)
+    assert np.all(got["t"][got["dir"] == 6] == 0)
+    pool.close()
+
+
+def test_random_and_edge_rays_d10(ort, O, gpu_device):
+    import sys
+    sys.path.insert(0, str(GOLD.parent))
+    from make_golden import edge_rays
+    tree = ort.build_terrain(10)
+    pool = ort.HOctree(tree.nodes, tree.root, 10, device=0)
+    ref_pool = O.OraclePool(tree.nodes, tree.root, 10, 1)
+    rng = np.random.default_rng(1)
+    o = rng.uniform(1.01, 1.99, (200000, 3)).astype(np.float32)
+    d = rng.uniform(-1, 1, (200000, 3)).astype(np.float32)
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    assert_same(gpu_trace_dev(pool, o, d), O.trace_batch(ref_pool, O.Rcp(None), o, d, nthreads=16, want_push=True))
+    eo, ed = edge_rays()
+    assert_same(gpu_trace_dev(pool, eo, ed), O.trace_batch(ref_pool, O.Rcp(None), eo, ed, want_push=True))
+    # unnormalised and tiny / huge directions
+    d2 = d[:50000] * rng.choice(np.array([1e-20, 1e-5, 3.0, 1e20], np.float32), (50000, 1))
+    assert_same(gpu_trace_dev(pool, o[:50000], d2), O.trace_batch(ref_pool, O.Rcp(None), o[:50000], d2, want_push=True))
+    pool.close()
+
+
+@pytest.mark.parametrize("W,H,pitch", [(1920, 1080, 0.0), (1920, 1080, -0.6), (641, 359, 0.4), (64, 36, -1.2)])
+def test_raygen_bit_exact(ort, O, gpu_device, W, H, pitch):
+    import torch
+    tree = ort.build_terrain(4)
+    pool = ort.HOctree(tree.nodes, tree.root, 4, device=0)
+    pool.set_stream(torch.cuda.current_stream())
+    cam = ort.camera((1.5, 1.5, 1.5), 0.3, pitch, 1.25, W, H)
+    dirs = torch.empty(W * H * 3, dtype=torch.float32, device="cuda")
+    pool.raygen_dev(cam, dirs)
+    torch.cuda.synchronize()
+    got = dirs.cpu().numpy().reshape(-1, 3)
+    want = O.raygen(0.3, pitch, 1.25, W, H)
+    assert np.array_equal(got.view(np.uint32), want.view(np.uint32))
+    pool.close()
+
+
+def test_render_frame_and_shards(ort, O, gpu_device):
+    import torch
+    tree = ort.build_terrain(9)
+    pal = ort.VoxelData().get_colours()
+    pool = ort.HOctree(tree.nodes, tree.root, 9, device=0)
+    pool.set_palette(pal)
+    W, H = 800, 450
+    cam = ort.camera((1.5, 1.5, 1.5), 0.3, -0.6, 1.25, W, H)
+    frame = pool.render(cam)
+    rays = O.raygen(0.3, -0.6, 1.25, W, H)
+    r = O.trace_batch(O.OraclePool(tree.nodes, tree.root, 9, 1), O.Rcp(None), ORIGIN, rays, nthreads=16)
+    want = O.shade(r["dir"], r["voxel"], pal).reshape(H, W)
+    assert np.array_equal(frame, want)
+    # sharded: 3 shards of 8-row chunks, gathered and unsharded on the device
+    pool.set_stream(torch.cuda.current_stream())
+    n, chunk = 3, 8
+    rows = ort.shard_rows(H, chunk, n)
+    gathered = torch.zeros((n, rows, W), dtype=torch.int32, device="cuda")
+    for s in range(n):
+        pool.render_dev(cam, gathered[s], chunk, s, n)
+    full = torch.empty((H, W), dtype=torch.int32, device="cuda")
+    pool.unshard_dev(gathered, full, W, H, chunk, n)
+    torch.cuda.synchronize()
+    assert np.array_equal(full.cpu().numpy().view(np.uint32), want)
+    pool.close()
+
+
+def test_empty_tree_renders_sky(ort, gpu_device):
+    pool = ort.HOctree(np.zeros((4, 8), np.uint32), 0, 5, device=0)
+    pool.set_palette(ort.VoxelData().get_colours())
+    frame = pool.render(ort.camera(width=32, height=16))
+    assert np.all(frame == 0xFFFEBF00)
+    d, v, t = pool.sse_trace(1.5, 1.5, 1.5, 0.3, 0.2, -0.9)
+    assert (int(d), v) == (6, 0) and math.isinf(t)
+    pool.close()
+
+
+def test_pool_update_after_edits(ort, O, gpu_device):
+    """h_octree::set path copies (ORT/och_h_octree.h:176-237) uploaded incrementally."""
+    T = O.HRef(7, 16)
+    T.fill_terrain()
+    before = T.nodes()
+    pool = ort.HOctree(before, T.root, 7, device=0)
+    rng = np.random.default_rng(4)
+    for x, y, z in rng.integers(30, 90, (300, 3)).tolist():      # dig and build
+        T.set(x, y, z, 0 if (x + y) % 2 else 3)
+    after = T.nodes()
+    changed = np.nonzero(np.any(before != after, axis=1))[0]
+    lo, hi = int(changed.min()), int(changed.max())
+    pool.update(lo + 1, after[lo:hi + 1], T.root)
+    rays = O.raygen(0.1, -0.3, 1.25, 320, 180)
+    ref = O.trace_batch(T.pool(), O.Rcp(None), ORIGIN, rays, want_push=True)
+    assert_same(gpu_trace_dev(pool, ORIGIN, rays), ref)
+    # an edit that would make a kernel read outside the pool is refused
+    bad = after[lo:lo + 1].copy()
+    bad[0, :] = before.shape[0] + 50
+    with pytest.raises(ort.OchError):
+        pool.update(lo + 1, bad, T.root)
+    assert_same(gpu_trace_dev(pool, ORIGIN, rays), ref)
+    pool.close()
+
+
+def test_error_paths(ort, gpu_device):
+    tree = ort.build_terrain(4)
+    pool = ort.HOctree(tree.nodes, tree.root, 4, device=0)
+    with pytest.raises(ort.OchError):
+        pool.set_rcp_lut(np.zeros(3, np.uint32))
+    with pytest.raises(ValueError):
+        pool.set_palette(np.zeros(5, np.uint32))
+    import ctypes as C
+    from octree_ray_tracing_amd._lib import call
+    with pytest.raises(ort.OchError):
+        call("och_gpu_trace_batch", pool._h, None, 2, None, 1, None, None, None)
+    pool.close()
+
+
+@pytest.mark.slow
+def test_depth12_camera_frame(ort, O, gpu_device):
+    """BASELINE config 3: depth-12 terrain, 1920x1080, both pitches, full-frame parity."""
+    tree = ort.build_terrain(12)
+    pool = ort.HOctree(tree.nodes, tree.root, 12, device=0)
+    ref_pool = O.OraclePool(tree.nodes, tree.root, 12, 1)
+    for pitch in (0.0, -0.6):
+        rays = O.raygen(0.3, pitch, 1.25, 1920, 1080)
+        ref = O.trace_batch(ref_pool, O.Rcp(None), ORIGIN, rays, nthreads=16, want_push=True)
+        assert_same(gpu_trace_dev(pool, ORIGIN, rays), ref)
+    pool.close()
