@@ -119,7 +119,9 @@ OCH_API int och_gpu_set_rcp_lut(och_gpu_pool *pool, const uint32_t *lut, int log
 /* Palette: n_voxels x 6 RGBA8 colours (olc::Pixel layout, r in the low byte),
  * ordered x_pos..z_neg per voxel id 1..n (ORT/och_voxel.cpp:195-305). */
 OCH_API int och_gpu_set_palette(och_gpu_pool *pool, const uint32_t *rgba, uint32_t n_voxels);
-/* Use a caller-owned HIP stream (hipStream_t) for all _dev calls; NULL = the pool's own. */
+/* Enqueue all later work on a caller-owned HIP stream (hipStream_t); NULL is
+ * HIP's null stream (torch's default stream).  Until called, the pool uses a
+ * non-blocking stream of its own. */
 OCH_API int och_gpu_set_stream(och_gpu_pool *pool, void *hip_stream);
 OCH_API int och_gpu_synchronize(och_gpu_pool *pool);
 /* Duration of the most recent trace/render kernel launched on the pool,

@@ -126,6 +126,7 @@ struct och_gpu_pool {
     uint32_t n_voxels = 0;
     hipStream_t own_stream = nullptr;
     hipStream_t ext_stream = nullptr;
+    bool use_ext = false;           // och_gpu_set_stream called: ext_stream (NULL = null stream)
     hipEvent_t ev_start = nullptr, ev_stop = nullptr;
     bool timed = false;
     // host mirror of the uploaded nodes (user numbering), for validating edits
@@ -134,7 +135,7 @@ struct och_gpu_pool {
     void *d_scratch = nullptr;
     size_t scratch_bytes = 0;
 
-    hipStream_t stream() const { return ext_stream ? ext_stream : own_stream; }
+    hipStream_t stream() const { return use_ext ? ext_stream : own_stream; }
 
     och::DevPool dev() const
     {
@@ -299,7 +300,7 @@ OCH_API int och_gpu_pool_destroy(och_gpu_pool *p)
     if (!p) return OCH_OK;
     DeviceGuard g(p->device);
     if (p->own_stream) (void)hipStreamSynchronize(p->own_stream);
-    if (p->ext_stream) (void)hipStreamSynchronize(p->ext_stream);
+    if (p->use_ext) (void)hipStreamSynchronize(p->ext_stream);
     if (p->d_nodes) (void)hipFree(p->d_nodes);
     if (p->d_lut) (void)hipFree(p->d_lut);
     if (p->d_palette) (void)hipFree(p->d_palette);
@@ -379,6 +380,7 @@ OCH_API int och_gpu_set_stream(och_gpu_pool *p, void *stream)
 {
     if (!p) return fail(OCH_E_INVALID, "pool is NULL");
     p->ext_stream = (hipStream_t)stream;
+    p->use_ext = true;
     return OCH_OK;
 }
 

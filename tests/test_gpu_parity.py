@@ -214,11 +214,12 @@ def test_pool_update_after_edits(ort, O, gpu_device):
     rays = O.raygen(0.1, -0.3, 1.25, 320, 180)
     ref = O.trace_batch(T.pool(), O.Rcp(None), ORIGIN, rays, want_push=True)
     assert_same(gpu_trace_dev(pool, ORIGIN, rays), ref)
-    # an edit that would make a kernel read outside the pool is refused
-    bad = after[lo:lo + 1].copy()
+    # an edit that would make a kernel read outside the pool is refused: the
+    # root is an interior node, so its slots must name nodes of the pool
+    bad = after[T.root - 1:T.root].copy()
     bad[0, :] = before.shape[0] + 50
     with pytest.raises(ort.OchError):
-        pool.update(lo + 1, bad, T.root)
+        pool.update(T.root, bad, T.root)
     assert_same(gpu_trace_dev(pool, ORIGIN, rays), ref)
     pool.close()
 
