@@ -124,6 +124,19 @@ OCH_API int och_gpu_set_palette(och_gpu_pool *pool, const uint32_t *rgba, uint32
  * non-blocking stream of its own. */
 OCH_API int och_gpu_set_stream(och_gpu_pool *pool, void *hip_stream);
 OCH_API int och_gpu_synchronize(och_gpu_pool *pool);
+/* Launch schedule of trace/render kernels. */
+typedef enum och_option {
+    OCH_OPT_SCHEDULE = 0,      /* 0 = grid (one ray per thread), 1 = persistent waves with lane refill */
+    OCH_OPT_BLOCK = 1,         /* threads per workgroup: 64..1024, multiple of 64 (default 256) */
+    OCH_OPT_WAVES_PER_CU = 2,  /* persistent: resident waves per compute unit (default 32) */
+    OCH_OPT_REFILL = 3         /* persistent: refill a wave once this many of its lanes are idle (1..64) */
+} och_option;
+OCH_API int och_gpu_set_option(och_gpu_pool *pool, int option, int value);
+OCH_API int och_gpu_get_option(const och_gpu_pool *pool, int option, int *value);
+/* Diagnostics: later trace/render launches write one record per wave into a
+ * device buffer of capacity_waves x 4 uint64: {start, end} (s_memrealtime,
+ * 100 MHz), HW_ID | XCC_ID << 32, rays finished.  NULL turns it off. */
+OCH_API int och_gpu_set_stamp_buffer(och_gpu_pool *pool, uint64_t *stamps, uint32_t capacity_waves);
 /* Duration of the most recent trace/render kernel launched on the pool,
  * measured with HIP events on the stream it ran on (blocks until it ends). */
 OCH_API int och_gpu_last_kernel_ms(och_gpu_pool *pool, float *ms);

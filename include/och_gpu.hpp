@@ -1,0 +1,109 @@
+// och_gpu.hpp -- header-only C++ host mirror over the C ABI (och_gpu.h).
+//
+// Gives a reference user the same call shapes they had:
+//   tree.sse_trace(ox, oy, oz, dx, dy, dz, hit_direction, hit_voxel, hit_time)
+//                                               ORT/och_h_octree.h:292, :449-452
+//   camera.update_position() + window.update_image()
+//                                               ORT/test_och_h_octree.cpp:87-138, :437-457
+// with the work done by the gfx950 kernels.  Errors throw och::gpu::error.
+#pragma once
+#include <cstdint>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "och_gpu.h"
+
+namespace och {
+namespace gpu {
+
+// och::direction (ORT/och_tree_helper.h:7-18).
+enum class direction : int32_t {
+    x_pos = 0, y_pos = 1, z_pos = 2, x_neg = 3, y_neg = 4, z_neg = 5, exit = 6, inside = 7, error = 8
+};
+
+struct error : std::runtime_error {
+    int status;
+    error(int s, const std::string &what) : std::runtime_error(what), status(s) {}
+};
+
+inline void check(int status, const char *what)
+{
+    if (status != OCH_OK) throw error(status, std::string(what) + ": " + och_last_error());
+}
+
+struct float3 {
+    float x, y, z;
+};
+
+// A node pool resident on one GPU.  Construct from the reference's own table
+// (h_octree: table->nodes, capacity, root_idx, Depth) or from och_build_terrain.
+class tree {
+public:
+    tree(const uint32_t *nodes, uint32_t n_nodes, uint32_t root, int depth, int index_base = 1,
+         float miss_t = __builtin_inff(), int device = -1)
+    {
+        check(och_gpu_pool_create(nodes, n_nodes, root, depth, index_base, miss_t, device, &pool_), "och_gpu_pool_create");
+    }
+    tree(const tree &) = delete;
+    tree &operator=(const tree &) = delete;
+    ~tree() { och_gpu_pool_destroy(pool_); }
+
+    // h_octree::sse_trace, one ray (synchronous; fine for the pick ray of :536).
+    void sse_trace(float ox, float oy, float oz, float dx, float dy, float dz, direction &hit_direction,
+                   uint32_t &hit_voxel, float &hit_time) const
+    {
+        int32_t d = 0;
+        check(och_gpu_trace(pool_, ox, oy, oz, dx, dy, dz, &d, &hit_voxel, &hit_time), "och_gpu_trace");
+        hit_direction = static_cast<direction>(d);
+    }
+    void sse_trace(float3 o, float3 d, direction &hit_direction, uint32_t &hit_voxel, float &hit_time) const
+    {
+        sse_trace(o.x, o.y, o.z, d.x, d.y, d.z, hit_direction, hit_voxel, hit_time);
+    }
+
+    // Many rays at once (the per-pixel loop's calls, batched).
+    void trace_batch(float3 origin, const std::vector<float3> &dirs, std::vector<direction> &dir_out,
+                     std::vector<uint32_t> &voxel_out, std::vector<float> &t_out) const
+    {
+        const uint32_t n = static_cast<uint32_t>(dirs.size());
+        std::vector<int32_t> d(n);
+        voxel_out.resize(n);
+        t_out.resize(n);
+        check(och_gpu_trace_batch(pool_, &origin.x, 0, &dirs[0].x, n, d.data(), voxel_out.data(), t_out.data()),
+              "och_gpu_trace_batch");
+        dir_out.resize(n);
+        for (uint32_t i = 0; i < n; ++i) dir_out[i] = static_cast<direction>(d[i]);
+    }
+
+    void set_palette(const std::vector<uint32_t> &rgba)
+    {
+        check(och_gpu_set_palette(pool_, rgba.data(), static_cast<uint32_t>(rgba.size() / 6)), "och_gpu_set_palette");
+    }
+
+    // update_position + update_image into an olc::Sprite-compatible RGBA8 buffer
+    // (memcpy it into GetDrawTarget()->GetData(), olcPixelGameEngine.h:945).
+    void render(const och_camera &cam, uint32_t *rgba) const { check(och_gpu_render(pool_, &cam, rgba), "och_gpu_render"); }
+
+    och_gpu_pool *handle() const { return pool_; }
+
+private:
+    och_gpu_pool *pool_ = nullptr;
+};
+
+// tree_camera's per-frame state (pos :55, dir :53, fov :95).
+struct camera {
+    float3 pos{1.5F, 1.5F, 1.5F};
+    float yaw = 0.0F, pitch = 0.0F, fov = 1.25F;
+    int width = 640, height = 360;
+
+    och_camera update_position() const
+    {
+        och_camera c;
+        check(och_camera_setup(pos.x, pos.y, pos.z, yaw, pitch, fov, width, height, &c), "och_camera_setup");
+        return c;
+    }
+};
+
+}  // namespace gpu
+}  // namespace och

@@ -129,6 +129,12 @@ struct och_gpu_pool {
     bool use_ext = false;           // och_gpu_set_stream called: ext_stream (NULL = null stream)
     hipEvent_t ev_start = nullptr, ev_stop = nullptr;
     bool timed = false;
+    // schedule (och_gpu_set_option)
+    int opt_schedule = 0, opt_block = 256, opt_waves_per_cu = 32, opt_refill = 16;
+    int cus = 256;
+    uint32_t *d_counter = nullptr;
+    uint64_t *stamps = nullptr;
+    uint32_t stamp_cap = 0;
     // host mirror of the uploaded nodes (user numbering), for validating edits
     std::vector<uint32_t> mirror;
     // host-call staging
@@ -136,6 +142,20 @@ struct och_gpu_pool {
     size_t scratch_bytes = 0;
 
     hipStream_t stream() const { return use_ext ? ext_stream : own_stream; }
+
+    och::Schedule schedule() const
+    {
+        och::Schedule sc;
+        sc.persistent = opt_schedule == 1;
+        sc.block = opt_block;
+        sc.waves_per_cu = opt_waves_per_cu;
+        sc.refill_min = opt_refill;
+        sc.cus = cus;
+        sc.counter = d_counter;
+        sc.stamps = stamps;
+        sc.stamp_cap = stamp_cap;
+        return sc;
+    }
 
     och::DevPool dev() const
     {
@@ -281,6 +301,10 @@ OCH_API int och_gpu_pool_create(const uint32_t *nodes, uint32_t n_nodes, uint32_
     if (hipMemcpy(p->d_nodes + 8 * index_base, nodes, (size_t)n_nodes * 32, hipMemcpyHostToDevice) != hipSuccess)
         return bail(fail(OCH_E_HIP, "node upload failed"));
     p->mirror.assign(nodes, nodes + (size_t)n_nodes * 8);
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
+        p->cus = prop.multiProcessorCount;
+    if (hipMalloc(&p->d_counter, 256) != hipSuccess) return bail(fail(OCH_E_NOMEM, "counter allocation failed"));
     if (hipStreamCreateWithFlags(&p->own_stream, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreate(&p->ev_start) != hipSuccess || hipEventCreate(&p->ev_stop) != hipSuccess)
         return bail(fail(OCH_E_HIP, "stream/event creation failed"));
@@ -305,6 +329,7 @@ OCH_API int och_gpu_pool_destroy(och_gpu_pool *p)
     if (p->d_lut) (void)hipFree(p->d_lut);
     if (p->d_palette) (void)hipFree(p->d_palette);
     if (p->d_scratch) (void)hipFree(p->d_scratch);
+    if (p->d_counter) (void)hipFree(p->d_counter);
     if (p->ev_start) (void)hipEventDestroy(p->ev_start);
     if (p->ev_stop) (void)hipEventDestroy(p->ev_stop);
     if (p->own_stream) (void)hipStreamDestroy(p->own_stream);
@@ -384,6 +409,51 @@ OCH_API int och_gpu_set_stream(och_gpu_pool *p, void *stream)
     return OCH_OK;
 }
 
+OCH_API int och_gpu_set_option(och_gpu_pool *p, int option, int value)
+{
+    if (!p) return fail(OCH_E_INVALID, "pool is NULL");
+    switch (option) {
+    case OCH_OPT_SCHEDULE:
+        if (value != 0 && value != 1) return fail(OCH_E_INVALID, "schedule must be 0 or 1");
+        p->opt_schedule = value;
+        return OCH_OK;
+    case OCH_OPT_BLOCK:
+        if (value < 64 || value > 1024 || value % 64) return fail(OCH_E_INVALID, "block %d", value);
+        p->opt_block = value;
+        return OCH_OK;
+    case OCH_OPT_WAVES_PER_CU:
+        if (value < 1 || value > 32) return fail(OCH_E_INVALID, "waves per CU %d outside 1..32", value);
+        p->opt_waves_per_cu = value;
+        return OCH_OK;
+    case OCH_OPT_REFILL:
+        if (value < 1 || value > 64) return fail(OCH_E_INVALID, "refill %d outside 1..64", value);
+        p->opt_refill = value;
+        return OCH_OK;
+    default:
+        return fail(OCH_E_INVALID, "unknown option %d", option);
+    }
+}
+
+OCH_API int och_gpu_get_option(const och_gpu_pool *p, int option, int *value)
+{
+    if (!p || !value) return fail(OCH_E_INVALID, "NULL argument");
+    switch (option) {
+    case OCH_OPT_SCHEDULE: *value = p->opt_schedule; return OCH_OK;
+    case OCH_OPT_BLOCK: *value = p->opt_block; return OCH_OK;
+    case OCH_OPT_WAVES_PER_CU: *value = p->opt_waves_per_cu; return OCH_OK;
+    case OCH_OPT_REFILL: *value = p->opt_refill; return OCH_OK;
+    default: return fail(OCH_E_INVALID, "unknown option %d", option);
+    }
+}
+
+OCH_API int och_gpu_set_stamp_buffer(och_gpu_pool *p, uint64_t *stamps, uint32_t capacity_waves)
+{
+    if (!p) return fail(OCH_E_INVALID, "pool is NULL");
+    p->stamps = capacity_waves ? stamps : nullptr;
+    p->stamp_cap = stamps ? capacity_waves : 0;
+    return OCH_OK;
+}
+
 OCH_API int och_gpu_synchronize(och_gpu_pool *p)
 {
     if (!p) return fail(OCH_E_INVALID, "pool is NULL");
@@ -413,7 +483,7 @@ OCH_API int och_gpu_trace_batch_dev(och_gpu_pool *p, const float *origin, int or
     DeviceGuard g(p->device);
     OCH_HIP(hipEventRecord(p->ev_start, p->stream()));
     OCH_HIP(och::launch_trace_batch(p->dev(), origin, origin_stride, dirs, n, hit_dir, hit_voxel,
-                                    reinterpret_cast<uint32_t *>(hit_time), push_count, p->stream()));
+                                    reinterpret_cast<uint32_t *>(hit_time), push_count, p->schedule(), p->stream()));
     OCH_HIP(hipEventRecord(p->ev_stop, p->stream()));
     p->timed = true;
     return OCH_OK;
@@ -521,7 +591,7 @@ OCH_API int och_gpu_render_dev(och_gpu_pool *p, const och_camera *cam, uint32_t 
     f.n_shards = n_shards;
     f.slice_rows = och_shard_rows(cam->height, row_chunk, n_shards);
     OCH_HIP(hipEventRecord(p->ev_start, p->stream()));
-    OCH_HIP(och::launch_render(p->dev(), f, p->stream()));
+    OCH_HIP(och::launch_render(p->dev(), f, p->schedule(), p->stream()));
     OCH_HIP(hipEventRecord(p->ev_stop, p->stream()));
     p->timed = true;
     return OCH_OK;

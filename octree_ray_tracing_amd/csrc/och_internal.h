@@ -26,15 +26,24 @@ struct DevFrame {
     int32_t row_chunk, shard, n_shards, slice_rows;
 };
 
+// How trace/render launches are scheduled (och_gpu_set_option).
+struct Schedule {
+    bool persistent;        // resident waves pulling rays from *counter, lane refill
+    int block;              // threads per workgroup (multiple of 64)
+    int waves_per_cu;       // persistent grid size per CU
+    int refill_min;         // refill once this many lanes of a wave are idle
+    int cus;                // compute units of the device
+    uint32_t *counter;      // device ray counter (persistent)
+    uint64_t *stamps;       // optional per-wave residency records
+    uint32_t stamp_cap;
+};
+
 hipError_t launch_trace_batch(const DevPool &p, const float *origin, int origin_stride, const float *dirs,
                               uint32_t n, int32_t *hit_dir, uint32_t *hit_voxel, uint32_t *hit_time,
-                              uint32_t *push_count, hipStream_t stream);
+                              uint32_t *push_count, const Schedule &sc, hipStream_t stream);
 hipError_t launch_raygen(const och_camera &cam, float *dirs, hipStream_t stream);
-hipError_t launch_render(const DevPool &p, const DevFrame &f, hipStream_t stream);
+hipError_t launch_render(const DevPool &p, const DevFrame &f, const Schedule &sc, hipStream_t stream);
 hipError_t launch_unshard(const uint32_t *gathered, uint32_t *frame, int width, int height, int row_chunk,
                           int n_shards, int slice_rows, hipStream_t stream);
-// Builder: voxel codes of the 2x2x2 leaves of one brick (GPU half of och_build_terrain).
-hipError_t launch_terrain_leaves(int depth, int tunnels, const int32_t *heights, const uint8_t *tops,
-                                 int bx, int by, int bz, int brick_leaves, uint32_t *codes, hipStream_t stream);
 
 }  // namespace och

@@ -8,6 +8,16 @@
 // RCPPS emulated from a host-captured table, x86's default NaN restored
 // before the unsigned t compare, denormal masks compared as integers.
 // Build with -ffp-contract=off and without denormal flushing.
+//
+// Two schedules share the traversal:
+//   grid       -- one ray per thread, the hardware dispatcher balances waves;
+//   persistent -- a resident grid of waves pulls rays from a device counter;
+//                 when enough lanes of a wave have finished (ballot +
+//                 popcount), one atomic refills them, so no lane idles while
+//                 its wave's slowest ray is still walking the DAG.
+// Two ray sources (a ray array, or the camera of tree_camera::update_position
+// mapped 8x8-pixel tile per wave) and two sinks (hit records, or the shaded
+// RGBA8 framebuffer of update_image) make up trace_batch and render.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -16,7 +26,6 @@
 namespace och {
 namespace {
 
-constexpr int kBlock = 256;                 // 4 waves
 constexpr uint32_t kX86DefaultNaN = 0xFFC00000u;
 
 __device__ __forceinline__ uint32_t fbits(float f) { return __float_as_uint(f); }
@@ -49,124 +58,138 @@ struct Hit {
     uint32_t push;
 };
 
-// h_octree::sse_trace / octree::sse_trace (ORT/och_h_octree.h:292-447,
-// ORT/och_octree.cpp:167-320) for one ray.  stack points at this lane's first
-// LDS slot; consecutive levels are kBlock words apart.
-template <bool kCount>
-__device__ __forceinline__ Hit trace_one(const DevPool &P, float ox, float oy, float oz, float dx, float dy,
-                                         float dz, uint32_t *stack)
+// Traversal state of one ray between iterations.
+struct Ray {
+    float c[3], b[3];     // coefficient (RCPPS of -|d|) and bias (-c * o') per axis
+    uint32_t p[3];        // position bits in the reflected frame
+    uint32_t inv;         // direction-sign mask (1 = positive)
+    uint32_t idx;         // child index bits at the current level
+    uint32_t dim;         // mantissa bit of the current child size
+    uint32_t node;
+    uint32_t t_min;       // bits of the entry t of the current cell
+    uint32_t min_axis;    // 1, 2, 4 (last STEP axis) or 8 (none yet)
+    int level;
+    bool stepping;        // next iteration starts at STEP (after a failed PUSH or a POP)
+    uint32_t push;
+};
+
+// Setup, ORT/och_h_octree.h:294-338.
+__device__ __forceinline__ void ray_init(Ray &r, const DevPool &P, const float *o, const float *d)
 {
-    const float o[3] = {ox, oy, oz};
-    const float d[3] = {dx, dy, dz};
-    float c[3], b[3];
-    uint32_t p[3];
-    uint32_t inv = 0, idx = 0;
+    r.inv = 0;
+    r.idx = 0;
 #pragma unroll
     for (int a = 0; a < 3; ++a) {
         const uint32_t db = fbits(d[a]);
         const bool positive = (int32_t)db > 0 && db <= 0x7F800000u;          // 0 < d, :310
-        inv |= (uint32_t)positive << a;
+        r.inv |= (uint32_t)positive << a;
         const float refl = fabsf(__fsub_rn(positive ? 3.0F : 0.0F, o[a]));   // :314
-        c[a] = ffrom(rcpps(db | 0x80000000u, P.lut, P.lut_shift));           // :312, :316
-        b[a] = ffrom(fbits(__fmul_rn(c[a], refl)) ^ 0x80000000u);           // :318
-        p[a] = fbits(refl) & 0x3FC00000u;                                   // :320
-        idx |= (uint32_t)(p[a] == 0x3FC00000u) << a;                        // :324
+        r.c[a] = ffrom(rcpps(db | 0x80000000u, P.lut, P.lut_shift));         // :312, :316
+        r.b[a] = ffrom(fbits(__fmul_rn(r.c[a], refl)) ^ 0x80000000u);       // :318
+        r.p[a] = fbits(refl) & 0x3FC00000u;                                 // :320
+        r.idx |= (uint32_t)(r.p[a] == 0x3FC00000u) << a;                    // :324
     }
-
-    const uint32_t *__restrict__ nodes = P.nodes;
-    uint32_t dim = 1u << 22;
-    uint32_t node = P.root;
-    uint32_t t_min = 0;           // +0.0F
-    int level = 1;
-    uint32_t min_axis = 8;
-    uint32_t push = 0;
-    bool stepping = false;
-    Hit h;
-    for (;;) {
-        if (!stepping) {                                                    // PUSH :342
-            if (kCount) ++push;
-            const uint32_t child = nodes[8u * node + ((idx ^ inv) & 7u)];
-            if (child) {
-                if (level == P.depth) {                                     // HIT :346-355
-                    h.voxel = child;
-                    h.dir = (int32_t)((min_axis >> 1) + 3u * ((inv & min_axis) == 0));
-                    h.t = t_min;
-                    break;
-                }
-                stack[(level - 1) * kBlock] = node;                          // :357
-                ++level;
-                node = child;
-                dim >>= 1;                                                  // :361
-                const float tm = ffrom(t_min);
-                uint32_t nidx = 0;
-#pragma unroll
-                for (int a = 0; a < 3; ++a) {                               // :363-373
-                    const float t_mid = __builtin_fmaf(ffrom(p[a] | dim), c[a], b[a]);
-                    const bool upper = t_mid >= tm;
-                    nidx |= (uint32_t)upper << a;
-                    p[a] |= upper ? dim : 0u;
-                }
-                idx = nidx;
-                continue;
-            }
-            stepping = true;
-        }
-        // STEP :378-419
-        const uint32_t tx = t_bits(__builtin_fmaf(ffrom(p[0]), c[0], b[0]));
-        const uint32_t ty = t_bits(__builtin_fmaf(ffrom(p[1]), c[1], b[1]));
-        const uint32_t tz = t_bits(__builtin_fmaf(ffrom(p[2]), c[2], b[2]));
-        const bool sx = tx <= ty && tx <= tz;
-        const bool sy = !sx && ty < tx && ty <= tz;
-        min_axis = sx ? 1u : (sy ? 2u : 4u);
-        t_min = sx ? tx : (sy ? ty : tz);
-        if (idx & min_axis) {                                               // advance :413-419
-            const int a = sx ? 0 : (sy ? 1 : 2);
-            p[a] &= ~dim;
-            idx ^= min_axis;
-            stepping = false;
-            continue;
-        }
-        // POP :421-446
-        if (--level == 0) {
-            h.voxel = 0;
-            h.dir = OCH_EXIT;
-            h.t = P.miss_bits;
-            break;
-        }
-        node = stack[(level - 1) * kBlock];
-#pragma unroll
-        for (int a = 0; a < 3; ++a) p[a] &= ~dim;
-        dim <<= 1;
-        idx = (uint32_t)((p[0] & dim) != 0) | ((uint32_t)((p[1] & dim) != 0) << 1) |
-              ((uint32_t)((p[2] & dim) != 0) << 2);
-    }
-    h.push = push;
-    return h;
+    r.dim = 1u << 22;                                                       // :326
+    r.node = P.root;
+    r.t_min = 0;                                                            // +0.0F
+    r.level = 1;
+    r.min_axis = 8;
+    r.stepping = false;
+    r.push = 0;
 }
 
+// One iteration of the PUSH / STEP / POP machine (ORT/och_h_octree.h:342-446,
+// ORT/och_octree.cpp:217-319): one child fetch, or one STEP possibly
+// followed by a POP.  Returns true when the ray has finished (h filled).
+// stack: this lane's first LDS slot, levels `stride` words apart.
 template <bool kCount>
-__global__ __launch_bounds__(kBlock) void k_trace_batch(DevPool P, const float *__restrict__ origin,
-                                                        int origin_stride, const float *__restrict__ dirs,
-                                                        uint32_t n, int32_t *__restrict__ hit_dir,
-                                                        uint32_t *__restrict__ hit_voxel,
-                                                        uint32_t *__restrict__ hit_time,
-                                                        uint32_t *__restrict__ push_count)
+__device__ __forceinline__ bool ray_iterate(Ray &r, const DevPool &P, uint32_t *stack, uint32_t stride, Hit &h)
 {
-    extern __shared__ uint32_t lds_stack[];
-    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
-    if (i >= n) return;
-    const float *o = origin + (size_t)origin_stride * i;
-    const float *d = dirs + 3 * (size_t)i;
-    const Hit h = trace_one<kCount>(P, o[0], o[1], o[2], d[0], d[1], d[2], lds_stack + threadIdx.x);
-    hit_dir[i] = h.dir;
-    hit_voxel[i] = h.voxel;
-    hit_time[i] = h.t;
-    if (kCount) push_count[i] = h.push;
+    if (!r.stepping) {                                                       // PUSH :342
+        if (kCount) ++r.push;
+        const uint32_t child = P.nodes[8u * r.node + ((r.idx ^ r.inv) & 7u)];
+        if (child) {
+            if (r.level == P.depth) {                                       // HIT :346-355
+                h.voxel = child;
+                h.dir = (int32_t)((r.min_axis >> 1) + 3u * ((r.inv & r.min_axis) == 0));
+                h.t = r.t_min;
+                h.push = r.push;
+                return true;
+            }
+            stack[(uint32_t)(r.level - 1) * stride] = r.node;               // :357
+            ++r.level;
+            r.node = child;
+            r.dim >>= 1;                                                    // :361
+            const float tm = ffrom(r.t_min);
+            uint32_t nidx = 0;
+#pragma unroll
+            for (int a = 0; a < 3; ++a) {                                   // :363-373
+                const float t_mid = __builtin_fmaf(ffrom(r.p[a] | r.dim), r.c[a], r.b[a]);
+                const bool upper = t_mid >= tm;
+                nidx |= (uint32_t)upper << a;
+                r.p[a] |= upper ? r.dim : 0u;
+            }
+            r.idx = nidx;
+            return false;
+        }
+        r.stepping = true;
+    }
+    // STEP :378-419
+    const uint32_t tx = t_bits(__builtin_fmaf(ffrom(r.p[0]), r.c[0], r.b[0]));
+    const uint32_t ty = t_bits(__builtin_fmaf(ffrom(r.p[1]), r.c[1], r.b[1]));
+    const uint32_t tz = t_bits(__builtin_fmaf(ffrom(r.p[2]), r.c[2], r.b[2]));
+    const bool sx = tx <= ty && tx <= tz;
+    const bool sy = !sx && ty < tx && ty <= tz;
+    r.min_axis = sx ? 1u : (sy ? 2u : 4u);
+    r.t_min = sx ? tx : (sy ? ty : tz);
+    if (r.idx & r.min_axis) {                                               // advance :413-419
+        if (sx) r.p[0] &= ~r.dim;
+        else if (sy) r.p[1] &= ~r.dim;
+        else r.p[2] &= ~r.dim;
+        r.idx ^= r.min_axis;
+        r.stepping = false;
+        return false;
+    }
+    // POP :421-446
+    if (--r.level == 0) {
+        h.voxel = 0;
+        h.dir = OCH_EXIT;
+        h.t = P.miss_bits;
+        h.push = r.push;
+        return true;
+    }
+    r.node = stack[(uint32_t)(r.level - 1) * stride];
+#pragma unroll
+    for (int a = 0; a < 3; ++a) r.p[a] &= ~r.dim;
+    r.dim <<= 1;
+    r.idx = (uint32_t)((r.p[0] & r.dim) != 0) | ((uint32_t)((r.p[1] & r.dim) != 0) << 1) |
+            ((uint32_t)((r.p[2] & r.dim) != 0) << 2);
+    return false;
 }
+
+// ---------------------------------------------------------------- sources
+
+// Rays from arrays: shared (stride 0) or per-ray (stride 3) origin, AoS float3 dirs.
+struct ArraySource {
+    const float *origin;
+    const float *dirs;
+    int origin_stride;
+    uint32_t n;
+    __device__ __forceinline__ uint32_t count() const { return n; }
+    __device__ __forceinline__ bool get(uint32_t i, float *o, float *d, uint32_t &out) const
+    {
+        const float *po = origin + (size_t)origin_stride * i;
+        const float *pd = dirs + 3 * (size_t)i;
+        o[0] = po[0]; o[1] = po[1]; o[2] = po[2];
+        d[0] = pd[0]; d[1] = pd[1]; d[2] = pd[2];
+        out = i;
+        return true;
+    }
+};
 
 // tree_camera::update_position per pixel (ORT/test_och_h_octree.cpp:119-136):
 // products rounded, sums left to right, correctly rounded sqrt and divide.
-__device__ __forceinline__ void camera_ray(const och_camera &C, int col, int row, float &rx, float &ry, float &rz)
+__device__ __forceinline__ void camera_ray(const och_camera &C, int col, int row, float *d)
 {
     const float u = __fmul_rn(C.aspect, __fsub_rn(__fmul_rn(C.view_x, (float)col), 1.0F));
     const float v = __fsub_rn(__fmul_rn(C.view_y, (float)row), 1.0F);
@@ -178,59 +201,180 @@ __device__ __forceinline__ void camera_ray(const och_camera &C, int col, int row
     const float mag2 = __fadd_rn(__fadd_rn(__fmul_rn(ru, ru), __fmul_rn(rv, rv)), __fmul_rn(rw, rw));
     // __builtin_sqrtf lowers to the correctly rounded expansion; __fsqrt_rn is a bare v_sqrt_f32 (1 ulp).
     const float rmag = __fdiv_rn(1.0F, __builtin_sqrtf(mag2));
-    rx = __fmul_rn(rw, rmag);
-    ry = __fmul_rn(ru, rmag);
-    rz = __fmul_rn(-rv, rmag);
+    d[0] = __fmul_rn(rw, rmag);
+    d[1] = __fmul_rn(ru, rmag);
+    d[2] = __fmul_rn(-rv, rmag);
 }
 
-__global__ __launch_bounds__(kBlock) void k_raygen(och_camera C, float *__restrict__ dirs)
+// Camera rays of one shard's slice, enumerated 8x8 pixel tile after tile
+// (ray i -> tile i / 64, pixel i % 64), so a wave's 64 rays are one tile.
+struct CameraSource {
+    och_camera cam;
+    int32_t row_chunk, shard, n_shards, slice_rows;
+    uint32_t tiles_x;
+    uint32_t n;      // tiles_x * tiles_y * 64
+    __device__ __forceinline__ uint32_t count() const { return n; }
+    __device__ __forceinline__ bool get(uint32_t i, float *o, float *d, uint32_t &out) const
+    {
+        const uint32_t tile = i >> 6, lane = i & 63u;
+        const int col = (int)((tile % tiles_x) * 8u + (lane & 7u));
+        const int srow = (int)((tile / tiles_x) * 8u + (lane >> 3));
+        if (col >= cam.width || srow >= slice_rows) return false;
+        const int chunk = srow / row_chunk, within = srow - chunk * row_chunk;
+        const int row = (chunk * n_shards + shard) * row_chunk + within;
+        if (row >= cam.height) return false;
+        o[0] = cam.pos[0]; o[1] = cam.pos[1]; o[2] = cam.pos[2];
+        camera_ray(cam, col, row, d);
+        out = (uint32_t)srow * (uint32_t)cam.width + (uint32_t)col;
+        return true;
+    }
+};
+
+// ---------------------------------------------------------------- sinks
+
+template <bool kCount>
+struct HitSink {
+    int32_t *dir;
+    uint32_t *voxel;
+    uint32_t *t;
+    uint32_t *push;
+    __device__ __forceinline__ void put(uint32_t i, const Hit &h) const
+    {
+        dir[i] = h.dir;
+        voxel[i] = h.voxel;
+        t[i] = h.t;
+        if (kCount) push[i] = h.push;
+    }
+};
+
+// trace_pixel's colour choice (ORT/test_och_h_octree.cpp:76-84) as olc::Pixel RGBA8.
+struct FrameSink {
+    uint32_t *out;
+    const uint32_t *palette;
+    uint32_t n_voxels;
+    __device__ __forceinline__ void put(uint32_t i, const Hit &h) const
+    {
+        uint32_t c;
+        if (h.dir == OCH_EXIT) c = 0xFFFEBF00u;           // {0x00, 0xBF, 0xFE}
+        else if (h.dir == OCH_INSIDE) c = 0xFF07193Fu;    // {0x3F, 0x19, 0x07}
+        else if (h.voxel == 0 || h.voxel > n_voxels) c = 0xFFFF00FFu;
+        else c = palette[6u * (h.voxel - 1u) + (uint32_t)h.dir];
+        out[i] = c;
+    }
+};
+
+// ---------------------------------------------------------------- stamps
+
+// Diagnostic residency record per wave: {start, end} in s_memrealtime ticks
+// (100 MHz), HW_ID | XCC_ID << 32, rays finished.  Off when stamps == null.
+__device__ __forceinline__ uint64_t realtime() { return __builtin_amdgcn_s_memrealtime(); }
+
+__device__ __forceinline__ uint64_t hw_ids()
+{
+    uint32_t hw, xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    return (uint64_t)hw | ((uint64_t)xcc << 32);
+}
+
+__device__ __forceinline__ void stamp(uint64_t *stamps, uint32_t cap, uint64_t t0, uint64_t rays)
+{
+    const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    if ((threadIdx.x & 63) == 0 && wave < cap) {
+        uint64_t *s = stamps + 4 * (size_t)wave;
+        s[0] = t0;
+        s[1] = realtime();
+        s[2] = hw_ids();
+        s[3] = rays;
+    }
+}
+
+// ---------------------------------------------------------------- kernels
+
+template <class Src, class Sink, bool kCount>
+__global__ void k_trace_grid(DevPool P, Src S, Sink K, uint64_t *stamps, uint32_t stamp_cap)
+{
+    extern __shared__ uint32_t lds_stack[];
+    const uint64_t t0 = stamps ? realtime() : 0;
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    float o[3], d[3];
+    uint32_t out;
+    if (i < S.count() && S.get(i, o, d, out)) {
+        Ray r;
+        ray_init(r, P, o, d);
+        Hit h;
+        while (!ray_iterate<kCount>(r, P, lds_stack + threadIdx.x, blockDim.x, h)) {
+        }
+        K.put(out, h);
+    }
+    if (stamps) stamp(stamps, stamp_cap, t0, 64);
+}
+
+template <class Src, class Sink, bool kCount>
+__global__ void k_trace_persistent(DevPool P, Src S, Sink K, uint32_t *counter, int refill_min, uint64_t *stamps,
+                                   uint32_t stamp_cap)
+{
+    extern __shared__ uint32_t lds_stack[];
+    const uint64_t t0 = stamps ? realtime() : 0;
+    uint32_t *stack = lds_stack + threadIdx.x;
+    const uint32_t n = S.count();
+    const int lane = threadIdx.x & 63;
+    const uint64_t below = (1ull << lane) - 1ull;
+    Ray r;
+    uint32_t out = 0;
+    bool active = false, drained = false;
+    uint64_t finished = 0;
+    for (;;) {
+        const uint64_t idle = __ballot(!active);
+        const int n_idle = __popcll(idle);
+        if (!drained && n_idle >= refill_min) {               // wave-uniform
+            const int leader = __ffsll((unsigned long long)idle) - 1;
+            uint32_t base = 0;
+            if (lane == leader) base = atomicAdd(counter, (uint32_t)n_idle);
+            base = __shfl(base, leader);
+            drained = base + (uint32_t)n_idle >= n;
+            if (!active) {
+                const uint32_t i = base + (uint32_t)__popcll(idle & below);
+                float o[3], d[3];
+                if (i < n && S.get(i, o, d, out)) {
+                    ray_init(r, P, o, d);
+                    active = true;
+                }
+            }
+        }
+        if (__ballot(active) == 0) {
+            if (drained) break;
+            continue;
+        }
+        if (active) {
+            Hit h;
+            if (ray_iterate<kCount>(r, P, stack, blockDim.x, h)) {
+                K.put(out, h);
+                active = false;
+                ++finished;
+            }
+        }
+    }
+    if (stamps) stamp(stamps, stamp_cap, t0, finished);
+}
+
+__global__ __launch_bounds__(256) void k_raygen(och_camera C, float *__restrict__ dirs)
 {
     const int col = blockIdx.x * 16 + (threadIdx.x & 15);
     const int row = blockIdx.y * 16 + (threadIdx.x >> 4);
     if (col >= C.width || row >= C.height) return;
-    float x, y, z;
-    camera_ray(C, col, row, x, y, z);
+    float d[3];
+    camera_ray(C, col, row, d);
     const size_t k = 3 * ((size_t)row * C.width + col);
-    dirs[k] = x;
-    dirs[k + 1] = y;
-    dirs[k + 2] = z;
+    dirs[k] = d[0];
+    dirs[k + 1] = d[1];
+    dirs[k + 2] = d[2];
 }
 
-// trace_pixel's colour choice (ORT/test_och_h_octree.cpp:76-84) as olc::Pixel RGBA8.
-__device__ __forceinline__ uint32_t shade(const Hit &h, const uint32_t *__restrict__ palette, uint32_t n_voxels)
+__global__ __launch_bounds__(256) void k_unshard(const uint32_t *__restrict__ gathered, uint32_t *__restrict__ frame,
+                                                 int width, int height, int row_chunk, int n_shards, int slice_rows)
 {
-    if (h.dir == OCH_EXIT) return 0xFFFEBF00u;      // {0x00, 0xBF, 0xFE}
-    if (h.dir == OCH_INSIDE) return 0xFF07193Fu;    // {0x3F, 0x19, 0x07}
-    if (h.voxel == 0 || h.voxel > n_voxels) return 0xFFFF00FFu;
-    return palette[6u * (h.voxel - 1u) + (uint32_t)h.dir];
-}
-
-// One frame of update_image for shard f.shard: each wave shades an 8x8 pixel
-// tile (so its 64 rays descend the same top-of-DAG lines), a 256-thread block
-// a 16x16 tile of the shard's compact slice.
-__global__ __launch_bounds__(kBlock) void k_render(DevPool P, DevFrame F)
-{
-    extern __shared__ uint32_t lds_stack[];
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int col = blockIdx.x * 16 + (wave & 1) * 8 + (lane & 7);
-    const int srow = blockIdx.y * 16 + (wave >> 1) * 8 + (lane >> 3);
-    if (srow >= F.slice_rows || col >= F.cam.width) return;
-    const int chunk = srow / F.row_chunk, within = srow - chunk * F.row_chunk;
-    const int row = (chunk * F.n_shards + F.shard) * F.row_chunk + within;
-    if (row >= F.cam.height) return;
-    // An empty h_octree (root 0) walks the all-zero padding node and misses
-    // everywhere: the exit colour update_image draws for it (:443-446).
-    float dx, dy, dz;
-    camera_ray(F.cam, col, row, dx, dy, dz);
-    const Hit h = trace_one<false>(P, F.cam.pos[0], F.cam.pos[1], F.cam.pos[2], dx, dy, dz, lds_stack + threadIdx.x);
-    F.out[(size_t)srow * F.cam.width + col] = shade(h, F.palette, F.n_voxels);
-}
-
-__global__ __launch_bounds__(kBlock) void k_unshard(const uint32_t *__restrict__ gathered, uint32_t *__restrict__ frame,
-                                                    int width, int height, int row_chunk, int n_shards,
-                                                    int slice_rows)
-{
-    const int col = blockIdx.x * kBlock + threadIdx.x;
+    const int col = blockIdx.x * 256 + threadIdx.x;
     const int row = blockIdx.y;
     if (col >= width || row >= height) return;
     const int gchunk = row / row_chunk, within = row - gchunk * row_chunk;
@@ -239,45 +383,70 @@ __global__ __launch_bounds__(kBlock) void k_unshard(const uint32_t *__restrict__
     frame[(size_t)row * width + col] = gathered[src];
 }
 
-size_t stack_bytes(int depth) { return (size_t)(depth > 1 ? depth - 1 : 1) * kBlock * sizeof(uint32_t); }
+size_t stack_bytes(int depth, int block) { return (size_t)(depth > 1 ? depth - 1 : 1) * block * sizeof(uint32_t); }
+
+template <class Src, class Sink, bool kCount>
+hipError_t launch(const DevPool &p, const Src &s, const Sink &k, uint32_t n, const Schedule &sc, hipStream_t stream)
+{
+    if (n == 0) return hipSuccess;
+    const int block = sc.block;
+    const size_t lds = stack_bytes(p.depth, block);
+    if (sc.persistent) {
+        hipError_t e = hipMemsetAsync(sc.counter, 0, sizeof(uint32_t), stream);
+        if (e != hipSuccess) return e;
+        const uint32_t blocks_per_cu = (uint32_t)((sc.waves_per_cu * 64 + block - 1) / block);
+        uint32_t grid = (uint32_t)sc.cus * blocks_per_cu;
+        const uint32_t needed = (n + block - 1) / block;
+        if (grid > needed) grid = needed;
+        hipLaunchKernelGGL((k_trace_persistent<Src, Sink, kCount>), dim3(grid), dim3(block), lds, stream, p, s, k,
+                           sc.counter, sc.refill_min, sc.stamps, sc.stamp_cap);
+    } else {
+        hipLaunchKernelGGL((k_trace_grid<Src, Sink, kCount>), dim3((n + block - 1) / block), dim3(block), lds, stream,
+                           p, s, k, sc.stamps, sc.stamp_cap);
+    }
+    return hipGetLastError();
+}
 
 }  // namespace
 
 hipError_t launch_trace_batch(const DevPool &p, const float *origin, int origin_stride, const float *dirs,
                               uint32_t n, int32_t *hit_dir, uint32_t *hit_voxel, uint32_t *hit_time,
-                              uint32_t *push_count, hipStream_t stream)
+                              uint32_t *push_count, const Schedule &sc, hipStream_t stream)
 {
-    if (n == 0) return hipSuccess;
-    const dim3 grid((n + kBlock - 1) / kBlock);
+    const ArraySource src{origin, dirs, origin_stride, n};
     if (push_count)
-        hipLaunchKernelGGL(k_trace_batch<true>, grid, dim3(kBlock), stack_bytes(p.depth), stream, p, origin,
-                           origin_stride, dirs, n, hit_dir, hit_voxel, hit_time, push_count);
-    else
-        hipLaunchKernelGGL(k_trace_batch<false>, grid, dim3(kBlock), stack_bytes(p.depth), stream, p, origin,
-                           origin_stride, dirs, n, hit_dir, hit_voxel, hit_time, push_count);
-    return hipGetLastError();
+        return launch<ArraySource, HitSink<true>, true>(p, src, HitSink<true>{hit_dir, hit_voxel, hit_time, push_count},
+                                                        n, sc, stream);
+    return launch<ArraySource, HitSink<false>, false>(p, src, HitSink<false>{hit_dir, hit_voxel, hit_time, nullptr}, n,
+                                                      sc, stream);
 }
 
 hipError_t launch_raygen(const och_camera &cam, float *dirs, hipStream_t stream)
 {
     const dim3 grid((cam.width + 15) / 16, (cam.height + 15) / 16);
-    hipLaunchKernelGGL(k_raygen, grid, dim3(kBlock), 0, stream, cam, dirs);
+    hipLaunchKernelGGL(k_raygen, grid, dim3(256), 0, stream, cam, dirs);
     return hipGetLastError();
 }
 
-hipError_t launch_render(const DevPool &p, const DevFrame &f, hipStream_t stream)
+hipError_t launch_render(const DevPool &p, const DevFrame &f, const Schedule &sc, hipStream_t stream)
 {
-    const dim3 grid((f.cam.width + 15) / 16, (f.slice_rows + 15) / 16);
-    hipLaunchKernelGGL(k_render, grid, dim3(kBlock), stack_bytes(p.depth), stream, p, f);
-    return hipGetLastError();
+    CameraSource src;
+    src.cam = f.cam;
+    src.row_chunk = f.row_chunk;
+    src.shard = f.shard;
+    src.n_shards = f.n_shards;
+    src.slice_rows = f.slice_rows;
+    src.tiles_x = (uint32_t)(f.cam.width + 7) / 8;
+    src.n = src.tiles_x * (uint32_t)((f.slice_rows + 7) / 8) * 64u;
+    return launch<CameraSource, FrameSink, false>(p, src, FrameSink{f.out, f.palette, f.n_voxels}, src.n, sc, stream);
 }
 
 hipError_t launch_unshard(const uint32_t *gathered, uint32_t *frame, int width, int height, int row_chunk,
                           int n_shards, int slice_rows, hipStream_t stream)
 {
-    const dim3 grid((width + kBlock - 1) / kBlock, height);
-    hipLaunchKernelGGL(k_unshard, grid, dim3(kBlock), 0, stream, gathered, frame, width, height, row_chunk,
-                       n_shards, slice_rows);
+    const dim3 grid((width + 255) / 256, height);
+    hipLaunchKernelGGL(k_unshard, grid, dim3(256), 0, stream, gathered, frame, width, height, row_chunk, n_shards,
+                       slice_rows);
     return hipGetLastError();
 }
 

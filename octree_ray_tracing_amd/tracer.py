@@ -121,7 +121,9 @@ class GpuPool:
         return self.info()["root"]
 
     def set_rcp_lut(self, lut: np.ndarray):
-        lut = np.ascontiguousarray(lut, np.uint32)
+        lut = np.ascontiguousarray(lut, np.uint32).reshape(-1)
+        if lut.size < 2 or lut.size & (lut.size - 1):
+            raise ValueError("RCPPS table size must be a power of two")
         call("och_gpu_set_rcp_lut", self._h, _np_ptr(lut), int(round(math.log2(lut.size))))
 
     def set_palette(self, rgba: np.ndarray):
@@ -139,6 +141,21 @@ class GpuPool:
     def update(self, first: int, nodes: np.ndarray, root: int):
         nodes = np.ascontiguousarray(nodes, np.uint32).reshape(-1, 8)
         call("och_gpu_pool_update", self._h, int(first), nodes.shape[0], _np_ptr(nodes), int(root))
+
+    OPTIONS = {"schedule": 0, "block": 1, "waves_per_cu": 2, "refill": 3}
+
+    def set_option(self, name: str, value: int):
+        """Launch schedule: schedule (0 grid / 1 persistent), block, waves_per_cu, refill."""
+        call("och_gpu_set_option", self._h, self.OPTIONS[name], int(value))
+
+    def get_option(self, name: str) -> int:
+        v = C.c_int()
+        call("och_gpu_get_option", self._h, self.OPTIONS[name], C.byref(v))
+        return v.value
+
+    def set_stamp_buffer(self, stamps, capacity_waves: int):
+        """Per-wave residency records (diagnostics); stamps = device int64 tensor or None."""
+        call("och_gpu_set_stamp_buffer", self._h, None if stamps is None else _dev_ptr(stamps), int(capacity_waves))
 
     def synchronize(self):
         call("och_gpu_synchronize", self._h)

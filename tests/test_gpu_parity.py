@@ -227,8 +227,10 @@ def test_pool_update_after_edits(ort, O, gpu_device):
 def test_error_paths(ort, gpu_device):
     tree = ort.build_terrain(4)
     pool = ort.HOctree(tree.nodes, tree.root, 4, device=0)
-    with pytest.raises(ort.OchError):
+    with pytest.raises(ValueError):
         pool.set_rcp_lut(np.zeros(3, np.uint32))
+    with pytest.raises(ort.OchError):
+        pool.set_option("block", 100)
     with pytest.raises(ValueError):
         pool.set_palette(np.zeros(5, np.uint32))
     import ctypes as C
