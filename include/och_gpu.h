@@ -137,6 +137,10 @@ OCH_API int och_gpu_get_option(const och_gpu_pool *pool, int option, int *value)
  * device buffer of capacity_waves x 4 uint64: {start, end} (s_memrealtime,
  * 100 MHz), HW_ID | XCC_ID << 32, rays finished.  NULL turns it off. */
 OCH_API int och_gpu_set_stamp_buffer(och_gpu_pool *pool, uint64_t *stamps, uint32_t capacity_waves);
+/* Diagnostics: HIP's occupancy answer (workgroups per CU) for kind 0 = render
+ * grid kernel, 1 = render persistent kernel, 2 = trace grid kernel, at the
+ * pool's block size and stack depth. */
+OCH_API int och_gpu_occupancy(const och_gpu_pool *pool, int kind, int *blocks_per_cu);
 /* Duration of the most recent trace/render kernel launched on the pool,
  * measured with HIP events on the stream it ran on (blocks until it ends). */
 OCH_API int och_gpu_last_kernel_ms(och_gpu_pool *pool, float *ms);

@@ -446,6 +446,14 @@ OCH_API int och_gpu_get_option(const och_gpu_pool *p, int option, int *value)
     }
 }
 
+OCH_API int och_gpu_occupancy(const och_gpu_pool *p, int kind, int *blocks_per_cu)
+{
+    if (!p || !blocks_per_cu) return fail(OCH_E_INVALID, "NULL argument");
+    DeviceGuard g(p->device);
+    OCH_HIP(och::occupancy_blocks_per_cu(kind, p->opt_block, p->depth, blocks_per_cu));
+    return OCH_OK;
+}
+
 OCH_API int och_gpu_set_stamp_buffer(och_gpu_pool *p, uint64_t *stamps, uint32_t capacity_waves)
 {
     if (!p) return fail(OCH_E_INVALID, "pool is NULL");

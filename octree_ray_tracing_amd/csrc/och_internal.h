@@ -41,6 +41,9 @@ struct Schedule {
 hipError_t launch_trace_batch(const DevPool &p, const float *origin, int origin_stride, const float *dirs,
                               uint32_t n, int32_t *hit_dir, uint32_t *hit_voxel, uint32_t *hit_time,
                               uint32_t *push_count, const Schedule &sc, hipStream_t stream);
+// hipOccupancyMaxActiveBlocksPerMultiprocessor of kind 0 render-grid,
+// 1 render-persistent, 2 trace-grid, at this block size and stack depth.
+hipError_t occupancy_blocks_per_cu(int kind, int block, int depth, int *blocks);
 hipError_t launch_raygen(const och_camera &cam, float *dirs, hipStream_t stream);
 hipError_t launch_render(const DevPool &p, const DevFrame &f, const Schedule &sc, hipStream_t stream);
 hipError_t launch_unshard(const uint32_t *gathered, uint32_t *frame, int width, int height, int row_chunk,

@@ -409,6 +409,23 @@ hipError_t launch(const DevPool &p, const Src &s, const Sink &k, uint32_t n, con
 
 }  // namespace
 
+hipError_t occupancy_blocks_per_cu(int kind, int block, int depth, int *blocks)
+{
+    const size_t lds = stack_bytes(depth, block);
+    switch (kind) {
+    case 0:
+        return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, k_trace_grid<CameraSource, FrameSink, false>, block, lds);
+    case 1:
+        return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, k_trace_persistent<CameraSource, FrameSink, false>,
+                                                            block, lds);
+    case 2:
+        return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, k_trace_grid<ArraySource, HitSink<false>, false>,
+                                                            block, lds);
+    default:
+        return hipErrorInvalidValue;
+    }
+}
+
 hipError_t launch_trace_batch(const DevPool &p, const float *origin, int origin_stride, const float *dirs,
                               uint32_t n, int32_t *hit_dir, uint32_t *hit_voxel, uint32_t *hit_time,
                               uint32_t *push_count, const Schedule &sc, hipStream_t stream)

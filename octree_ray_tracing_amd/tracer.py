@@ -157,6 +157,12 @@ class GpuPool:
         """Per-wave residency records (diagnostics); stamps = device int64 tensor or None."""
         call("och_gpu_set_stamp_buffer", self._h, None if stamps is None else _dev_ptr(stamps), int(capacity_waves))
 
+    def occupancy(self, kind: int = 0) -> int:
+        """HIP's workgroups-per-CU answer: 0 render grid, 1 render persistent, 2 trace grid."""
+        v = C.c_int()
+        call("och_gpu_occupancy", self._h, int(kind), C.byref(v))
+        return v.value
+
     def synchronize(self):
         call("och_gpu_synchronize", self._h)
 
