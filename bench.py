@@ -155,7 +155,7 @@ def main():
     pool.set_palette(ort.VoxelData().get_colours())
     stream = torch.cuda.current_stream()
     pool.set_stream(stream)
-    sf = ShardedFrame(pool, W, H, a.row_chunk)
+    sf = ShardedFrame(pool, W, H, a.row_chunk, n_views=len(PITCHES))
     cams = [ort.camera(ORIGIN, YAW, p, FOV, W, H) for p in PITCHES]
 
     # PUSH counts of this rank's rays (for the algorithmic byte count): trace
@@ -199,8 +199,7 @@ def main():
 
     # warmup
     for _ in range(a.warmup):
-        for cam in cams:
-            sf.render(cam)
+        sf.render(cams)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -208,13 +207,12 @@ def main():
     ev = []
     t0 = time.perf_counter()
     for _ in range(a.steps):
-        for cam in cams:
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record(stream)
-            sf.render_local(cam)
-            e1.record(stream)
-            sf.exchange()
-            ev.append((e0, e1))
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        sf.render_local(cams)
+        e1.record(stream)
+        sf.exchange()
+        ev.append((e0, e1))
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -229,10 +227,10 @@ def main():
     frames = a.steps * len(cams)
     total_rays = W * H * frames
     value = total_rays / elapsed / 1e6
-    # Algorithmic bytes of the dominant kernel (k_render) per launch on this
-    # rank: 4 B pixel store per ray + 4 B per child-slot read (PUSH) + 4 B
-    # palette read per hit ray; averaged over the two pitches.
-    bytes_per_launch = (4 * rays_rank + 4 * push_total + 4 * hits_total) / len(cams)
+    # Algorithmic bytes of the dominant kernel (the render launch, both views)
+    # on this rank: 4 B pixel store per ray + 4 B per child-slot read (PUSH,
+    # SURVEY 8d) + 4 B palette read per hit ray.
+    bytes_per_launch = 4 * rays_rank + 4 * push_total + 4 * hits_total
     k_avg_ms = float(kms.mean())
     achieved = bytes_per_launch / (k_avg_ms * 1e-3) / 1e9
     pmc = load_pmc("k_render", f"d{a.depth}_{W}x{H}_n{world}")
@@ -266,7 +264,7 @@ def main():
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 5),
                          "traffic": None if pmc is None else pmc.get("hbm_bytes_per_launch"),
-                         "kernel": "k_render", "kernel_ms": round(k_avg_ms, 4),
+                         "kernel": "k_trace_grid<CameraSource,FrameSink> (2 views per launch)", "kernel_ms": round(k_avg_ms, 4),
                          "bytes_per_launch": int(bytes_per_launch),
                          "push_per_ray": round(push_total / rays_rank, 3),
                          "note": "pointer-chase over an L2/MALL-resident DAG: latency/VALU-bound, not HBM-bound"},

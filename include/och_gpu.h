@@ -29,6 +29,7 @@ extern "C" {
 #endif
 
 #define OCH_GPU_ABI_VERSION 1
+#define OCH_MAX_VIEWS 8
 
 #if defined(__GNUC__)
 #define OCH_API __attribute__((visibility("default")))
@@ -180,10 +181,19 @@ OCH_API int och_gpu_render(och_gpu_pool *pool, const och_camera *cam, uint32_t *
 OCH_API int och_gpu_render_dev(och_gpu_pool *pool, const och_camera *cam, uint32_t *rgba_slice,
                                int row_chunk, int shard, int n_shards);
 OCH_API int och_shard_rows(int height, int row_chunk, int n_shards);
+/* Several cameras of equal size in one launch (stereo / multi-view frames):
+ * view v's slice goes to rgba_slices + v * och_shard_rows(H, row_chunk, n_shards) * W.
+ * One launch keeps the GPU busy with other views while a view's slowest rays finish. */
+OCH_API int och_gpu_render_views_dev(och_gpu_pool *pool, const och_camera *cams, int n_views, uint32_t *rgba_slices,
+                                     int row_chunk, int shard, int n_shards);
 /* Reassemble n_shards gathered slices (slice s at gathered + s*rows*W) into a
  * full W*H frame on the device. */
 OCH_API int och_gpu_unshard_dev(och_gpu_pool *pool, const uint32_t *gathered, uint32_t *frame,
                                 int width, int height, int row_chunk, int n_shards);
+/* Multi-view form: gathered = [n_shards][n_views][rows][W] (each rank's
+ * och_gpu_render_views_dev output, all-gathered), frames = [n_views][H][W]. */
+OCH_API int och_gpu_unshard_views_dev(och_gpu_pool *pool, const uint32_t *gathered, uint32_t *frames,
+                                      int width, int height, int row_chunk, int n_shards, int n_views);
 
 /* ------------------------------------------------------------ builder */
 /* The demo terrain (ORT/test_och_h_octree.cpp:561-787) built in parallel

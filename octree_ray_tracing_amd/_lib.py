@@ -80,7 +80,9 @@ PROTOTYPES = {
     "och_gpu_render": (C.c_int, [_P, C.POINTER(Camera), _P]),
     "och_gpu_render_dev": (C.c_int, [_P, C.POINTER(Camera), _P, C.c_int, C.c_int, C.c_int]),
     "och_shard_rows": (C.c_int, [C.c_int, C.c_int, C.c_int]),
+    "och_gpu_render_views_dev": (C.c_int, [_P, _P, C.c_int, _P, C.c_int, C.c_int, C.c_int]),
     "och_gpu_unshard_dev": (C.c_int, [_P, _P, _P, C.c_int, C.c_int, C.c_int, C.c_int]),
+    "och_gpu_unshard_views_dev": (C.c_int, [_P, _P, _P, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int]),
     "och_build_terrain": (C.c_int, [C.POINTER(TerrainParams), C.POINTER(HostPool)]),
     "och_host_pool_free": (None, [C.POINTER(HostPool)]),
     "och_pool_at": (_u32, [_P, _u32, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int]),

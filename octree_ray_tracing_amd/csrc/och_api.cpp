@@ -581,23 +581,30 @@ OCH_API int och_shard_rows(int height, int row_chunk, int n_shards)
     return ((chunks + n_shards - 1) / n_shards) * row_chunk;
 }
 
-OCH_API int och_gpu_render_dev(och_gpu_pool *p, const och_camera *cam, uint32_t *rgba_slice, int row_chunk, int shard,
-                               int n_shards)
+OCH_API int och_gpu_render_views_dev(och_gpu_pool *p, const och_camera *cams, int n_views, uint32_t *rgba_slices,
+                                     int row_chunk, int shard, int n_shards)
 {
-    if (!p || !cam || !rgba_slice) return fail(OCH_E_INVALID, "NULL argument");
+    if (!p || !cams || !rgba_slices) return fail(OCH_E_INVALID, "NULL argument");
+    if (n_views < 1 || n_views > OCH_MAX_VIEWS) return fail(OCH_E_INVALID, "n_views %d outside 1..%d", n_views, OCH_MAX_VIEWS);
     if (row_chunk <= 0 || n_shards <= 0 || shard < 0 || shard >= n_shards)
         return fail(OCH_E_INVALID, "bad sharding (%d, %d, %d)", row_chunk, shard, n_shards);
+    for (int v = 0; v < n_views; ++v)
+        if (cams[v].width != cams[0].width || cams[v].height != cams[0].height || cams[v].width <= 0 || cams[v].height <= 0)
+            return fail(OCH_E_INVALID, "views must share one positive width and height");
+    if ((uint64_t)cams[0].width * cams[0].height * n_views >= (1ull << 32))
+        return fail(OCH_E_INVALID, "frame too large");
     if (!p->d_lut) return fail(OCH_E_RCP_MODEL, "no RCPPS table on this pool (call och_gpu_set_rcp_lut)");
     DeviceGuard g(p->device);
     och::DevFrame f;
-    f.cam = *cam;
+    for (int v = 0; v < n_views; ++v) f.cams[v] = cams[v];
+    f.n_views = n_views;
     f.palette = p->d_palette;
     f.n_voxels = p->n_voxels;
-    f.out = rgba_slice;
+    f.out = rgba_slices;
     f.row_chunk = row_chunk;
     f.shard = shard;
     f.n_shards = n_shards;
-    f.slice_rows = och_shard_rows(cam->height, row_chunk, n_shards);
+    f.slice_rows = och_shard_rows(cams[0].height, row_chunk, n_shards);
     OCH_HIP(hipEventRecord(p->ev_start, p->stream()));
     OCH_HIP(och::launch_render(p->dev(), f, p->schedule(), p->stream()));
     OCH_HIP(hipEventRecord(p->ev_stop, p->stream()));
@@ -605,15 +612,28 @@ OCH_API int och_gpu_render_dev(och_gpu_pool *p, const och_camera *cam, uint32_t 
     return OCH_OK;
 }
 
+OCH_API int och_gpu_render_dev(och_gpu_pool *p, const och_camera *cam, uint32_t *rgba_slice, int row_chunk, int shard,
+                               int n_shards)
+{
+    if (!cam) return fail(OCH_E_INVALID, "NULL camera");
+    return och_gpu_render_views_dev(p, cam, 1, rgba_slice, row_chunk, shard, n_shards);
+}
+
+OCH_API int och_gpu_unshard_views_dev(och_gpu_pool *p, const uint32_t *gathered, uint32_t *frames, int width,
+                                      int height, int row_chunk, int n_shards, int n_views)
+{
+    if (!p || !gathered || !frames || width <= 0 || height <= 0 || row_chunk <= 0 || n_shards <= 0 || n_views < 1)
+        return fail(OCH_E_INVALID, "bad unshard arguments");
+    DeviceGuard g(p->device);
+    OCH_HIP(och::launch_unshard(gathered, frames, width, height, row_chunk, n_shards,
+                                och_shard_rows(height, row_chunk, n_shards), n_views, p->stream()));
+    return OCH_OK;
+}
+
 OCH_API int och_gpu_unshard_dev(och_gpu_pool *p, const uint32_t *gathered, uint32_t *frame, int width, int height,
                                 int row_chunk, int n_shards)
 {
-    if (!p || !gathered || !frame || width <= 0 || height <= 0 || row_chunk <= 0 || n_shards <= 0)
-        return fail(OCH_E_INVALID, "bad unshard arguments");
-    DeviceGuard g(p->device);
-    OCH_HIP(och::launch_unshard(gathered, frame, width, height, row_chunk, n_shards,
-                                och_shard_rows(height, row_chunk, n_shards), p->stream()));
-    return OCH_OK;
+    return och_gpu_unshard_views_dev(p, gathered, frame, width, height, row_chunk, n_shards, 1);
 }
 
 OCH_API int och_gpu_render(och_gpu_pool *p, const och_camera *cam, uint32_t *rgba)

@@ -19,10 +19,11 @@ struct DevPool {
 };
 
 struct DevFrame {
-    och_camera cam;
+    och_camera cams[OCH_MAX_VIEWS];   // equal width / height
+    int32_t n_views;
     const uint32_t *palette;  // 6 * n_voxels RGBA8
     uint32_t n_voxels;
-    uint32_t *out;            // compact slice, slice_rows x width
+    uint32_t *out;            // n_views compact slices, each slice_rows x width
     int32_t row_chunk, shard, n_shards, slice_rows;
 };
 
@@ -46,7 +47,7 @@ hipError_t launch_trace_batch(const DevPool &p, const float *origin, int origin_
 hipError_t occupancy_blocks_per_cu(int kind, int block, int depth, int *blocks);
 hipError_t launch_raygen(const och_camera &cam, float *dirs, hipStream_t stream);
 hipError_t launch_render(const DevPool &p, const DevFrame &f, const Schedule &sc, hipStream_t stream);
-hipError_t launch_unshard(const uint32_t *gathered, uint32_t *frame, int width, int height, int row_chunk,
-                          int n_shards, int slice_rows, hipStream_t stream);
+hipError_t launch_unshard(const uint32_t *gathered, uint32_t *frames, int width, int height, int row_chunk,
+                          int n_shards, int slice_rows, int n_views, hipStream_t stream);
 
 }  // namespace och

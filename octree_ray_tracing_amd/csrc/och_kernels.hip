@@ -27,6 +27,7 @@ namespace och {
 namespace {
 
 constexpr uint32_t kX86DefaultNaN = 0xFFC00000u;
+constexpr int kMaxViews = OCH_MAX_VIEWS;
 
 __device__ __forceinline__ uint32_t fbits(float f) { return __float_as_uint(f); }
 __device__ __forceinline__ float ffrom(uint32_t u) { return __uint_as_float(u); }
@@ -58,10 +59,14 @@ struct Hit {
     uint32_t push;
 };
 
-// Traversal state of one ray between iterations.
+// Traversal state of one ray between iterations.  The current node's eight
+// child slots are held in VGPRs (loaded as two 16-byte loads when the ray
+// enters or returns to a node), so a PUSH into an empty child and the sibling
+// advance after it cost no memory round trip.
 struct Ray {
     float c[3], b[3];     // coefficient (RCPPS of -|d|) and bias (-c * o') per axis
     uint32_t p[3];        // position bits in the reflected frame
+    uint32_t k0, k1, k2, k3, k4, k5, k6, k7;   // child slots of `node` (scalars: no indexed access)
     uint32_t inv;         // direction-sign mask (1 = positive)
     uint32_t idx;         // child index bits at the current level
     uint32_t dim;         // mantissa bit of the current child size
@@ -72,6 +77,24 @@ struct Ray {
     bool stepping;        // next iteration starts at STEP (after a failed PUSH or a POP)
     uint32_t push;
 };
+
+__device__ __forceinline__ void load_node(Ray &r, const DevPool &P, uint32_t v)
+{
+    const uint4 *q = reinterpret_cast<const uint4 *>(P.nodes + 8u * v);
+    const uint4 a = q[0], b = q[1];
+    r.k0 = a.x; r.k1 = a.y; r.k2 = a.z; r.k3 = a.w;
+    r.k4 = b.x; r.k5 = b.y; r.k6 = b.z; r.k7 = b.w;
+}
+
+// children[k] of the held node: a 3-level select instead of indexed registers.
+__device__ __forceinline__ uint32_t child_of(const Ray &r, uint32_t k)
+{
+    const bool b0 = k & 1u, b1 = k & 2u;
+    const uint32_t s01 = b0 ? r.k1 : r.k0, s23 = b0 ? r.k3 : r.k2;
+    const uint32_t s45 = b0 ? r.k5 : r.k4, s67 = b0 ? r.k7 : r.k6;
+    const uint32_t lo = b1 ? s23 : s01, hi = b1 ? s67 : s45;
+    return (k & 4u) ? hi : lo;
+}
 
 // Setup, ORT/och_h_octree.h:294-338.
 __device__ __forceinline__ void ray_init(Ray &r, const DevPool &P, const float *o, const float *d)
@@ -91,6 +114,7 @@ __device__ __forceinline__ void ray_init(Ray &r, const DevPool &P, const float *
     }
     r.dim = 1u << 22;                                                       // :326
     r.node = P.root;
+    load_node(r, P, P.root);
     r.t_min = 0;                                                            // +0.0F
     r.level = 1;
     r.min_axis = 8;
@@ -107,7 +131,7 @@ __device__ __forceinline__ bool ray_iterate(Ray &r, const DevPool &P, uint32_t *
 {
     if (!r.stepping) {                                                       // PUSH :342
         if (kCount) ++r.push;
-        const uint32_t child = P.nodes[8u * r.node + ((r.idx ^ r.inv) & 7u)];
+        const uint32_t child = child_of(r, (r.idx ^ r.inv) & 7u);
         if (child) {
             if (r.level == P.depth) {                                       // HIT :346-355
                 h.voxel = child;
@@ -119,6 +143,7 @@ __device__ __forceinline__ bool ray_iterate(Ray &r, const DevPool &P, uint32_t *
             stack[(uint32_t)(r.level - 1) * stride] = r.node;               // :357
             ++r.level;
             r.node = child;
+            load_node(r, P, child);
             r.dim >>= 1;                                                    // :361
             const float tm = ffrom(r.t_min);
             uint32_t nidx = 0;
@@ -159,6 +184,7 @@ __device__ __forceinline__ bool ray_iterate(Ray &r, const DevPool &P, uint32_t *
         return true;
     }
     r.node = stack[(uint32_t)(r.level - 1) * stride];
+    load_node(r, P, r.node);              // consumed by the next PUSH; overlaps the STEP
 #pragma unroll
     for (int a = 0; a < 3; ++a) r.p[a] &= ~r.dim;
     r.dim <<= 1;
@@ -206,26 +232,29 @@ __device__ __forceinline__ void camera_ray(const och_camera &C, int col, int row
     d[2] = __fmul_rn(-rv, rmag);
 }
 
-// Camera rays of one shard's slice, enumerated 8x8 pixel tile after tile
-// (ray i -> tile i / 64, pixel i % 64), so a wave's 64 rays are one tile.
+// Camera rays of one shard's slice for up to kMaxViews cameras of equal size,
+// enumerated view after view, 8x8 pixel tile after tile (ray i -> tile i / 64,
+// pixel i % 64), so a wave's 64 rays are one tile of one view.  The output
+// token is view * slice_pixels + slice pixel.
 struct CameraSource {
-    och_camera cam;
-    int32_t row_chunk, shard, n_shards, slice_rows;
-    uint32_t tiles_x;
-    uint32_t n;      // tiles_x * tiles_y * 64
-    __device__ __forceinline__ uint32_t count() const { return n; }
+    och_camera cam[kMaxViews];
+    int32_t n_views, row_chunk, shard, n_shards, slice_rows, width, height;
+    uint32_t tiles_x, per_view, slice_pixels;
+    __host__ __device__ __forceinline__ uint32_t count() const { return per_view * (uint32_t)n_views; }
     __device__ __forceinline__ bool get(uint32_t i, float *o, float *d, uint32_t &out) const
     {
-        const uint32_t tile = i >> 6, lane = i & 63u;
+        const uint32_t view = i / per_view, j = i - view * per_view;
+        const uint32_t tile = j >> 6, lane = j & 63u;
         const int col = (int)((tile % tiles_x) * 8u + (lane & 7u));
         const int srow = (int)((tile / tiles_x) * 8u + (lane >> 3));
-        if (col >= cam.width || srow >= slice_rows) return false;
+        if (col >= width || srow >= slice_rows) return false;
         const int chunk = srow / row_chunk, within = srow - chunk * row_chunk;
         const int row = (chunk * n_shards + shard) * row_chunk + within;
-        if (row >= cam.height) return false;
-        o[0] = cam.pos[0]; o[1] = cam.pos[1]; o[2] = cam.pos[2];
-        camera_ray(cam, col, row, d);
-        out = (uint32_t)srow * (uint32_t)cam.width + (uint32_t)col;
+        if (row >= height) return false;
+        const och_camera &C = cam[view];
+        o[0] = C.pos[0]; o[1] = C.pos[1]; o[2] = C.pos[2];
+        camera_ray(C, col, row, d);
+        out = view * slice_pixels + (uint32_t)srow * (uint32_t)width + (uint32_t)col;
         return true;
     }
 };
@@ -371,16 +400,18 @@ __global__ __launch_bounds__(256) void k_raygen(och_camera C, float *__restrict_
     dirs[k + 2] = d[2];
 }
 
-__global__ __launch_bounds__(256) void k_unshard(const uint32_t *__restrict__ gathered, uint32_t *__restrict__ frame,
-                                                 int width, int height, int row_chunk, int n_shards, int slice_rows)
+// gathered: [n_shards][n_views][slice_rows][width] -> frames: [n_views][height][width]
+__global__ __launch_bounds__(256) void k_unshard(const uint32_t *__restrict__ gathered, uint32_t *__restrict__ frames,
+                                                 int width, int height, int row_chunk, int n_shards, int slice_rows,
+                                                 int n_views)
 {
     const int col = blockIdx.x * 256 + threadIdx.x;
-    const int row = blockIdx.y;
+    const int row = blockIdx.y, view = blockIdx.z;
     if (col >= width || row >= height) return;
     const int gchunk = row / row_chunk, within = row - gchunk * row_chunk;
     const int shard = gchunk % n_shards, lchunk = gchunk / n_shards;
-    const size_t src = ((size_t)shard * slice_rows + (size_t)lchunk * row_chunk + within) * width + col;
-    frame[(size_t)row * width + col] = gathered[src];
+    const size_t src = (((size_t)shard * n_views + view) * slice_rows + (size_t)lchunk * row_chunk + within) * width + col;
+    frames[((size_t)view * height + row) * width + col] = gathered[src];
 }
 
 size_t stack_bytes(int depth, int block) { return (size_t)(depth > 1 ? depth - 1 : 1) * block * sizeof(uint32_t); }
@@ -447,23 +478,29 @@ hipError_t launch_raygen(const och_camera &cam, float *dirs, hipStream_t stream)
 
 hipError_t launch_render(const DevPool &p, const DevFrame &f, const Schedule &sc, hipStream_t stream)
 {
+    if (f.n_views < 1 || f.n_views > kMaxViews) return hipErrorInvalidValue;
     CameraSource src;
-    src.cam = f.cam;
+    for (int v = 0; v < f.n_views; ++v) src.cam[v] = f.cams[v];
+    src.n_views = f.n_views;
     src.row_chunk = f.row_chunk;
     src.shard = f.shard;
     src.n_shards = f.n_shards;
     src.slice_rows = f.slice_rows;
-    src.tiles_x = (uint32_t)(f.cam.width + 7) / 8;
-    src.n = src.tiles_x * (uint32_t)((f.slice_rows + 7) / 8) * 64u;
-    return launch<CameraSource, FrameSink, false>(p, src, FrameSink{f.out, f.palette, f.n_voxels}, src.n, sc, stream);
+    src.width = f.cams[0].width;
+    src.height = f.cams[0].height;
+    src.tiles_x = (uint32_t)(src.width + 7) / 8;
+    src.per_view = src.tiles_x * (uint32_t)((f.slice_rows + 7) / 8) * 64u;
+    src.slice_pixels = (uint32_t)f.slice_rows * (uint32_t)src.width;
+    return launch<CameraSource, FrameSink, false>(p, src, FrameSink{f.out, f.palette, f.n_voxels}, src.count(), sc,
+                                                  stream);
 }
 
-hipError_t launch_unshard(const uint32_t *gathered, uint32_t *frame, int width, int height, int row_chunk,
-                          int n_shards, int slice_rows, hipStream_t stream)
+hipError_t launch_unshard(const uint32_t *gathered, uint32_t *frames, int width, int height, int row_chunk,
+                          int n_shards, int slice_rows, int n_views, hipStream_t stream)
 {
-    const dim3 grid((width + 255) / 256, height);
-    hipLaunchKernelGGL(k_unshard, grid, dim3(256), 0, stream, gathered, frame, width, height, row_chunk, n_shards,
-                       slice_rows);
+    const dim3 grid((width + 255) / 256, height, n_views);
+    hipLaunchKernelGGL(k_unshard, grid, dim3(256), 0, stream, gathered, frames, width, height, row_chunk, n_shards,
+                       slice_rows, n_views);
     return hipGetLastError();
 }
 

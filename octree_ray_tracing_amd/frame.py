@@ -36,42 +36,48 @@ def unshard_host(gathered: np.ndarray, height: int, row_chunk: int) -> np.ndarra
 
 
 class ShardedFrame:
-    """Renders frames across the ranks of the default process group.
+    """Renders frames of one or more equal-size views across the ranks of the
+    default process group.
 
-    pool: this rank's GpuPool (same tree on every rank).  The all-gather runs
-    on the current torch stream, which the pool is bound to, so render ->
-    all-gather -> unshard are ordered without host synchronisation.
+    pool: this rank's GpuPool (same tree on every rank).  Everything runs on
+    the current torch stream, which the pool is bound to, so render ->
+    all-gather -> unshard are ordered without host synchronisation.  Views
+    are rendered by one launch (och_gpu_render_views_dev), gathered by one
+    collective and unsharded by one kernel.
     """
 
-    def __init__(self, pool: GpuPool, width: int, height: int, row_chunk: int = 8, group=None):
+    def __init__(self, pool: GpuPool, width: int, height: int, row_chunk: int = 8, n_views: int = 1, group=None):
         import torch
         import torch.distributed as dist
 
         self.pool, self.width, self.height, self.row_chunk = pool, width, height, row_chunk
-        self.group = group
+        self.n_views, self.group = n_views, group
         self.rank = dist.get_rank(group) if dist.is_initialized() else 0
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
         self.rows = shard_rows(height, row_chunk, self.world)
         dev = torch.device("cuda", torch.cuda.current_device())
-        self.slice = torch.empty((self.rows, width), dtype=torch.int32, device=dev)
-        self.gathered = torch.empty((self.world, self.rows, width), dtype=torch.int32, device=dev)
-        self.frame = torch.empty((height, width), dtype=torch.int32, device=dev)
+        self.slice = torch.empty((n_views, self.rows, width), dtype=torch.int32, device=dev)
+        self.gathered = torch.empty((self.world, n_views, self.rows, width), dtype=torch.int32, device=dev)
+        self.frames = torch.empty((n_views, height, width), dtype=torch.int32, device=dev)
         pool.set_stream(torch.cuda.current_stream())
 
-    def render_local(self, cam):
-        self.pool.render_dev(cam, self.slice, self.row_chunk, self.rank, self.world)
+    def render_local(self, cams):
+        if not isinstance(cams, (list, tuple)):
+            cams = [cams]
+        assert len(cams) == self.n_views
+        self.pool.render_views_dev(list(cams), self.slice, self.row_chunk, self.rank, self.world)
         return self.slice
 
     def exchange(self):
         import torch.distributed as dist
 
+        src = self.slice
         if self.world > 1:
             dist.all_gather_into_tensor(self.gathered, self.slice, group=self.group)
-            self.pool.unshard_dev(self.gathered, self.frame, self.width, self.height, self.row_chunk, self.world)
-        else:
-            self.pool.unshard_dev(self.slice, self.frame, self.width, self.height, self.row_chunk, 1)
-        return self.frame
+            src = self.gathered
+        self.pool.unshard_dev(src, self.frames, self.width, self.height, self.row_chunk, self.world, self.n_views)
+        return self.frames
 
-    def render(self, cam):
-        self.render_local(cam)
+    def render(self, cams):
+        self.render_local(cams)
         return self.exchange()

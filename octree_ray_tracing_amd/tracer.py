@@ -216,9 +216,17 @@ class GpuPool:
         call("och_gpu_render_dev", self._h, C.byref(cam), _dev_ptr(rgba_slice), int(row_chunk),
              int(shard), int(n_shards))
 
-    def unshard_dev(self, gathered, frame, width: int, height: int, row_chunk: int, n_shards: int):
-        call("och_gpu_unshard_dev", self._h, _dev_ptr(gathered), _dev_ptr(frame), int(width), int(height),
-             int(row_chunk), int(n_shards))
+    def render_views_dev(self, cams, rgba_slices, row_chunk: int | None = None, shard: int = 0, n_shards: int = 1):
+        """Several equal-size cameras in one launch; rgba_slices holds the views' slices back to back."""
+        arr = (Camera * len(cams))(*cams)
+        if row_chunk is None:
+            row_chunk = cams[0].height
+        call("och_gpu_render_views_dev", self._h, C.cast(arr, C.c_void_p), len(cams), _dev_ptr(rgba_slices),
+             int(row_chunk), int(shard), int(n_shards))
+
+    def unshard_dev(self, gathered, frame, width: int, height: int, row_chunk: int, n_shards: int, n_views: int = 1):
+        call("och_gpu_unshard_views_dev", self._h, _dev_ptr(gathered), _dev_ptr(frame), int(width), int(height),
+             int(row_chunk), int(n_shards), int(n_views))
 
 
 def shard_rows(height: int, row_chunk: int, n_shards: int) -> int:

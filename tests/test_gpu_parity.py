@@ -91,7 +91,9 @@ def test_camera_frames_host_rcpps(ort, O, gpu_device, depth):
     for pitch in (0.0, -0.6):
         rays = O.raygen(0.3, pitch, 1.25, 1920, 1080)
         ref = O.trace_batch(ref_pool, O.Rcp(None), ORIGIN, rays, nthreads=16, want_push=True)
-        assert_same(gpu_trace_dev(pool, ORIGIN, rays), ref)
+        for sched in (0, 1):
+            pool.set_option("schedule", sched)
+            assert_same(gpu_trace_dev(pool, ORIGIN, rays), ref)
     pool.close()
 
 
@@ -185,6 +187,37 @@ def test_render_frame_and_shards(ort, O, gpu_device):
     pool.unshard_dev(gathered, full, W, H, chunk, n)
     torch.cuda.synchronize()
     assert np.array_equal(full.cpu().numpy().view(np.uint32), want)
+    pool.close()
+
+
+def test_multi_view_render_and_unshard(ort, O, gpu_device):
+    """Several cameras in one launch == one launch per camera; sharded multi-view
+    slices reassemble exactly."""
+    import torch
+    tree = ort.build_terrain(9)
+    pool = ort.HOctree(tree.nodes, tree.root, 9, device=0)
+    pool.set_palette(ort.VoxelData().get_colours())
+    pool.set_stream(torch.cuda.current_stream())
+    W, H = 320, 200
+    cams = [ort.camera((1.5, 1.5, 1.5), y, p, 1.25, W, H) for y, p in ((0.3, 0.0), (0.3, -0.6), (1.9, -0.2))]
+    single = [torch.from_numpy(pool.render(c).view(np.int32)) for c in cams]
+    for sched in (0, 1):
+        pool.set_option("schedule", sched)
+        out = torch.zeros((3, H, W), dtype=torch.int32, device="cuda")
+        pool.render_views_dev(cams, out)
+        torch.cuda.synchronize()
+        for v in range(3):
+            assert torch.equal(out[v].cpu(), single[v])
+        n, chunk = 4, 8
+        rows = ort.shard_rows(H, chunk, n)
+        gathered = torch.zeros((n, 3, rows, W), dtype=torch.int32, device="cuda")
+        for s_ in range(n):
+            pool.render_views_dev(cams, gathered[s_], chunk, s_, n)
+        frames = torch.empty((3, H, W), dtype=torch.int32, device="cuda")
+        pool.unshard_dev(gathered, frames, W, H, chunk, n, 3)
+        torch.cuda.synchronize()
+        for v in range(3):
+            assert torch.equal(frames[v].cpu(), single[v])
     pool.close()
 
 
