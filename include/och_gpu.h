@@ -130,7 +130,10 @@ typedef enum och_option {
     OCH_OPT_SCHEDULE = 0,      /* 0 = grid (one ray per thread), 1 = persistent waves with lane refill */
     OCH_OPT_BLOCK = 1,         /* threads per workgroup: 64..1024, multiple of 64 (default 256) */
     OCH_OPT_WAVES_PER_CU = 2,  /* persistent: resident waves per compute unit (default 32) */
-    OCH_OPT_REFILL = 3         /* persistent: refill a wave once this many of its lanes are idle (1..64) */
+    OCH_OPT_REFILL = 3,        /* persistent: refill a wave once this many of its lanes are idle (1..64) */
+    OCH_OPT_LAYOUT = 4         /* 0 = the caller's node layout; 1 = packed (default when the DAG has < 2^24
+                                  (node, level) pairs): per-level breadth-first ids, interior slots carry the
+                                  child's occupancy mask so only descents and hits touch memory */
 } och_option;
 OCH_API int och_gpu_set_option(och_gpu_pool *pool, int option, int value);
 OCH_API int och_gpu_get_option(const och_gpu_pool *pool, int option, int *value);
@@ -224,6 +227,12 @@ typedef struct och_host_pool {
 
 OCH_API int och_build_terrain(const och_terrain_params *params, och_host_pool *out);
 OCH_API void och_host_pool_free(och_host_pool *pool);
+/* The packed device layout (OCH_OPT_LAYOUT 1) of a pool, on the host: node 0
+ * is zero padding, ids are breadth-first per level, interior slots hold
+ * child_id | child_mask << 24, leaf-level slots voxel ids; *out_root =
+ * root_id | root_mask << 24.  out = NULL only reports *out_nodes. */
+OCH_API int och_pool_pack(const uint32_t *nodes, uint32_t n_nodes, uint32_t root, int depth, int index_base,
+                          uint32_t *out, uint32_t out_capacity, uint32_t *out_nodes, uint32_t *out_root);
 /* h_octree::at over any pool (ORT/och_h_octree.h:239-258). */
 OCH_API uint32_t och_pool_at(const uint32_t *nodes, uint32_t root, int depth, int index_base,
                              int x, int y, int z);

@@ -48,3 +48,15 @@ def build_terrain(depth: int, tunnels: bool = True, dedup: bool = True, rand_kin
         call("och_host_pool_free", C.byref(hp))
     return NodePool(arr, hp.root, hp.depth, hp.index_base, hp.solid_voxels, list(hp.voxel_hist),
                     hp.tree_nodes, hp.build_seconds)
+
+
+def pack_pool(nodes: np.ndarray, root: int, depth: int, index_base: int = 1):
+    """The packed device layout of a pool (och_pool_pack): (packed nodes, packed root)."""
+    nodes = np.ascontiguousarray(nodes, np.uint32).reshape(-1, 8)
+    n, r = C.c_uint32(), C.c_uint32()
+    call("och_pool_pack", nodes.ctypes.data, nodes.shape[0], int(root), int(depth), int(index_base), None, 0,
+         C.byref(n), C.byref(r))
+    out = np.zeros((n.value, 8), np.uint32)
+    call("och_pool_pack", nodes.ctypes.data, nodes.shape[0], int(root), int(depth), int(index_base), out.ctypes.data,
+         n.value, C.byref(n), C.byref(r))
+    return out, r.value

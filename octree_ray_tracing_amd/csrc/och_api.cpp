@@ -10,11 +10,14 @@
 #include <cstring>
 #include <mutex>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "och_internal.h"
 
 namespace {
+
+constexpr uint32_t kIdLimit = 1u << 24;   // packed ids are 24 bits
 
 thread_local std::string g_error;
 
@@ -137,6 +140,11 @@ struct och_gpu_pool {
     uint32_t stamp_cap = 0;
     // host mirror of the uploaded nodes (user numbering), for validating edits
     std::vector<uint32_t> mirror;
+    // packed layout (see och_internal.h DevPool)
+    uint32_t *d_packed = nullptr;
+    uint32_t packed_root = 0;
+    uint32_t packed_nodes = 0;
+    int opt_layout = 1;
     // host-call staging
     void *d_scratch = nullptr;
     size_t scratch_bytes = 0;
@@ -160,9 +168,11 @@ struct och_gpu_pool {
     och::DevPool dev() const
     {
         och::DevPool p;
-        p.nodes = d_nodes;
+        const bool pk = opt_layout == 1 && d_packed;
+        p.nodes = pk ? d_packed : d_nodes;
+        p.packed = pk ? 1 : 0;
         p.lut = d_lut;
-        p.root = root;
+        p.root = pk ? packed_root : root;
         p.depth = depth;
         p.lut_shift = 23 - lut_log2;
         uint32_t mb;
@@ -215,6 +225,93 @@ int validate_pool(const uint32_t *nodes, uint32_t n_nodes, uint32_t root, int de
         }
         cur.swap(next);
     }
+    return OCH_OK;
+}
+
+// Packed layout: every reachable (node, level) pair gets a breadth-first id
+// (1-based; 0 is a zero padding node).  Interior slots become
+// child_id | child_mask << 24, leaf-level slots keep the voxel ids.  A node
+// the caller's table shares between levels (h_octree hash-conses by content
+// alone) is simply emitted once per level.  Returns false when more than
+// 2^24 - 1 ids would be needed.
+bool pack_pool(const uint32_t *nodes, uint32_t n_nodes, uint32_t root, int depth, int base,
+               std::vector<uint32_t> &out, uint32_t &packed_root)
+{
+    auto mask_of = [&](uint32_t v) {
+        const uint32_t *c = nodes + (size_t)(v - base) * 8;
+        uint32_t m = 0;
+        for (int k = 0; k < 8; ++k) m |= (uint32_t)(c[k] != 0) << k;
+        return m;
+    };
+    out.assign(8, 0u);                               // padding node 0
+    if (base == 1 && root == 0) {
+        packed_root = 0;
+        return true;
+    }
+    // id of (v, level): first_level[v] / first_id[v] hold the common case, a
+    // map holds the rare extra levels.
+    std::vector<uint8_t> first_level(n_nodes, 0);
+    std::vector<uint32_t> first_id(n_nodes, 0);
+    std::unordered_map<uint64_t, uint32_t> extra;
+    std::vector<uint32_t> order_v;
+    std::vector<uint8_t> order_l;
+    uint32_t next = 1;
+    auto id_of = [&](uint32_t v, int level, bool create) -> uint32_t {
+        const uint32_t i = v - base;
+        if (first_level[i] == level) return first_id[i];
+        if (first_level[i] == 0) {
+            if (!create) return 0;
+            first_level[i] = (uint8_t)level;
+            first_id[i] = next;
+            order_v.push_back(v);
+            order_l.push_back((uint8_t)level);
+            return next++;
+        }
+        const uint64_t key = ((uint64_t)i << 5) | (uint64_t)level;
+        auto it = extra.find(key);
+        if (it != extra.end()) return it->second;
+        if (!create) return 0;
+        extra.emplace(key, next);
+        order_v.push_back(v);
+        order_l.push_back((uint8_t)level);
+        return next++;
+    };
+    id_of(root, 1, true);
+    for (size_t q = 0; q < order_v.size(); ++q) {        // breadth-first: order grows as we go
+        const int level = order_l[q];
+        if (level >= depth) continue;
+        const uint32_t *c = nodes + (size_t)(order_v[q] - base) * 8;
+        for (int k = 0; k < 8; ++k)
+            if (c[k]) id_of(c[k], level + 1, true);
+        if (next > kIdLimit) return false;
+    }
+    out.resize((size_t)next * 8, 0u);
+    for (size_t q = 0; q < order_v.size(); ++q) {
+        const uint32_t v = order_v[q];
+        const int level = order_l[q];
+        const uint32_t *c = nodes + (size_t)(v - base) * 8;
+        uint32_t *o = out.data() + (q + 1) * 8;
+        for (int k = 0; k < 8; ++k) {
+            if (!c[k]) continue;
+            o[k] = level == depth ? c[k] : (id_of(c[k], level + 1, false) | (mask_of(c[k]) << 24));
+        }
+    }
+    packed_root = 1u | (mask_of(root) << 24);
+    return true;
+}
+
+int upload_packed(och_gpu_pool *p, const uint32_t *nodes, uint32_t n_nodes)
+{
+    std::vector<uint32_t> packed;
+    uint32_t proot = 0;
+    if (p->d_packed) OCH_HIP(hipFree(p->d_packed));
+    p->d_packed = nullptr;
+    p->packed_nodes = 0;
+    if (!pack_pool(nodes, n_nodes, p->root, p->depth, p->index_base, packed, proot)) return OCH_OK;   // raw only
+    OCH_HIP(hipMalloc(&p->d_packed, packed.size() * 4));
+    OCH_HIP(hipMemcpy(p->d_packed, packed.data(), packed.size() * 4, hipMemcpyHostToDevice));
+    p->packed_root = proot;
+    p->packed_nodes = (uint32_t)(packed.size() / 8);
     return OCH_OK;
 }
 
@@ -301,6 +398,8 @@ OCH_API int och_gpu_pool_create(const uint32_t *nodes, uint32_t n_nodes, uint32_
     if (hipMemcpy(p->d_nodes + 8 * index_base, nodes, (size_t)n_nodes * 32, hipMemcpyHostToDevice) != hipSuccess)
         return bail(fail(OCH_E_HIP, "node upload failed"));
     p->mirror.assign(nodes, nodes + (size_t)n_nodes * 8);
+    st = upload_packed(p, nodes, n_nodes);
+    if (st != OCH_OK) return bail(st);
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
         p->cus = prop.multiProcessorCount;
@@ -326,6 +425,7 @@ OCH_API int och_gpu_pool_destroy(och_gpu_pool *p)
     if (p->own_stream) (void)hipStreamSynchronize(p->own_stream);
     if (p->use_ext) (void)hipStreamSynchronize(p->ext_stream);
     if (p->d_nodes) (void)hipFree(p->d_nodes);
+    if (p->d_packed) (void)hipFree(p->d_packed);
     if (p->d_lut) (void)hipFree(p->d_lut);
     if (p->d_palette) (void)hipFree(p->d_palette);
     if (p->d_scratch) (void)hipFree(p->d_scratch);
@@ -375,7 +475,7 @@ OCH_API int och_gpu_pool_update(och_gpu_pool *p, uint32_t first, uint32_t count,
                                (size_t)count * 32, hipMemcpyHostToDevice, p->stream()));
     OCH_HIP(hipStreamSynchronize(p->stream()));
     p->root = root;
-    return OCH_OK;
+    return upload_packed(p, p->mirror.data(), n_user);
 }
 
 OCH_API int och_gpu_set_rcp_lut(och_gpu_pool *p, const uint32_t *lut, int log2_entries)
@@ -429,6 +529,11 @@ OCH_API int och_gpu_set_option(och_gpu_pool *p, int option, int value)
         if (value < 1 || value > 64) return fail(OCH_E_INVALID, "refill %d outside 1..64", value);
         p->opt_refill = value;
         return OCH_OK;
+    case OCH_OPT_LAYOUT:
+        if (value != 0 && value != 1) return fail(OCH_E_INVALID, "layout must be 0 or 1");
+        if (value == 1 && !p->d_packed) return fail(OCH_E_INVALID, "pool too large for the packed layout");
+        p->opt_layout = value;
+        return OCH_OK;
     default:
         return fail(OCH_E_INVALID, "unknown option %d", option);
     }
@@ -442,6 +547,7 @@ OCH_API int och_gpu_get_option(const och_gpu_pool *p, int option, int *value)
     case OCH_OPT_BLOCK: *value = p->opt_block; return OCH_OK;
     case OCH_OPT_WAVES_PER_CU: *value = p->opt_waves_per_cu; return OCH_OK;
     case OCH_OPT_REFILL: *value = p->opt_refill; return OCH_OK;
+    case OCH_OPT_LAYOUT: *value = (p->opt_layout == 1 && p->d_packed) ? 1 : 0; return OCH_OK;
     default: return fail(OCH_E_INVALID, "unknown option %d", option);
     }
 }
@@ -647,6 +753,25 @@ OCH_API int och_gpu_render(och_gpu_pool *p, const och_camera *cam, uint32_t *rgb
     if (st != OCH_OK) return st;
     OCH_HIP(hipMemcpyAsync(rgba, p->d_scratch, bytes, hipMemcpyDeviceToHost, p->stream()));
     OCH_HIP(hipStreamSynchronize(p->stream()));
+    return OCH_OK;
+}
+
+OCH_API int och_pool_pack(const uint32_t *nodes, uint32_t n_nodes, uint32_t root, int depth, int index_base,
+                          uint32_t *out, uint32_t out_capacity, uint32_t *out_nodes, uint32_t *out_root)
+{
+    if (!nodes || !out_nodes || !out_root) return fail(OCH_E_INVALID, "NULL argument");
+    int st = validate_pool(nodes, n_nodes, root, depth, index_base);
+    if (st != OCH_OK) return st;
+    std::vector<uint32_t> packed;
+    uint32_t proot = 0;
+    if (!pack_pool(nodes, n_nodes, root, depth, index_base, packed, proot))
+        return fail(OCH_E_CAPACITY, "more than 2^24 - 1 (node, level) pairs");
+    *out_nodes = (uint32_t)(packed.size() / 8);
+    *out_root = proot;
+    if (out) {
+        if (out_capacity < *out_nodes) return fail(OCH_E_CAPACITY, "output holds %u nodes, %u needed", out_capacity, *out_nodes);
+        std::memcpy(out, packed.data(), packed.size() * 4);
+    }
     return OCH_OK;
 }
 

@@ -9,10 +9,20 @@
 namespace och {
 
 // What a kernel needs to walk one pool: all device pointers.
+// Two device layouts of the same DAG:
+//   raw    -- the caller's nodes, nodes[8 * v + c] = child c of the node the
+//             reference calls v (1-based pools get one zero padding node at 0);
+//   packed -- re-linearised breadth-first per level; an interior slot holds
+//             child_id | child_mask << 24 (child_mask = which of the child's
+//             eight slots are non-empty), leaf-level slots hold voxel ids.
+//             An empty child is rejected from the held mask and a POP
+//             restores (node | mask << 24) from the LDS stack, so only a
+//             descent or a hit touches memory.
 struct DevPool {
-    const uint32_t *nodes;  // nodes[8 * v + c] = child c of the node the reference calls v
+    const uint32_t *nodes;  // raw or packed, per `packed`
     const uint32_t *lut;    // RCPPS table, 1 << (23 - lut_shift) entries
-    uint32_t root;
+    uint32_t root;          // raw: root index; packed: root_id | root_mask << 24
+    int32_t packed;
     int32_t depth;
     int32_t lut_shift;
     uint32_t miss_bits;     // hit_time bits of a miss (+INF or +0.0)

@@ -59,18 +59,15 @@ struct Hit {
     uint32_t push;
 };
 
-// Traversal state of one ray between iterations.  The current node's eight
-// child slots are held in VGPRs (loaded as two 16-byte loads when the ray
-// enters or returns to a node), so a PUSH into an empty child and the sibling
-// advance after it cost no memory round trip.
+// Traversal state of one ray between iterations.
 struct Ray {
     float c[3], b[3];     // coefficient (RCPPS of -|d|) and bias (-c * o') per axis
     uint32_t p[3];        // position bits in the reflected frame
-    uint32_t k0, k1, k2, k3, k4, k5, k6, k7;   // child slots of `node` (scalars: no indexed access)
     uint32_t inv;         // direction-sign mask (1 = positive)
     uint32_t idx;         // child index bits at the current level
     uint32_t dim;         // mantissa bit of the current child size
     uint32_t node;
+    uint32_t mask;        // packed layout: non-empty children of `node`
     uint32_t t_min;       // bits of the entry t of the current cell
     uint32_t min_axis;    // 1, 2, 4 (last STEP axis) or 8 (none yet)
     int level;
@@ -78,25 +75,10 @@ struct Ray {
     uint32_t push;
 };
 
-__device__ __forceinline__ void load_node(Ray &r, const DevPool &P, uint32_t v)
-{
-    const uint4 *q = reinterpret_cast<const uint4 *>(P.nodes + 8u * v);
-    const uint4 a = q[0], b = q[1];
-    r.k0 = a.x; r.k1 = a.y; r.k2 = a.z; r.k3 = a.w;
-    r.k4 = b.x; r.k5 = b.y; r.k6 = b.z; r.k7 = b.w;
-}
-
-// children[k] of the held node: a 3-level select instead of indexed registers.
-__device__ __forceinline__ uint32_t child_of(const Ray &r, uint32_t k)
-{
-    const bool b0 = k & 1u, b1 = k & 2u;
-    const uint32_t s01 = b0 ? r.k1 : r.k0, s23 = b0 ? r.k3 : r.k2;
-    const uint32_t s45 = b0 ? r.k5 : r.k4, s67 = b0 ? r.k7 : r.k6;
-    const uint32_t lo = b1 ? s23 : s01, hi = b1 ? s67 : s45;
-    return (k & 4u) ? hi : lo;
-}
+constexpr uint32_t kIdMask = 0x00FFFFFFu;
 
 // Setup, ORT/och_h_octree.h:294-338.
+template <bool kPacked>
 __device__ __forceinline__ void ray_init(Ray &r, const DevPool &P, const float *o, const float *d)
 {
     r.inv = 0;
@@ -113,8 +95,8 @@ __device__ __forceinline__ void ray_init(Ray &r, const DevPool &P, const float *
         r.idx |= (uint32_t)(r.p[a] == 0x3FC00000u) << a;                    // :324
     }
     r.dim = 1u << 22;                                                       // :326
-    r.node = P.root;
-    load_node(r, P, P.root);
+    r.node = kPacked ? (P.root & kIdMask) : P.root;
+    r.mask = P.root >> 24;
     r.t_min = 0;                                                            // +0.0F
     r.level = 1;
     r.min_axis = 8;
@@ -123,16 +105,25 @@ __device__ __forceinline__ void ray_init(Ray &r, const DevPool &P, const float *
 }
 
 // One iteration of the PUSH / STEP / POP machine (ORT/och_h_octree.h:342-446,
-// ORT/och_octree.cpp:217-319): one child fetch, or one STEP possibly
-// followed by a POP.  Returns true when the ray has finished (h filled).
+// ORT/och_octree.cpp:217-319): one PUSH, or one STEP possibly followed by a
+// POP.  Returns true when the ray has finished (h filled).
 // stack: this lane's first LDS slot, levels `stride` words apart.
-template <bool kCount>
+template <bool kPacked, bool kCount>
 __device__ __forceinline__ bool ray_iterate(Ray &r, const DevPool &P, uint32_t *stack, uint32_t stride, Hit &h)
 {
     if (!r.stepping) {                                                       // PUSH :342
         if (kCount) ++r.push;
-        const uint32_t child = child_of(r, (r.idx ^ r.inv) & 7u);
-        if (child) {
+        const uint32_t c = (r.idx ^ r.inv) & 7u;
+        uint32_t child = 0;
+        bool present;
+        if (kPacked) {
+            present = (r.mask >> c) & 1u;
+        } else {
+            child = P.nodes[8u * r.node + c];
+            present = child != 0;
+        }
+        if (present) {
+            if (kPacked) child = P.nodes[8u * r.node + c];
             if (r.level == P.depth) {                                       // HIT :346-355
                 h.voxel = child;
                 h.dir = (int32_t)((r.min_axis >> 1) + 3u * ((r.inv & r.min_axis) == 0));
@@ -140,10 +131,10 @@ __device__ __forceinline__ bool ray_iterate(Ray &r, const DevPool &P, uint32_t *
                 h.push = r.push;
                 return true;
             }
-            stack[(uint32_t)(r.level - 1) * stride] = r.node;               // :357
+            stack[(uint32_t)(r.level - 1) * stride] = kPacked ? (r.node | (r.mask << 24)) : r.node;   // :357
             ++r.level;
-            r.node = child;
-            load_node(r, P, child);
+            r.node = kPacked ? (child & kIdMask) : child;
+            r.mask = child >> 24;
             r.dim >>= 1;                                                    // :361
             const float tm = ffrom(r.t_min);
             uint32_t nidx = 0;
@@ -183,8 +174,9 @@ __device__ __forceinline__ bool ray_iterate(Ray &r, const DevPool &P, uint32_t *
         h.push = r.push;
         return true;
     }
-    r.node = stack[(uint32_t)(r.level - 1) * stride];
-    load_node(r, P, r.node);              // consumed by the next PUSH; overlaps the STEP
+    const uint32_t e = stack[(uint32_t)(r.level - 1) * stride];
+    r.node = kPacked ? (e & kIdMask) : e;
+    r.mask = e >> 24;
 #pragma unroll
     for (int a = 0; a < 3; ++a) r.p[a] &= ~r.dim;
     r.dim <<= 1;
@@ -320,7 +312,7 @@ __device__ __forceinline__ void stamp(uint64_t *stamps, uint32_t cap, uint64_t t
 
 // ---------------------------------------------------------------- kernels
 
-template <class Src, class Sink, bool kCount>
+template <class Src, class Sink, bool kPacked, bool kCount>
 __global__ void k_trace_grid(DevPool P, Src S, Sink K, uint64_t *stamps, uint32_t stamp_cap)
 {
     extern __shared__ uint32_t lds_stack[];
@@ -330,16 +322,16 @@ __global__ void k_trace_grid(DevPool P, Src S, Sink K, uint64_t *stamps, uint32_
     uint32_t out;
     if (i < S.count() && S.get(i, o, d, out)) {
         Ray r;
-        ray_init(r, P, o, d);
+        ray_init<kPacked>(r, P, o, d);
         Hit h;
-        while (!ray_iterate<kCount>(r, P, lds_stack + threadIdx.x, blockDim.x, h)) {
+        while (!ray_iterate<kPacked, kCount>(r, P, lds_stack + threadIdx.x, blockDim.x, h)) {
         }
         K.put(out, h);
     }
     if (stamps) stamp(stamps, stamp_cap, t0, 64);
 }
 
-template <class Src, class Sink, bool kCount>
+template <class Src, class Sink, bool kPacked, bool kCount>
 __global__ void k_trace_persistent(DevPool P, Src S, Sink K, uint32_t *counter, int refill_min, uint64_t *stamps,
                                    uint32_t stamp_cap)
 {
@@ -366,7 +358,7 @@ __global__ void k_trace_persistent(DevPool P, Src S, Sink K, uint32_t *counter, 
                 const uint32_t i = base + (uint32_t)__popcll(idle & below);
                 float o[3], d[3];
                 if (i < n && S.get(i, o, d, out)) {
-                    ray_init(r, P, o, d);
+                    ray_init<kPacked>(r, P, o, d);
                     active = true;
                 }
             }
@@ -377,7 +369,7 @@ __global__ void k_trace_persistent(DevPool P, Src S, Sink K, uint32_t *counter, 
         }
         if (active) {
             Hit h;
-            if (ray_iterate<kCount>(r, P, stack, blockDim.x, h)) {
+            if (ray_iterate<kPacked, kCount>(r, P, stack, blockDim.x, h)) {
                 K.put(out, h);
                 active = false;
                 ++finished;
@@ -416,8 +408,8 @@ __global__ __launch_bounds__(256) void k_unshard(const uint32_t *__restrict__ ga
 
 size_t stack_bytes(int depth, int block) { return (size_t)(depth > 1 ? depth - 1 : 1) * block * sizeof(uint32_t); }
 
-template <class Src, class Sink, bool kCount>
-hipError_t launch(const DevPool &p, const Src &s, const Sink &k, uint32_t n, const Schedule &sc, hipStream_t stream)
+template <class Src, class Sink, bool kPacked, bool kCount>
+hipError_t launch_as(const DevPool &p, const Src &s, const Sink &k, uint32_t n, const Schedule &sc, hipStream_t stream)
 {
     if (n == 0) return hipSuccess;
     const int block = sc.block;
@@ -429,13 +421,20 @@ hipError_t launch(const DevPool &p, const Src &s, const Sink &k, uint32_t n, con
         uint32_t grid = (uint32_t)sc.cus * blocks_per_cu;
         const uint32_t needed = (n + block - 1) / block;
         if (grid > needed) grid = needed;
-        hipLaunchKernelGGL((k_trace_persistent<Src, Sink, kCount>), dim3(grid), dim3(block), lds, stream, p, s, k,
-                           sc.counter, sc.refill_min, sc.stamps, sc.stamp_cap);
+        hipLaunchKernelGGL((k_trace_persistent<Src, Sink, kPacked, kCount>), dim3(grid), dim3(block), lds, stream, p, s,
+                           k, sc.counter, sc.refill_min, sc.stamps, sc.stamp_cap);
     } else {
-        hipLaunchKernelGGL((k_trace_grid<Src, Sink, kCount>), dim3((n + block - 1) / block), dim3(block), lds, stream,
-                           p, s, k, sc.stamps, sc.stamp_cap);
+        hipLaunchKernelGGL((k_trace_grid<Src, Sink, kPacked, kCount>), dim3((n + block - 1) / block), dim3(block), lds,
+                           stream, p, s, k, sc.stamps, sc.stamp_cap);
     }
     return hipGetLastError();
+}
+
+template <class Src, class Sink, bool kCount>
+hipError_t launch(const DevPool &p, const Src &s, const Sink &k, uint32_t n, const Schedule &sc, hipStream_t stream)
+{
+    return p.packed ? launch_as<Src, Sink, true, kCount>(p, s, k, n, sc, stream)
+                    : launch_as<Src, Sink, false, kCount>(p, s, k, n, sc, stream);
 }
 
 }  // namespace
@@ -445,12 +444,12 @@ hipError_t occupancy_blocks_per_cu(int kind, int block, int depth, int *blocks)
     const size_t lds = stack_bytes(depth, block);
     switch (kind) {
     case 0:
-        return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, k_trace_grid<CameraSource, FrameSink, false>, block, lds);
+        return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, k_trace_grid<CameraSource, FrameSink, true, false>, block, lds);
     case 1:
-        return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, k_trace_persistent<CameraSource, FrameSink, false>,
+        return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, k_trace_persistent<CameraSource, FrameSink, true, false>,
                                                             block, lds);
     case 2:
-        return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, k_trace_grid<ArraySource, HitSink<false>, false>,
+        return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, k_trace_grid<ArraySource, HitSink<false>, true, false>,
                                                             block, lds);
     default:
         return hipErrorInvalidValue;

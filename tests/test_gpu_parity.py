@@ -55,9 +55,11 @@ def golden():
     return np.load(GOLD / "trace_d6.npz")
 
 
-def test_golden_vectors_intel_table(ort, gpu_device, golden, intel_lut):
+@pytest.mark.parametrize("layout", [0, 1])
+def test_golden_vectors_intel_table(ort, gpu_device, golden, intel_lut, layout):
     pool = ort.HOctree(golden["nodes"], int(golden["root"]), int(golden["depth"]), device=0)
     pool.set_rcp_lut(intel_lut)
+    pool.set_option("layout", layout)
     for name in ("cam", "rnd", "edge"):
         want = {"dir": golden[f"{name}_dir"], "voxel": golden[f"{name}_vox"], "t": golden[f"{name}_t"],
                 "push": golden[f"{name}_push"]}
@@ -92,8 +94,10 @@ def test_camera_frames_host_rcpps(ort, O, gpu_device, depth):
         rays = O.raygen(0.3, pitch, 1.25, 1920, 1080)
         ref = O.trace_batch(ref_pool, O.Rcp(None), ORIGIN, rays, nthreads=16, want_push=True)
         for sched in (0, 1):
-            pool.set_option("schedule", sched)
-            assert_same(gpu_trace_dev(pool, ORIGIN, rays), ref)
+            for layout in (0, 1):
+                pool.set_option("schedule", sched)
+                pool.set_option("layout", layout)
+                assert_same(gpu_trace_dev(pool, ORIGIN, rays), ref)
     pool.close()
 
 
@@ -108,7 +112,9 @@ def test_reference_hash_table_layout(ort, O, gpu_device):
     d = rng.uniform(-1, 1, (100000, 3)).astype(np.float32)
     d /= np.linalg.norm(d, axis=1, keepdims=True)
     ref = O.trace_batch(T.pool(), O.Rcp(None), o, d, nthreads=16, want_push=True)
-    assert_same(gpu_trace_dev(pool, o, d), ref)
+    for layout in (0, 1):
+        pool.set_option("layout", layout)
+        assert_same(gpu_trace_dev(pool, o, d), ref)
     rays = O.raygen(0.3, -0.6, 1.25, 640, 360)
     assert_same(gpu_trace_dev(pool, ORIGIN, rays), O.trace_batch(T.pool(), O.Rcp(None), ORIGIN, rays, want_push=True))
     pool.close()
@@ -144,6 +150,8 @@ def test_random_and_edge_rays_d10(ort, O, gpu_device):
     # unnormalised and tiny / huge directions
     d2 = d[:50000] * rng.choice(np.array([1e-20, 1e-5, 3.0, 1e20], np.float32), (50000, 1))
     assert_same(gpu_trace_dev(pool, o[:50000], d2), O.trace_batch(ref_pool, O.Rcp(None), o[:50000], d2, want_push=True))
+    pool.set_option("layout", 0)
+    assert_same(gpu_trace_dev(pool, eo, ed), O.trace_batch(ref_pool, O.Rcp(None), eo, ed, want_push=True))
     pool.close()
 
 
@@ -246,7 +254,9 @@ def test_pool_update_after_edits(ort, O, gpu_device):
     pool.update(lo + 1, after[lo:hi + 1], T.root)
     rays = O.raygen(0.1, -0.3, 1.25, 320, 180)
     ref = O.trace_batch(T.pool(), O.Rcp(None), ORIGIN, rays, want_push=True)
-    assert_same(gpu_trace_dev(pool, ORIGIN, rays), ref)
+    for layout in (1, 0):
+        pool.set_option("layout", layout)
+        assert_same(gpu_trace_dev(pool, ORIGIN, rays), ref)
     # an edit that would make a kernel read outside the pool is refused: the
     # root is an interior node, so its slots must name nodes of the pool
     bad = after[T.root - 1:T.root].copy()

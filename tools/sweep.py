@@ -93,7 +93,7 @@ def main():
         torch.cuda.synchronize()
         ref[p] = (hd.clone(), hv.clone(), ht.clone(), frame.clone())
 
-    variants = [("grid", 0, b, 0, 0) for b in (64, 128, 256, 512)]
+    variants = [("grid", 0, b, 0, 0) for b in (64, 128, 256, 512)] + [("grid-raw", 0, b, 0, 0) for b in (64, 256)]
     wpc = (16, 32) if a.quick else (8, 16, 24, 32)
     rf = (8, 32) if a.quick else (1, 8, 16, 32, 48, 64)
     for b, w, r in itertools.product((64, 256), wpc, rf):
@@ -102,6 +102,7 @@ def main():
     for name, sched, block, w, r in variants:
         pool.set_option("schedule", sched)
         pool.set_option("block", block)
+        pool.set_option("layout", 0 if name == "grid-raw" else 1)
         if sched:
             pool.set_option("waves_per_cu", w)
             pool.set_option("refill", r)
@@ -114,6 +115,11 @@ def main():
                        and torch.equal(frame, ref[p][3]))
             row[f"trace_ms_p{p}"] = round(tt, 4)
             row[f"render_ms_p{p}"] = round(tr, 4)
+        both = torch.empty(2 * n, dtype=torch.int32, device=dev)
+        tv = timed(lambda: pool.render_views_dev([cams[0.0], cams[-0.6]], both))
+        ok &= bool(torch.equal(both[:n], ref[0.0][3]) and torch.equal(both[n:], ref[-0.6][3]))
+        row["render2_ms"] = round(tv, 4)
+        row["render2_mrays_s"] = round(2 * n / tv / 1e3, 1)
         row["trace_mrays_s"] = round(2 * n / (row["trace_ms_p0.0"] + row["trace_ms_p-0.6"]) / 1e3, 1)
         row["render_mrays_s"] = round(2 * n / (row["render_ms_p0.0"] + row["render_ms_p-0.6"]) / 1e3, 1)
         row["bit_exact_vs_grid"] = ok
@@ -122,6 +128,7 @@ def main():
     # residency of the default grid and of the best persistent variant
     best = max((r for r in results if r["schedule"] == "persistent"), key=lambda r: r["render_mrays_s"])
     res = {}
+    pool.set_option("layout", 1)
     for tag, cfg in (("grid256", (0, 256, 0, 0)), ("best_persistent", (1, best["block"], best["waves_per_cu"], best["refill"]))):
         pool.set_option("schedule", cfg[0])
         pool.set_option("block", cfg[1])
