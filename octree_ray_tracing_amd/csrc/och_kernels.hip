@@ -62,20 +62,42 @@ struct Hit {
 // Traversal state of one ray between iterations.
 struct Ray {
     float c[3], b[3];     // coefficient (RCPPS of -|d|) and bias (-c * o') per axis
+    uint32_t nan_or[3];   // 0xFFC00000 where c is +-inf (t is NaN at every STEP), else 0
     uint32_t p[3];        // position bits in the reflected frame
     uint32_t inv;         // direction-sign mask (1 = positive)
     uint32_t idx;         // child index bits at the current level
     uint32_t dim;         // mantissa bit of the current child size
     uint32_t node;
     uint32_t mask;        // packed layout: non-empty children of `node`
+    uint4 ka, kb;         // packed layout: the eight slots of `node` (see load_record)
     uint32_t t_min;       // bits of the entry t of the current cell
     uint32_t min_axis;    // 1, 2, 4 (last STEP axis) or 8 (none yet)
     int level;
-    bool stepping;        // next iteration starts at STEP (after a failed PUSH or a POP)
     uint32_t push;
 };
 
 constexpr uint32_t kIdMask = 0x00FFFFFFu;
+
+// Packed layout: the slots of the current node live in VGPRs.  They are read
+// only by the next descent or hit -- the PUSH test itself uses `mask`, which
+// came with the node's id from its parent's slot -- so the load overlaps the
+// PUSH tests, STEPs and POPs in between.
+__device__ __forceinline__ void load_record(Ray &r, const DevPool &P, uint32_t v)
+{
+    const uint4 *q = reinterpret_cast<const uint4 *>(P.nodes + 8u * v);
+    r.ka = q[0];
+    r.kb = q[1];
+}
+
+// Slot k of the held record: a 3-level select, no indexed register access.
+__device__ __forceinline__ uint32_t slot_of(const Ray &r, uint32_t k)
+{
+    const bool b0 = k & 1u, b1 = k & 2u;
+    const uint32_t s01 = b0 ? r.ka.y : r.ka.x, s23 = b0 ? r.ka.w : r.ka.z;
+    const uint32_t s45 = b0 ? r.kb.y : r.kb.x, s67 = b0 ? r.kb.w : r.kb.z;
+    const uint32_t lo = b1 ? s23 : s01, hi = b1 ? s67 : s45;
+    return (k & 4u) ? hi : lo;
+}
 
 // Setup, ORT/och_h_octree.h:294-338.
 template <bool kPacked>
@@ -89,99 +111,109 @@ __device__ __forceinline__ void ray_init(Ray &r, const DevPool &P, const float *
         const bool positive = (int32_t)db > 0 && db <= 0x7F800000u;          // 0 < d, :310
         r.inv |= (uint32_t)positive << a;
         const float refl = fabsf(__fsub_rn(positive ? 3.0F : 0.0F, o[a]));   // :314
-        r.c[a] = ffrom(rcpps(db | 0x80000000u, P.lut, P.lut_shift));         // :312, :316
+        const uint32_t cb = rcpps(db | 0x80000000u, P.lut, P.lut_shift);     // :312, :316
+        r.c[a] = ffrom(cb);
         r.b[a] = ffrom(fbits(__fmul_rn(r.c[a], refl)) ^ 0x80000000u);       // :318
+        // fma(p, -inf, +inf) is NaN for every p: x86 gives 0xFFC00000, gfx950
+        // 0x7FC00000; OR-ing 0xFFC00000 into t restores x86's pattern for the
+        // unsigned compare of STEP (:384-406).  A finite c never yields NaN.
+        r.nan_or[a] = ((cb & 0x7FFFFFFFu) == 0x7F800000u) ? kX86DefaultNaN : 0u;
         r.p[a] = fbits(refl) & 0x3FC00000u;                                 // :320
         r.idx |= (uint32_t)(r.p[a] == 0x3FC00000u) << a;                    // :324
     }
     r.dim = 1u << 22;                                                       // :326
     r.node = kPacked ? (P.root & kIdMask) : P.root;
     r.mask = P.root >> 24;
+    if (kPacked) load_record(r, P, r.node);
     r.t_min = 0;                                                            // +0.0F
     r.level = 1;
     r.min_axis = 8;
-    r.stepping = false;
     r.push = 0;
 }
 
-// One iteration of the PUSH / STEP / POP machine (ORT/och_h_octree.h:342-446,
-// ORT/och_octree.cpp:217-319): one PUSH, or one STEP possibly followed by a
-// POP.  Returns true when the ray has finished (h filled).
+// One PUSH of the PUSH / STEP / POP machine (ORT/och_h_octree.h:342-446,
+// ORT/och_octree.cpp:217-319) and, when the PUSH finds no child, the STEP /
+// POP cascade that follows it, run in registers until a sibling advance.
+// Returns true when the ray has finished (h filled).
 // stack: this lane's first LDS slot, levels `stride` words apart.
 template <bool kPacked, bool kCount>
 __device__ __forceinline__ bool ray_iterate(Ray &r, const DevPool &P, uint32_t *stack, uint32_t stride, Hit &h)
 {
-    if (!r.stepping) {                                                       // PUSH :342
-        if (kCount) ++r.push;
-        const uint32_t c = (r.idx ^ r.inv) & 7u;
-        uint32_t child = 0;
-        bool present;
-        if (kPacked) {
-            present = (r.mask >> c) & 1u;
-        } else {
-            child = P.nodes[8u * r.node + c];
-            present = child != 0;
-        }
-        if (present) {
-            if (kPacked) child = P.nodes[8u * r.node + c];
-            if (r.level == P.depth) {                                       // HIT :346-355
-                h.voxel = child;
-                h.dir = (int32_t)((r.min_axis >> 1) + 3u * ((r.inv & r.min_axis) == 0));
-                h.t = r.t_min;
-                h.push = r.push;
-                return true;
-            }
-            stack[(uint32_t)(r.level - 1) * stride] = kPacked ? (r.node | (r.mask << 24)) : r.node;   // :357
-            ++r.level;
-            r.node = kPacked ? (child & kIdMask) : child;
-            r.mask = child >> 24;
-            r.dim >>= 1;                                                    // :361
-            const float tm = ffrom(r.t_min);
-            uint32_t nidx = 0;
-#pragma unroll
-            for (int a = 0; a < 3; ++a) {                                   // :363-373
-                const float t_mid = __builtin_fmaf(ffrom(r.p[a] | r.dim), r.c[a], r.b[a]);
-                const bool upper = t_mid >= tm;
-                nidx |= (uint32_t)upper << a;
-                r.p[a] |= upper ? r.dim : 0u;
-            }
-            r.idx = nidx;
-            return false;
-        }
-        r.stepping = true;
+    // PUSH :342-376
+    if (kCount) ++r.push;
+    const uint32_t c = (r.idx ^ r.inv) & 7u;
+    uint32_t child = 0;
+    bool present;
+    if (kPacked) {
+        present = (r.mask >> c) & 1u;
+    } else {
+        child = P.nodes[8u * r.node + c];
+        present = child != 0;
     }
-    // STEP :378-419
-    const uint32_t tx = t_bits(__builtin_fmaf(ffrom(r.p[0]), r.c[0], r.b[0]));
-    const uint32_t ty = t_bits(__builtin_fmaf(ffrom(r.p[1]), r.c[1], r.b[1]));
-    const uint32_t tz = t_bits(__builtin_fmaf(ffrom(r.p[2]), r.c[2], r.b[2]));
-    const bool sx = tx <= ty && tx <= tz;
-    const bool sy = !sx && ty < tx && ty <= tz;
-    r.min_axis = sx ? 1u : (sy ? 2u : 4u);
-    r.t_min = sx ? tx : (sy ? ty : tz);
-    if (r.idx & r.min_axis) {                                               // advance :413-419
-        if (sx) r.p[0] &= ~r.dim;
-        else if (sy) r.p[1] &= ~r.dim;
-        else r.p[2] &= ~r.dim;
-        r.idx ^= r.min_axis;
-        r.stepping = false;
+    if (present) {
+        if (kPacked) child = slot_of(r, c);
+        if (r.level == P.depth) {                                           // HIT :346-355
+            h.voxel = child;
+            h.dir = (int32_t)((r.min_axis >> 1) + 3u * ((r.inv & r.min_axis) == 0));
+            h.t = r.t_min;
+            h.push = r.push;
+            return true;
+        }
+        stack[(uint32_t)(r.level - 1) * stride] = kPacked ? (r.node | (r.mask << 24)) : r.node;   // :357
+        ++r.level;
+        r.node = kPacked ? (child & kIdMask) : child;
+        r.mask = child >> 24;
+        if (kPacked) load_record(r, P, r.node);
+        r.dim >>= 1;                                                        // :361
+        const float tm = ffrom(r.t_min);
+        uint32_t nidx = 0;
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {                                       // :363-373
+            const float t_mid = __builtin_fmaf(ffrom(r.p[a] | r.dim), r.c[a], r.b[a]);
+            const bool upper = t_mid >= tm;
+            nidx |= (uint32_t)upper << a;
+            r.p[a] |= upper ? r.dim : 0u;
+        }
+        r.idx = nidx;
         return false;
     }
-    // POP :421-446
-    if (--r.level == 0) {
-        h.voxel = 0;
-        h.dir = OCH_EXIT;
-        h.t = P.miss_bits;
-        h.push = r.push;
-        return true;
-    }
-    const uint32_t e = stack[(uint32_t)(r.level - 1) * stride];
-    r.node = kPacked ? (e & kIdMask) : e;
-    r.mask = e >> 24;
+    // STEP :378-419, POP :421-446, repeated until an advance or the exit.
+    bool popped = false;
+    for (;;) {
+        const uint32_t tx = fbits(__builtin_fmaf(ffrom(r.p[0]), r.c[0], r.b[0])) | r.nan_or[0];
+        const uint32_t ty = fbits(__builtin_fmaf(ffrom(r.p[1]), r.c[1], r.b[1])) | r.nan_or[1];
+        const uint32_t tz = fbits(__builtin_fmaf(ffrom(r.p[2]), r.c[2], r.b[2])) | r.nan_or[2];
+        const bool sx = tx <= ty && tx <= tz;
+        const bool sy = !sx && ty < tx && ty <= tz;
+        r.min_axis = sx ? 1u : (sy ? 2u : 4u);
+        r.t_min = sx ? tx : (sy ? ty : tz);
+        if (r.idx & r.min_axis) {                                           // advance :413-419
+            if (sx) r.p[0] &= ~r.dim;
+            else if (sy) r.p[1] &= ~r.dim;
+            else r.p[2] &= ~r.dim;
+            r.idx ^= r.min_axis;
+            break;
+        }
+        if (--r.level == 0) {                                               // MISS :423-431
+            h.voxel = 0;
+            h.dir = OCH_EXIT;
+            h.t = P.miss_bits;
+            h.push = r.push;
+            return true;
+        }
 #pragma unroll
-    for (int a = 0; a < 3; ++a) r.p[a] &= ~r.dim;
-    r.dim <<= 1;
-    r.idx = (uint32_t)((r.p[0] & r.dim) != 0) | ((uint32_t)((r.p[1] & r.dim) != 0) << 1) |
-            ((uint32_t)((r.p[2] & r.dim) != 0) << 2);
+        for (int a = 0; a < 3; ++a) r.p[a] &= ~r.dim;                       // :436
+        r.dim <<= 1;                                                        // :438
+        r.idx = (uint32_t)((r.p[0] & r.dim) != 0) | ((uint32_t)((r.p[1] & r.dim) != 0) << 1) |
+                ((uint32_t)((r.p[2] & r.dim) != 0) << 2);                   // :440-444
+        popped = true;
+    }
+    if (popped) {                                                           // the parent (:434), once
+        const uint32_t e = stack[(uint32_t)(r.level - 1) * stride];
+        r.node = kPacked ? (e & kIdMask) : e;
+        r.mask = e >> 24;
+        if (kPacked) load_record(r, P, r.node);
+    }
     return false;
 }
 
