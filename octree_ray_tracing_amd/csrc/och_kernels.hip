@@ -44,14 +44,6 @@ __device__ __forceinline__ uint32_t rcpps(uint32_t x, const uint32_t *__restrict
     return ne <= 0 ? sign : (sign | ((uint32_t)ne << 23) | (ent & 0x7FFFFFu));
 }
 
-// The t compare of STEP is on raw bit patterns (ORT/och_h_octree.h:384-406);
-// x86 produces 0xFFC00000 for fma(p, -inf, +inf), gfx950 0x7FC00000.
-__device__ __forceinline__ uint32_t t_bits(float t)
-{
-    const uint32_t u = fbits(t);
-    return ((u & 0x7FFFFFFFu) > 0x7F800000u) ? kX86DefaultNaN : u;
-}
-
 struct Hit {
     int32_t dir;
     uint32_t voxel;
@@ -73,6 +65,7 @@ struct Ray {
     uint32_t t_min;       // bits of the entry t of the current cell
     uint32_t min_axis;    // 1, 2, 4 (last STEP axis) or 8 (none yet)
     int level;
+    bool stepping;        // next iteration starts at STEP (after a failed PUSH or a POP)
     uint32_t push;
 };
 
@@ -128,58 +121,62 @@ __device__ __forceinline__ void ray_init(Ray &r, const DevPool &P, const float *
     r.t_min = 0;                                                            // +0.0F
     r.level = 1;
     r.min_axis = 8;
+    r.stepping = false;
     r.push = 0;
 }
 
-// One PUSH of the PUSH / STEP / POP machine (ORT/och_h_octree.h:342-446,
-// ORT/och_octree.cpp:217-319) and, when the PUSH finds no child, the STEP /
-// POP cascade that follows it, run in registers until a sibling advance.
-// Returns true when the ray has finished (h filled).
+// One iteration of the PUSH / STEP / POP machine (ORT/och_h_octree.h:342-446,
+// ORT/och_octree.cpp:217-319): one PUSH, or one STEP possibly followed by a
+// POP -- a flat iteration, so lanes in different states progress together.
+// Returns true when the ray has finished (h filled).  The packed record of a
+// node entered by a descent or a POP is loaded at one site at the end.
 // stack: this lane's first LDS slot, levels `stride` words apart.
 template <bool kPacked, bool kCount>
 __device__ __forceinline__ bool ray_iterate(Ray &r, const DevPool &P, uint32_t *stack, uint32_t stride, Hit &h)
 {
-    // PUSH :342-376
-    if (kCount) ++r.push;
-    const uint32_t c = (r.idx ^ r.inv) & 7u;
-    uint32_t child = 0;
-    bool present;
-    if (kPacked) {
-        present = (r.mask >> c) & 1u;
-    } else {
-        child = P.nodes[8u * r.node + c];
-        present = child != 0;
-    }
-    if (present) {
-        if (kPacked) child = slot_of(r, c);
-        if (r.level == P.depth) {                                           // HIT :346-355
-            h.voxel = child;
-            h.dir = (int32_t)((r.min_axis >> 1) + 3u * ((r.inv & r.min_axis) == 0));
-            h.t = r.t_min;
-            h.push = r.push;
-            return true;
+    bool enter = false;                       // a new node: (re)load its record
+    if (!r.stepping) {                                                       // PUSH :342
+        if (kCount) ++r.push;
+        const uint32_t c = (r.idx ^ r.inv) & 7u;
+        uint32_t child = 0;
+        bool present;
+        if (kPacked) {
+            present = (r.mask >> c) & 1u;
+        } else {
+            child = P.nodes[8u * r.node + c];
+            present = child != 0;
         }
-        stack[(uint32_t)(r.level - 1) * stride] = kPacked ? (r.node | (r.mask << 24)) : r.node;   // :357
-        ++r.level;
-        r.node = kPacked ? (child & kIdMask) : child;
-        r.mask = child >> 24;
-        if (kPacked) load_record(r, P, r.node);
-        r.dim >>= 1;                                                        // :361
-        const float tm = ffrom(r.t_min);
-        uint32_t nidx = 0;
+        if (present) {
+            if (kPacked) child = slot_of(r, c);
+            if (r.level == P.depth) {                                       // HIT :346-355
+                h.voxel = child;
+                h.dir = (int32_t)((r.min_axis >> 1) + 3u * ((r.inv & r.min_axis) == 0));
+                h.t = r.t_min;
+                h.push = r.push;
+                return true;
+            }
+            stack[(uint32_t)(r.level - 1) * stride] = kPacked ? (r.node | (r.mask << 24)) : r.node;   // :357
+            ++r.level;
+            r.node = kPacked ? (child & kIdMask) : child;
+            r.mask = child >> 24;
+            r.dim >>= 1;                                                    // :361
+            const float tm = ffrom(r.t_min);
+            uint32_t nidx = 0;
 #pragma unroll
-        for (int a = 0; a < 3; ++a) {                                       // :363-373
-            const float t_mid = __builtin_fmaf(ffrom(r.p[a] | r.dim), r.c[a], r.b[a]);
-            const bool upper = t_mid >= tm;
-            nidx |= (uint32_t)upper << a;
-            r.p[a] |= upper ? r.dim : 0u;
+            for (int a = 0; a < 3; ++a) {                                   // :363-373
+                const float t_mid = __builtin_fmaf(ffrom(r.p[a] | r.dim), r.c[a], r.b[a]);
+                const bool upper = t_mid >= tm;
+                nidx |= (uint32_t)upper << a;
+                r.p[a] |= upper ? r.dim : 0u;
+            }
+            r.idx = nidx;
+            enter = true;
+        } else {
+            r.stepping = true;
         }
-        r.idx = nidx;
-        return false;
     }
-    // STEP :378-419, POP :421-446, repeated until an advance or the exit.
-    bool popped = false;
-    for (;;) {
+    if (r.stepping) {
+        // STEP :378-419
         const uint32_t tx = fbits(__builtin_fmaf(ffrom(r.p[0]), r.c[0], r.b[0])) | r.nan_or[0];
         const uint32_t ty = fbits(__builtin_fmaf(ffrom(r.p[1]), r.c[1], r.b[1])) | r.nan_or[1];
         const uint32_t tz = fbits(__builtin_fmaf(ffrom(r.p[2]), r.c[2], r.b[2])) | r.nan_or[2];
@@ -192,28 +189,27 @@ __device__ __forceinline__ bool ray_iterate(Ray &r, const DevPool &P, uint32_t *
             else if (sy) r.p[1] &= ~r.dim;
             else r.p[2] &= ~r.dim;
             r.idx ^= r.min_axis;
-            break;
-        }
-        if (--r.level == 0) {                                               // MISS :423-431
-            h.voxel = 0;
-            h.dir = OCH_EXIT;
-            h.t = P.miss_bits;
-            h.push = r.push;
-            return true;
-        }
+            r.stepping = false;
+        } else {
+            if (--r.level == 0) {                                           // MISS :423-431
+                h.voxel = 0;
+                h.dir = OCH_EXIT;
+                h.t = P.miss_bits;
+                h.push = r.push;
+                return true;
+            }
+            const uint32_t e = stack[(uint32_t)(r.level - 1) * stride];      // POP :434
+            r.node = kPacked ? (e & kIdMask) : e;
+            r.mask = e >> 24;
 #pragma unroll
-        for (int a = 0; a < 3; ++a) r.p[a] &= ~r.dim;                       // :436
-        r.dim <<= 1;                                                        // :438
-        r.idx = (uint32_t)((r.p[0] & r.dim) != 0) | ((uint32_t)((r.p[1] & r.dim) != 0) << 1) |
-                ((uint32_t)((r.p[2] & r.dim) != 0) << 2);                   // :440-444
-        popped = true;
+            for (int a = 0; a < 3; ++a) r.p[a] &= ~r.dim;                   // :436
+            r.dim <<= 1;                                                    // :438
+            r.idx = (uint32_t)((r.p[0] & r.dim) != 0) | ((uint32_t)((r.p[1] & r.dim) != 0) << 1) |
+                    ((uint32_t)((r.p[2] & r.dim) != 0) << 2);               // :440-444
+            enter = true;
+        }
     }
-    if (popped) {                                                           // the parent (:434), once
-        const uint32_t e = stack[(uint32_t)(r.level - 1) * stride];
-        r.node = kPacked ? (e & kIdMask) : e;
-        r.mask = e >> 24;
-        if (kPacked) load_record(r, P, r.node);
-    }
+    if (kPacked && enter) load_record(r, P, r.node);
     return false;
 }
 
