@@ -133,7 +133,7 @@ struct och_gpu_pool {
     hipEvent_t ev_start = nullptr, ev_stop = nullptr;
     bool timed = false;
     // schedule (och_gpu_set_option)
-    int opt_schedule = 0, opt_block = 256, opt_waves_per_cu = 32, opt_refill = 16;
+    int opt_schedule = 0, opt_block = 64, opt_waves_per_cu = 32, opt_refill = 16;
     int cus = 256;
     uint32_t *d_counter = nullptr;
     uint64_t *stamps = nullptr;

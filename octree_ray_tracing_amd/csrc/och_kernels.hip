@@ -61,36 +61,15 @@ struct Ray {
     uint32_t dim;         // mantissa bit of the current child size
     uint32_t node;
     uint32_t mask;        // packed layout: non-empty children of `node`
-    uint4 ka, kb;         // packed layout: the eight slots of `node` (see load_record)
     uint32_t t_min;       // bits of the entry t of the current cell
     uint32_t min_axis;    // 1, 2, 4 (last STEP axis) or 8 (none yet)
-    int level;
+    uint32_t voxel;       // the hit voxel id (valid once level > depth)
+    int level;            // 1..depth while walking; 0 after a miss, depth + 1 after a hit
     bool stepping;        // next iteration starts at STEP (after a failed PUSH or a POP)
     uint32_t push;
 };
 
 constexpr uint32_t kIdMask = 0x00FFFFFFu;
-
-// Packed layout: the slots of the current node live in VGPRs.  They are read
-// only by the next descent or hit -- the PUSH test itself uses `mask`, which
-// came with the node's id from its parent's slot -- so the load overlaps the
-// PUSH tests, STEPs and POPs in between.
-__device__ __forceinline__ void load_record(Ray &r, const DevPool &P, uint32_t v)
-{
-    const uint4 *q = reinterpret_cast<const uint4 *>(P.nodes + 8u * v);
-    r.ka = q[0];
-    r.kb = q[1];
-}
-
-// Slot k of the held record: a 3-level select, no indexed register access.
-__device__ __forceinline__ uint32_t slot_of(const Ray &r, uint32_t k)
-{
-    const bool b0 = k & 1u, b1 = k & 2u;
-    const uint32_t s01 = b0 ? r.ka.y : r.ka.x, s23 = b0 ? r.ka.w : r.ka.z;
-    const uint32_t s45 = b0 ? r.kb.y : r.kb.x, s67 = b0 ? r.kb.w : r.kb.z;
-    const uint32_t lo = b1 ? s23 : s01, hi = b1 ? s67 : s45;
-    return (k & 4u) ? hi : lo;
-}
 
 // Setup, ORT/och_h_octree.h:294-338.
 template <bool kPacked>
@@ -117,10 +96,10 @@ __device__ __forceinline__ void ray_init(Ray &r, const DevPool &P, const float *
     r.dim = 1u << 22;                                                       // :326
     r.node = kPacked ? (P.root & kIdMask) : P.root;
     r.mask = P.root >> 24;
-    if (kPacked) load_record(r, P, r.node);
     r.t_min = 0;                                                            // +0.0F
     r.level = 1;
     r.min_axis = 8;
+    r.voxel = 0;
     r.stepping = false;
     r.push = 0;
 }
@@ -128,31 +107,30 @@ __device__ __forceinline__ void ray_init(Ray &r, const DevPool &P, const float *
 // One iteration of the PUSH / STEP / POP machine (ORT/och_h_octree.h:342-446,
 // ORT/och_octree.cpp:217-319): one PUSH, or one STEP possibly followed by a
 // POP -- a flat iteration, so lanes in different states progress together.
-// Returns true when the ray has finished (h filled).  The packed record of a
-// node entered by a descent or a POP is loaded at one site at the end.
+// The only global load is the child's slot word on a PUSH: every one in the
+// raw layout, only when the held child mask says "present" in the packed
+// layout.  Returns true when the ray has finished (see ray_result).
 // stack: this lane's first LDS slot, levels `stride` words apart.
 template <bool kPacked, bool kCount>
-__device__ __forceinline__ bool ray_iterate(Ray &r, const DevPool &P, uint32_t *stack, uint32_t stride, Hit &h)
+__device__ __forceinline__ bool ray_iterate(Ray &r, const DevPool &P, uint32_t *stack, uint32_t stride)
 {
-    bool enter = false;                       // a new node: (re)load its record
     if (!r.stepping) {                                                       // PUSH :342
         if (kCount) ++r.push;
         const uint32_t c = (r.idx ^ r.inv) & 7u;
+        const uint32_t *slot = P.nodes + 8u * r.node + c;
         uint32_t child = 0;
         bool present;
         if (kPacked) {
             present = (r.mask >> c) & 1u;
+            if (present) child = *slot;
         } else {
-            child = P.nodes[8u * r.node + c];
+            child = *slot;
             present = child != 0;
         }
         if (present) {
-            if (kPacked) child = slot_of(r, c);
             if (r.level == P.depth) {                                       // HIT :346-355
-                h.voxel = child;
-                h.dir = (int32_t)((r.min_axis >> 1) + 3u * ((r.inv & r.min_axis) == 0));
-                h.t = r.t_min;
-                h.push = r.push;
+                r.voxel = child;
+                r.level = P.depth + 1;
                 return true;
             }
             stack[(uint32_t)(r.level - 1) * stride] = kPacked ? (r.node | (r.mask << 24)) : r.node;   // :357
@@ -170,47 +148,59 @@ __device__ __forceinline__ bool ray_iterate(Ray &r, const DevPool &P, uint32_t *
                 r.p[a] |= upper ? r.dim : 0u;
             }
             r.idx = nidx;
-            enter = true;
-        } else {
-            r.stepping = true;
+            return false;
         }
+        r.stepping = true;
     }
-    if (r.stepping) {
-        // STEP :378-419
-        const uint32_t tx = fbits(__builtin_fmaf(ffrom(r.p[0]), r.c[0], r.b[0])) | r.nan_or[0];
-        const uint32_t ty = fbits(__builtin_fmaf(ffrom(r.p[1]), r.c[1], r.b[1])) | r.nan_or[1];
-        const uint32_t tz = fbits(__builtin_fmaf(ffrom(r.p[2]), r.c[2], r.b[2])) | r.nan_or[2];
-        const bool sx = tx <= ty && tx <= tz;
-        const bool sy = !sx && ty < tx && ty <= tz;
-        r.min_axis = sx ? 1u : (sy ? 2u : 4u);
-        r.t_min = sx ? tx : (sy ? ty : tz);
-        if (r.idx & r.min_axis) {                                           // advance :413-419
-            if (sx) r.p[0] &= ~r.dim;
-            else if (sy) r.p[1] &= ~r.dim;
-            else r.p[2] &= ~r.dim;
-            r.idx ^= r.min_axis;
-            r.stepping = false;
-        } else {
-            if (--r.level == 0) {                                           // MISS :423-431
-                h.voxel = 0;
-                h.dir = OCH_EXIT;
-                h.t = P.miss_bits;
-                h.push = r.push;
-                return true;
-            }
-            const uint32_t e = stack[(uint32_t)(r.level - 1) * stride];      // POP :434
-            r.node = kPacked ? (e & kIdMask) : e;
-            r.mask = e >> 24;
+    // STEP :378-419.  The reference's cascade (x if tx <= ty && tx <= tz, else
+    // y if ty < tx && ty <= tz, else z) picks the first axis holding the
+    // unsigned minimum.
+    const uint32_t tx = fbits(__builtin_fmaf(ffrom(r.p[0]), r.c[0], r.b[0])) | r.nan_or[0];
+    const uint32_t ty = fbits(__builtin_fmaf(ffrom(r.p[1]), r.c[1], r.b[1])) | r.nan_or[1];
+    const uint32_t tz = fbits(__builtin_fmaf(ffrom(r.p[2]), r.c[2], r.b[2])) | r.nan_or[2];
+    const uint32_t tm = min(min(tx, ty), tz);
+    const bool sx = tx == tm;
+    const bool sy = !sx && ty == tm;
+    const bool sz = !sx && !sy;
+    const uint32_t axis = sx ? 1u : (sy ? 2u : 4u);
+    r.min_axis = axis;
+    r.t_min = tm;
+    if (r.idx & axis) {                                                     // advance :413-419
+        const uint32_t clr = ~r.dim;
+        r.p[0] &= sx ? clr : 0xFFFFFFFFu;
+        r.p[1] &= sy ? clr : 0xFFFFFFFFu;
+        r.p[2] &= sz ? clr : 0xFFFFFFFFu;
+        r.idx ^= axis;
+        r.stepping = false;
+        return false;
+    }
+    if (--r.level == 0) return true;                                        // MISS :423-431
+    const uint32_t e = stack[(uint32_t)(r.level - 1) * stride];              // POP :434
+    r.node = kPacked ? (e & kIdMask) : e;
+    r.mask = e >> 24;
 #pragma unroll
-            for (int a = 0; a < 3; ++a) r.p[a] &= ~r.dim;                   // :436
-            r.dim <<= 1;                                                    // :438
-            r.idx = (uint32_t)((r.p[0] & r.dim) != 0) | ((uint32_t)((r.p[1] & r.dim) != 0) << 1) |
-                    ((uint32_t)((r.p[2] & r.dim) != 0) << 2);               // :440-444
-            enter = true;
-        }
-    }
-    if (kPacked && enter) load_record(r, P, r.node);
+    for (int a = 0; a < 3; ++a) r.p[a] &= ~r.dim;                           // :436
+    r.dim <<= 1;                                                            // :438
+    r.idx = (uint32_t)((r.p[0] & r.dim) != 0) | ((uint32_t)((r.p[1] & r.dim) != 0) << 1) |
+            ((uint32_t)((r.p[2] & r.dim) != 0) << 2);                       // :440-444
     return false;
+}
+
+// The hit record of a finished ray (:346-355 hit, :423-431 miss).
+__device__ __forceinline__ Hit ray_result(const Ray &r, const DevPool &P)
+{
+    Hit h;
+    if (r.level == 0) {
+        h.dir = OCH_EXIT;
+        h.voxel = 0;
+        h.t = P.miss_bits;
+    } else {
+        h.dir = (int32_t)((r.min_axis >> 1) + 3u * ((r.inv & r.min_axis) == 0));
+        h.voxel = r.voxel;
+        h.t = r.t_min;
+    }
+    h.push = r.push;
+    return h;
 }
 
 // ---------------------------------------------------------------- sources
@@ -351,10 +341,9 @@ __global__ void k_trace_grid(DevPool P, Src S, Sink K, uint64_t *stamps, uint32_
     if (i < S.count() && S.get(i, o, d, out)) {
         Ray r;
         ray_init<kPacked>(r, P, o, d);
-        Hit h;
-        while (!ray_iterate<kPacked, kCount>(r, P, lds_stack + threadIdx.x, blockDim.x, h)) {
+        while (!ray_iterate<kPacked, kCount>(r, P, lds_stack + threadIdx.x, blockDim.x)) {
         }
-        K.put(out, h);
+        K.put(out, ray_result(r, P));
     }
     if (stamps) stamp(stamps, stamp_cap, t0, 64);
 }
@@ -396,9 +385,8 @@ __global__ void k_trace_persistent(DevPool P, Src S, Sink K, uint32_t *counter, 
             continue;
         }
         if (active) {
-            Hit h;
-            if (ray_iterate<kPacked, kCount>(r, P, stack, blockDim.x, h)) {
-                K.put(out, h);
+            if (ray_iterate<kPacked, kCount>(r, P, stack, blockDim.x)) {
+                K.put(out, ray_result(r, P));
                 active = false;
                 ++finished;
             }
