@@ -130,6 +130,9 @@ def main():
     ap.add_argument("--row-chunk", type=int, default=8)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=8.0)
+    ap.add_argument("--inflight", type=int, default=3,
+                    help="frames in flight: steps alternate over this many HIP streams, so one step's "
+                         "slowest rays overlap the next step's bulk (1 = serialised)")
     a = ap.parse_args()
 
     import torch
@@ -155,8 +158,15 @@ def main():
     pool.set_palette(ort.VoxelData().get_colours())
     stream = torch.cuda.current_stream()
     pool.set_stream(stream)
-    sf = ShardedFrame(pool, W, H, a.row_chunk, n_views=len(PITCHES))
     cams = [ort.camera(ORIGIN, YAW, p, FOV, W, H) for p in PITCHES]
+    # One frame buffer set and one HIP stream per frame in flight.
+    streams = [stream] + [torch.cuda.Stream(device=dev) for _ in range(max(1, a.inflight) - 1)]
+    sfs = []
+    for s_ in streams:
+        with torch.cuda.stream(s_):
+            sfs.append(ShardedFrame(pool, W, H, a.row_chunk, n_views=len(PITCHES)))
+    pool.set_stream(stream)
+    sf = sfs[0]
 
     # PUSH counts of this rank's rays (for the algorithmic byte count): trace
     # the rank's own rows once with counting on; not part of the timed region.
@@ -197,27 +207,44 @@ def main():
                       "bytes_per_ray": 12 + 12 + 4 * push_total / (W * H * len(cams))}
         del hd, hv, ht, hp
 
+    def step(k, ev=None):
+        """One step: render both views of this rank's rows, all-gather, unshard --
+        on stream k % inflight, into that stream's own frame buffers."""
+        s_, f_ = streams[k % len(streams)], sfs[k % len(sfs)]
+        pool.set_stream(s_)
+        with torch.cuda.stream(s_):
+            if ev is not None:
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(s_)
+            f_.render_local(cams)
+            if ev is not None:
+                e1.record(s_)
+                ev.append((e0, e1))
+            f_.exchange()
+
+    # Frame latency: the render launch alone on an otherwise idle GPU.
+    lat = []
+    for k in range(max(a.warmup, 1) + 5):
+        step(0, lat if k >= max(a.warmup, 1) else None)
+        torch.cuda.synchronize()
+    latency_ms = float(np.median([x.elapsed_time(y) for x, y in lat]))
     # warmup
-    for _ in range(a.warmup):
-        sf.render(cams)
+    for k in range(a.warmup):
+        step(k)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     ev = []
     t0 = time.perf_counter()
-    for _ in range(a.steps):
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record(stream)
-        sf.render_local(cams)
-        e1.record(stream)
-        sf.exchange()
-        ev.append((e0, e1))
+    for k in range(a.steps):
+        step(k, ev)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    pool.set_stream(stream)
     kms = np.array([x.elapsed_time(y) for x, y in ev])
     t_max = torch.tensor([elapsed], dtype=torch.float64, device=dev)
     if world > 1:
@@ -265,6 +292,7 @@ def main():
                          "frac": round(achieved / HBM_PEAK_GBS, 5),
                          "traffic": None if pmc is None else pmc.get("hbm_bytes_per_launch"),
                          "kernel": "k_trace_grid<CameraSource,FrameSink> (2 views per launch)", "kernel_ms": round(k_avg_ms, 4),
+                         "kernel_ms_idle_gpu": round(latency_ms, 4), "frames_in_flight": len(streams),
                          "bytes_per_launch": int(bytes_per_launch),
                          "push_per_ray": round(push_total / rays_rank, 3),
                          "note": "pointer-chase over an L2/MALL-resident DAG: latency/VALU-bound, not HBM-bound"},

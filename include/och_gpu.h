@@ -131,9 +131,11 @@ typedef enum och_option {
     OCH_OPT_BLOCK = 1,         /* threads per workgroup: 64..1024, multiple of 64 (default 256) */
     OCH_OPT_WAVES_PER_CU = 2,  /* persistent: resident waves per compute unit (default 32) */
     OCH_OPT_REFILL = 3,        /* persistent: refill a wave once this many of its lanes are idle (1..64) */
-    OCH_OPT_LAYOUT = 4         /* 0 = the caller's node layout; 1 = packed (default when the DAG has < 2^24
+    OCH_OPT_LAYOUT = 4,        /* 0 = the caller's node layout; 1 = packed (default when the DAG has < 2^24
                                   (node, level) pairs): per-level breadth-first ids, interior slots carry the
                                   child's occupancy mask so only descents and hits touch memory */
+    OCH_OPT_TILE_ORDER = 5     /* camera rays (render): 0 = 8x8-pixel tiles row-major; 1 = 64x64-pixel supertiles,
+                                  each handed to one XCD so neighbouring rays share that XCD's L2 */
 } och_option;
 OCH_API int och_gpu_set_option(och_gpu_pool *pool, int option, int value);
 OCH_API int och_gpu_get_option(const och_gpu_pool *pool, int option, int *value);

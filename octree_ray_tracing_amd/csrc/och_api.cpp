@@ -145,6 +145,7 @@ struct och_gpu_pool {
     uint32_t packed_root = 0;
     uint32_t packed_nodes = 0;
     int opt_layout = 1;
+    int opt_tile_order = 0;
     // host-call staging
     void *d_scratch = nullptr;
     size_t scratch_bytes = 0;
@@ -158,6 +159,7 @@ struct och_gpu_pool {
         sc.block = opt_block;
         sc.waves_per_cu = opt_waves_per_cu;
         sc.refill_min = opt_refill;
+        sc.tile_order = opt_tile_order;
         sc.cus = cus;
         sc.counter = d_counter;
         sc.stamps = stamps;
@@ -534,6 +536,10 @@ OCH_API int och_gpu_set_option(och_gpu_pool *p, int option, int value)
         if (value == 1 && !p->d_packed) return fail(OCH_E_INVALID, "pool too large for the packed layout");
         p->opt_layout = value;
         return OCH_OK;
+    case OCH_OPT_TILE_ORDER:
+        if (value != 0 && value != 1) return fail(OCH_E_INVALID, "tile order must be 0 or 1");
+        p->opt_tile_order = value;
+        return OCH_OK;
     default:
         return fail(OCH_E_INVALID, "unknown option %d", option);
     }
@@ -548,6 +554,7 @@ OCH_API int och_gpu_get_option(const och_gpu_pool *p, int option, int *value)
     case OCH_OPT_WAVES_PER_CU: *value = p->opt_waves_per_cu; return OCH_OK;
     case OCH_OPT_REFILL: *value = p->opt_refill; return OCH_OK;
     case OCH_OPT_LAYOUT: *value = (p->opt_layout == 1 && p->d_packed) ? 1 : 0; return OCH_OK;
+    case OCH_OPT_TILE_ORDER: *value = p->opt_tile_order; return OCH_OK;
     default: return fail(OCH_E_INVALID, "unknown option %d", option);
     }
 }

@@ -43,6 +43,7 @@ struct Schedule {
     int block;              // threads per workgroup (multiple of 64)
     int waves_per_cu;       // persistent grid size per CU
     int refill_min;         // refill once this many lanes of a wave are idle
+    int tile_order;         // camera rays: 0 row-major 8x8 tiles, 1 supertiles grouped per XCD
     int cus;                // compute units of the device
     uint32_t *counter;      // device ray counter (persistent)
     uint64_t *stamps;       // optional per-wave residency records

@@ -64,8 +64,10 @@ struct Ray {
     uint32_t t_min;       // bits of the entry t of the current cell
     uint32_t min_axis;    // 1, 2, 4 (last STEP axis) or 8 (none yet)
     uint32_t voxel;       // the hit voxel id (valid once level > depth)
+    uint32_t child;       // slot word loaded by the last PUSH (pending)
     int level;            // 1..depth while walking; 0 after a miss, depth + 1 after a hit
     bool stepping;        // next iteration starts at STEP (after a failed PUSH or a POP)
+    bool pending;         // a PUSH found its child; the slot word is in flight
     uint32_t push;
 };
 
@@ -101,89 +103,132 @@ __device__ __forceinline__ void ray_init(Ray &r, const DevPool &P, const float *
     r.min_axis = 8;
     r.voxel = 0;
     r.stepping = false;
+    r.pending = false;
+    r.child = 0;
     r.push = 0;
+    const uint32_t c = r.idx ^ r.inv;                                       // the first PUSH, at the root
+    r.push = 1;
+    if (!kPacked || ((r.mask >> c) & 1u)) {
+        r.child = P.nodes[8u * r.node + c];
+        r.pending = true;
+    } else {
+        r.stepping = true;
+    }
 }
 
-// One iteration of the PUSH / STEP / POP machine (ORT/och_h_octree.h:342-446,
-// ORT/och_octree.cpp:217-319): one PUSH, or one STEP possibly followed by a
-// POP -- a flat iteration, so lanes in different states progress together.
-// The only global load is the child's slot word on a PUSH: every one in the
-// raw layout, only when the held child mask says "present" in the packed
-// layout.  Returns true when the ray has finished (see ray_result).
+// The PUSH / STEP / POP machine (ORT/och_h_octree.h:342-446,
+// ORT/och_octree.cpp:217-319) as three phases per iteration, software-
+// pipelined so that a slot load is in flight while other lanes STEP:
+//   step    -- lanes due to STEP do so, then advance to a sibling or POP;
+//   descend -- lanes whose PUSH found its child (slot word loaded by the
+//              previous iteration's push) hit or descend;
+//   push    -- every lane now at a PUSH tests its child and, if present,
+//              issues the load of the child's slot word.
+// The packed layout tests presence with the child mask held since the node
+// was entered, so only present children are loaded and the order is
+// step, descend, push.  The raw layout must load every PUSH's slot to test it,
+// so it resolves the slot first (descend, step, push): an empty child then
+// STEPs in the same iteration.
 // stack: this lane's first LDS slot, levels `stride` words apart.
 template <bool kPacked, bool kCount>
-__device__ __forceinline__ bool ray_iterate(Ray &r, const DevPool &P, uint32_t *stack, uint32_t stride)
+__device__ __forceinline__ void ray_phase_step(Ray &r, const DevPool &P, uint32_t *stack, uint32_t stride)
 {
-    if (!r.stepping) {                                                       // PUSH :342
-        if (kCount) ++r.push;
-        const uint32_t c = (r.idx ^ r.inv) & 7u;
-        const uint32_t *slot = P.nodes + 8u * r.node + c;
-        uint32_t child = 0;
-        bool present;
-        if (kPacked) {
-            present = (r.mask >> c) & 1u;
-            if (present) child = *slot;
-        } else {
-            child = *slot;
-            present = child != 0;
+    if (r.stepping) {
+        // STEP :378-419.  The reference's cascade (x if tx <= ty && tx <= tz,
+        // else y if ty < tx && ty <= tz, else z) picks the first axis holding
+        // the unsigned minimum.
+        const uint32_t tx = fbits(__builtin_fmaf(ffrom(r.p[0]), r.c[0], r.b[0])) | r.nan_or[0];
+        const uint32_t ty = fbits(__builtin_fmaf(ffrom(r.p[1]), r.c[1], r.b[1])) | r.nan_or[1];
+        const uint32_t tz = fbits(__builtin_fmaf(ffrom(r.p[2]), r.c[2], r.b[2])) | r.nan_or[2];
+        const uint32_t tm = min(min(tx, ty), tz);
+        const bool sx = tx == tm;
+        const bool sy = !sx && ty == tm;
+        const bool sz = !sx && !sy;
+        const uint32_t axis = sx ? 1u : (sy ? 2u : 4u);
+        r.min_axis = axis;
+        r.t_min = tm;
+        const bool adv = r.idx & axis;
+        r.stepping = !adv;
+        if (adv) {                                                          // advance :413-419
+            const uint32_t clr = ~r.dim;
+            r.p[0] &= sx ? clr : 0xFFFFFFFFu;
+            r.p[1] &= sy ? clr : 0xFFFFFFFFu;
+            r.p[2] &= sz ? clr : 0xFFFFFFFFu;
+            r.idx ^= axis;
+        } else if (--r.level != 0) {                                        // POP :421-446 (0: MISS :423-431)
+            const uint32_t e = stack[(uint32_t)(r.level - 1) * stride];      // :434
+            r.node = kPacked ? (e & kIdMask) : e;
+            r.mask = e >> 24;
+#pragma unroll
+            for (int a = 0; a < 3; ++a) r.p[a] &= ~r.dim;                   // :436
+            r.dim <<= 1;                                                    // :438
+            r.idx = (uint32_t)((r.p[0] & r.dim) != 0) | ((uint32_t)((r.p[1] & r.dim) != 0) << 1) |
+                    ((uint32_t)((r.p[2] & r.dim) != 0) << 2);               // :440-444
         }
-        if (present) {
+    }
+}
+
+template <bool kPacked, bool kCount>
+__device__ __forceinline__ void ray_phase_descend(Ray &r, const DevPool &P, uint32_t *stack, uint32_t stride)
+{
+    if (r.pending) {
+        r.pending = false;
+        const uint32_t child = r.child;
+        if (kPacked || child != 0) {
             if (r.level == P.depth) {                                       // HIT :346-355
                 r.voxel = child;
                 r.level = P.depth + 1;
-                return true;
-            }
-            stack[(uint32_t)(r.level - 1) * stride] = kPacked ? (r.node | (r.mask << 24)) : r.node;   // :357
-            ++r.level;
-            r.node = kPacked ? (child & kIdMask) : child;
-            r.mask = child >> 24;
-            r.dim >>= 1;                                                    // :361
-            const float tm = ffrom(r.t_min);
-            uint32_t nidx = 0;
+            } else {
+                stack[(uint32_t)(r.level - 1) * stride] = kPacked ? (r.node | (r.mask << 24)) : r.node;   // :357
+                ++r.level;
+                r.node = kPacked ? (child & kIdMask) : child;
+                r.mask = child >> 24;
+                r.dim >>= 1;                                                // :361
+                const float tm = ffrom(r.t_min);
+                uint32_t nidx = 0;
 #pragma unroll
-            for (int a = 0; a < 3; ++a) {                                   // :363-373
-                const float t_mid = __builtin_fmaf(ffrom(r.p[a] | r.dim), r.c[a], r.b[a]);
-                const bool upper = t_mid >= tm;
-                nidx |= (uint32_t)upper << a;
-                r.p[a] |= upper ? r.dim : 0u;
+                for (int a = 0; a < 3; ++a) {                               // :363-373
+                    const float t_mid = __builtin_fmaf(ffrom(r.p[a] | r.dim), r.c[a], r.b[a]);
+                    const bool upper = t_mid >= tm;
+                    nidx |= (uint32_t)upper << a;
+                    r.p[a] |= upper ? r.dim : 0u;
+                }
+                r.idx = nidx;
             }
-            r.idx = nidx;
-            return false;
+        } else {
+            r.stepping = true;                                              // raw layout: empty child
         }
-        r.stepping = true;
     }
-    // STEP :378-419.  The reference's cascade (x if tx <= ty && tx <= tz, else
-    // y if ty < tx && ty <= tz, else z) picks the first axis holding the
-    // unsigned minimum.
-    const uint32_t tx = fbits(__builtin_fmaf(ffrom(r.p[0]), r.c[0], r.b[0])) | r.nan_or[0];
-    const uint32_t ty = fbits(__builtin_fmaf(ffrom(r.p[1]), r.c[1], r.b[1])) | r.nan_or[1];
-    const uint32_t tz = fbits(__builtin_fmaf(ffrom(r.p[2]), r.c[2], r.b[2])) | r.nan_or[2];
-    const uint32_t tm = min(min(tx, ty), tz);
-    const bool sx = tx == tm;
-    const bool sy = !sx && ty == tm;
-    const bool sz = !sx && !sy;
-    const uint32_t axis = sx ? 1u : (sy ? 2u : 4u);
-    r.min_axis = axis;
-    r.t_min = tm;
-    if (r.idx & axis) {                                                     // advance :413-419
-        const uint32_t clr = ~r.dim;
-        r.p[0] &= sx ? clr : 0xFFFFFFFFu;
-        r.p[1] &= sy ? clr : 0xFFFFFFFFu;
-        r.p[2] &= sz ? clr : 0xFFFFFFFFu;
-        r.idx ^= axis;
-        r.stepping = false;
-        return false;
+}
+
+template <bool kPacked, bool kCount>
+__device__ __forceinline__ void ray_phase_push(Ray &r, const DevPool &P, uint32_t *stack, uint32_t stride)
+{
+    if (!r.stepping && (uint32_t)(r.level - 1) < (uint32_t)P.depth) {       // PUSH :342-344
+        if (kCount) ++r.push;
+        const uint32_t c = (r.idx ^ r.inv) & 7u;
+        if (!kPacked || ((r.mask >> c) & 1u)) {
+            r.child = P.nodes[8u * r.node + c];
+            r.pending = true;
+        } else {
+            r.stepping = true;
+        }
     }
-    if (--r.level == 0) return true;                                        // MISS :423-431
-    const uint32_t e = stack[(uint32_t)(r.level - 1) * stride];              // POP :434
-    r.node = kPacked ? (e & kIdMask) : e;
-    r.mask = e >> 24;
-#pragma unroll
-    for (int a = 0; a < 3; ++a) r.p[a] &= ~r.dim;                           // :436
-    r.dim <<= 1;                                                            // :438
-    r.idx = (uint32_t)((r.p[0] & r.dim) != 0) | ((uint32_t)((r.p[1] & r.dim) != 0) << 1) |
-            ((uint32_t)((r.p[2] & r.dim) != 0) << 2);                       // :440-444
-    return false;
+}
+
+template <bool kPacked, bool kCount>
+__device__ __forceinline__ void ray_iterate(Ray &r, const DevPool &P, uint32_t *stack, uint32_t stride)
+{
+    if (!kPacked) ray_phase_descend<kPacked, kCount>(r, P, stack, stride);
+    ray_phase_step<kPacked, kCount>(r, P, stack, stride);
+    if (kPacked) ray_phase_descend<kPacked, kCount>(r, P, stack, stride);
+    ray_phase_push<kPacked, kCount>(r, P, stack, stride);
+}
+
+// Still walking: level in 1..depth (0 = missed, depth + 1 = hit).
+__device__ __forceinline__ bool ray_active(const Ray &r, const DevPool &P)
+{
+    return (uint32_t)(r.level - 1) < (uint32_t)P.depth;
 }
 
 // The hit record of a finished ray (:346-355 hit, :423-431 miss).
@@ -243,20 +288,31 @@ __device__ __forceinline__ void camera_ray(const och_camera &C, int col, int row
 }
 
 // Camera rays of one shard's slice for up to kMaxViews cameras of equal size,
-// enumerated view after view, 8x8 pixel tile after tile (ray i -> tile i / 64,
-// pixel i % 64), so a wave's 64 rays are one tile of one view.  The output
-// token is view * slice_pixels + slice pixel.
+// enumerated view after view, 8x8 pixel tile after tile, so a wave's 64 rays
+// are one tile of one view (ray i -> tile i / 64, pixel i % 64).  Tiles run
+// row-major (order 0) or in 64x64-pixel supertiles of 8x8 tiles (order 1),
+// which the grid kernel hands to one XCD as a unit (see xcd_block).  The
+// output token is view * slice_pixels + slice pixel.
 struct CameraSource {
     och_camera cam[kMaxViews];
-    int32_t n_views, row_chunk, shard, n_shards, slice_rows, width, height;
-    uint32_t tiles_x, per_view, slice_pixels;
+    int32_t n_views, row_chunk, shard, n_shards, slice_rows, width, height, order;
+    uint32_t tiles_x, supertiles_x, per_view, slice_pixels;
     __host__ __device__ __forceinline__ uint32_t count() const { return per_view * (uint32_t)n_views; }
     __device__ __forceinline__ bool get(uint32_t i, float *o, float *d, uint32_t &out) const
     {
         const uint32_t view = i / per_view, j = i - view * per_view;
         const uint32_t tile = j >> 6, lane = j & 63u;
-        const int col = (int)((tile % tiles_x) * 8u + (lane & 7u));
-        const int srow = (int)((tile / tiles_x) * 8u + (lane >> 3));
+        uint32_t tx, ty;
+        if (order == 1) {
+            const uint32_t st = tile >> 6, sub = tile & 63u;
+            tx = (st % supertiles_x) * 8u + (sub & 7u);
+            ty = (st / supertiles_x) * 8u + (sub >> 3);
+        } else {
+            tx = tile % tiles_x;
+            ty = tile / tiles_x;
+        }
+        const int col = (int)(tx * 8u + (lane & 7u));
+        const int srow = (int)(ty * 8u + (lane >> 3));
         if (col >= width || srow >= slice_rows) return false;
         const int chunk = srow / row_chunk, within = srow - chunk * row_chunk;
         const int row = (chunk * n_shards + shard) * row_chunk + within;
@@ -330,19 +386,34 @@ __device__ __forceinline__ void stamp(uint64_t *stamps, uint32_t cap, uint64_t t
 
 // ---------------------------------------------------------------- kernels
 
+// Workgroups are dealt round-robin over the 8 XCDs (blocks b, b + 8, ... share
+// one XCD and its L2).  Remap so each XCD receives runs of `group`
+// consecutive logical blocks -- one supertile of neighbouring rays, which walk
+// the same DAG nodes -- instead of every eighth block.  A bijection on the
+// grid; placement only changes speed, never results.
+__device__ __forceinline__ uint32_t xcd_block(uint32_t b, uint32_t nb, uint32_t group)
+{
+    if (group == 0) return b;
+    const uint32_t span = 8u * group, full = nb - nb % span;
+    if (b >= full) return b;
+    const uint32_t x = b & 7u, s = b >> 3;
+    return ((s / group) * 8u + x) * group + s % group;
+}
+
 template <class Src, class Sink, bool kPacked, bool kCount>
-__global__ void k_trace_grid(DevPool P, Src S, Sink K, uint64_t *stamps, uint32_t stamp_cap)
+__global__ void k_trace_grid(DevPool P, Src S, Sink K, uint32_t xcd_group, uint64_t *stamps, uint32_t stamp_cap)
 {
     extern __shared__ uint32_t lds_stack[];
     const uint64_t t0 = stamps ? realtime() : 0;
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t i = xcd_block(blockIdx.x, gridDim.x, xcd_group) * blockDim.x + threadIdx.x;
     float o[3], d[3];
     uint32_t out;
     if (i < S.count() && S.get(i, o, d, out)) {
         Ray r;
         ray_init<kPacked>(r, P, o, d);
-        while (!ray_iterate<kPacked, kCount>(r, P, lds_stack + threadIdx.x, blockDim.x)) {
-        }
+        do {
+            ray_iterate<kPacked, kCount>(r, P, lds_stack + threadIdx.x, blockDim.x);
+        } while (ray_active(r, P));
         K.put(out, ray_result(r, P));
     }
     if (stamps) stamp(stamps, stamp_cap, t0, 64);
@@ -385,7 +456,8 @@ __global__ void k_trace_persistent(DevPool P, Src S, Sink K, uint32_t *counter, 
             continue;
         }
         if (active) {
-            if (ray_iterate<kPacked, kCount>(r, P, stack, blockDim.x)) {
+            ray_iterate<kPacked, kCount>(r, P, stack, blockDim.x);
+            if (!ray_active(r, P)) {
                 K.put(out, ray_result(r, P));
                 active = false;
                 ++finished;
@@ -425,7 +497,8 @@ __global__ __launch_bounds__(256) void k_unshard(const uint32_t *__restrict__ ga
 size_t stack_bytes(int depth, int block) { return (size_t)(depth > 1 ? depth - 1 : 1) * block * sizeof(uint32_t); }
 
 template <class Src, class Sink, bool kPacked, bool kCount>
-hipError_t launch_as(const DevPool &p, const Src &s, const Sink &k, uint32_t n, const Schedule &sc, hipStream_t stream)
+hipError_t launch_as(const DevPool &p, const Src &s, const Sink &k, uint32_t n, const Schedule &sc, hipStream_t stream,
+                     uint32_t supertile_rays = 0)
 {
     if (n == 0) return hipSuccess;
     const int block = sc.block;
@@ -440,17 +513,19 @@ hipError_t launch_as(const DevPool &p, const Src &s, const Sink &k, uint32_t n, 
         hipLaunchKernelGGL((k_trace_persistent<Src, Sink, kPacked, kCount>), dim3(grid), dim3(block), lds, stream, p, s,
                            k, sc.counter, sc.refill_min, sc.stamps, sc.stamp_cap);
     } else {
+        const uint32_t xcd_group = supertile_rays >= (uint32_t)block ? supertile_rays / (uint32_t)block : 0u;
         hipLaunchKernelGGL((k_trace_grid<Src, Sink, kPacked, kCount>), dim3((n + block - 1) / block), dim3(block), lds,
-                           stream, p, s, k, sc.stamps, sc.stamp_cap);
+                           stream, p, s, k, xcd_group, sc.stamps, sc.stamp_cap);
     }
     return hipGetLastError();
 }
 
 template <class Src, class Sink, bool kCount>
-hipError_t launch(const DevPool &p, const Src &s, const Sink &k, uint32_t n, const Schedule &sc, hipStream_t stream)
+hipError_t launch(const DevPool &p, const Src &s, const Sink &k, uint32_t n, const Schedule &sc, hipStream_t stream,
+                  uint32_t supertile_rays = 0)
 {
-    return p.packed ? launch_as<Src, Sink, true, kCount>(p, s, k, n, sc, stream)
-                    : launch_as<Src, Sink, false, kCount>(p, s, k, n, sc, stream);
+    return p.packed ? launch_as<Src, Sink, true, kCount>(p, s, k, n, sc, stream, supertile_rays)
+                    : launch_as<Src, Sink, false, kCount>(p, s, k, n, sc, stream, supertile_rays);
 }
 
 }  // namespace
@@ -504,10 +579,13 @@ hipError_t launch_render(const DevPool &p, const DevFrame &f, const Schedule &sc
     src.width = f.cams[0].width;
     src.height = f.cams[0].height;
     src.tiles_x = (uint32_t)(src.width + 7) / 8;
-    src.per_view = src.tiles_x * (uint32_t)((f.slice_rows + 7) / 8) * 64u;
+    src.order = sc.tile_order;
+    const uint32_t tiles_y = (uint32_t)(f.slice_rows + 7) / 8;
+    src.supertiles_x = (src.tiles_x + 7) / 8;
+    src.per_view = sc.tile_order == 1 ? src.supertiles_x * ((tiles_y + 7) / 8) * 64u * 64u : src.tiles_x * tiles_y * 64u;
     src.slice_pixels = (uint32_t)f.slice_rows * (uint32_t)src.width;
     return launch<CameraSource, FrameSink, false>(p, src, FrameSink{f.out, f.palette, f.n_voxels}, src.count(), sc,
-                                                  stream);
+                                                  stream, sc.tile_order == 1 ? 64u * 64u : 0u);
 }
 
 hipError_t launch_unshard(const uint32_t *gathered, uint32_t *frames, int width, int height, int row_chunk,

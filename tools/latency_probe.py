@@ -90,6 +90,11 @@ def main():
                     ms = timed(lambda: pool.trace_batch_dev(o, d, hd, hv, ht, n=1))
                     row[f"ray_{y}_{x}"] = {"push": push, "us": round(ms * 1e3, 1),
                                            "ns_per_push": round(ms * 1e6 / push, 1)}
+                    # the same ray in every lane of one wave, and in 8 waves (one per XCD: warm L2s)
+                    for copies in (64, 512):
+                        dc = d.repeat(copies)
+                        hc = [torch.empty(copies, dtype=t, device=dev) for t in (torch.int32, torch.int32, torch.float32)]
+                        row[f"ray_{y}_{x}_x{copies}_us"] = round(timed(lambda: pool.trace_batch_dev(o, dc, *hc, n=copies)) * 1e3, 1)
                     # its 8x8 tile alone (64 rays)
                     ty, tx = y // 8 * 8, x // 8 * 8
                     tile = np.ascontiguousarray(rays.reshape(1080, 1920, 3)[ty:ty + 8, tx:tx + 8].reshape(-1, 3))
