@@ -169,6 +169,20 @@ OCH_API int och_gpu_trace_batch_dev(och_gpu_pool *pool, const float *origin, int
                                     int32_t *hit_direction, uint32_t *hit_voxel, float *hit_time,
                                     uint32_t *push_count);
 
+/* Config 5 (BASELINE configs[4]): each primary ray that hits a voxel face
+ * spawns one secondary ray -- from o + d*t - offset, the point half a voxel in
+ * front of the hit face (get_directional_hit_offset, ORT/test_och_h_octree.cpp:
+ * 487-502, as the editor's placement point :385), along d mirrored on the hit
+ * axis -- traced by the same traversal.  Build-defined: the reference renders
+ * primary rays only.  Secondary records: direction -1, voxel 0, t 0 when the
+ * primary ray did not hit (exit / inside).  push_count (optional) receives the
+ * PUSH iterations of both rays.  Device buffers, asynchronous on the pool stream. */
+OCH_API int och_gpu_trace_bounce_batch_dev(och_gpu_pool *pool, const float *origin, int origin_stride,
+                                           const float *dirs, uint32_t n,
+                                           int32_t *hit_direction, uint32_t *hit_voxel, float *hit_time,
+                                           int32_t *bounce_direction, uint32_t *bounce_voxel, float *bounce_time,
+                                           uint32_t *push_count);
+
 /* ------------------------------------------------------------ camera / frame */
 /* tree_camera::update_position's per-frame constants (ORT/test_och_h_octree.cpp:89-115):
  * yaw = camera.dir.x, pitch = camera.dir.y, fov = 1.25F in the reference. */
@@ -191,6 +205,11 @@ OCH_API int och_shard_rows(int height, int row_chunk, int n_shards);
  * One launch keeps the GPU busy with other views while a view's slowest rays finish. */
 OCH_API int och_gpu_render_views_dev(och_gpu_pool *pool, const och_camera *cams, int n_views, uint32_t *rgba_slices,
                                      int row_chunk, int shard, int n_shards);
+/* Config 5 frame: och_gpu_render_views_dev with one bounce per hit; a hit
+ * pixel keeps its face colour when its secondary ray escapes (exit) and is
+ * halved (RGB >> 1, alpha kept) when the secondary ray is blocked. */
+OCH_API int och_gpu_render_bounce_views_dev(och_gpu_pool *pool, const och_camera *cams, int n_views,
+                                            uint32_t *rgba_slices, int row_chunk, int shard, int n_shards);
 /* Reassemble n_shards gathered slices (slice s at gathered + s*rows*W) into a
  * full W*H frame on the device. */
 OCH_API int och_gpu_unshard_dev(och_gpu_pool *pool, const uint32_t *gathered, uint32_t *frame,

@@ -180,6 +180,7 @@ struct och_gpu_pool {
         uint32_t mb;
         std::memcpy(&mb, &miss_t, 4);
         p.miss_bits = mb;
+        p.half_voxel = std::ldexp(1.0F, -(depth + 1));
         return p;
     }
 };
@@ -610,6 +611,27 @@ OCH_API int och_gpu_trace_batch_dev(och_gpu_pool *p, const float *origin, int or
     return OCH_OK;
 }
 
+OCH_API int och_gpu_trace_bounce_batch_dev(och_gpu_pool *p, const float *origin, int origin_stride, const float *dirs,
+                                           uint32_t n, int32_t *hit_dir, uint32_t *hit_voxel, float *hit_time,
+                                           int32_t *bounce_dir, uint32_t *bounce_voxel, float *bounce_time,
+                                           uint32_t *push_count)
+{
+    if (!p || (n && (!origin || !dirs || !hit_dir || !hit_voxel || !hit_time || !bounce_dir || !bounce_voxel ||
+                     !bounce_time)))
+        return fail(OCH_E_INVALID, "NULL argument");
+    if (origin_stride != 0 && origin_stride != 3) return fail(OCH_E_INVALID, "origin_stride must be 0 or 3");
+    if (!p->d_lut) return fail(OCH_E_RCP_MODEL, "no RCPPS table on this pool (call och_gpu_set_rcp_lut)");
+    DeviceGuard g(p->device);
+    OCH_HIP(hipEventRecord(p->ev_start, p->stream()));
+    OCH_HIP(och::launch_trace_bounce_batch(p->dev(), origin, origin_stride, dirs, n, hit_dir, hit_voxel,
+                                           reinterpret_cast<uint32_t *>(hit_time), bounce_dir, bounce_voxel,
+                                           reinterpret_cast<uint32_t *>(bounce_time), push_count, p->schedule(),
+                                           p->stream()));
+    OCH_HIP(hipEventRecord(p->ev_stop, p->stream()));
+    p->timed = true;
+    return OCH_OK;
+}
+
 OCH_API int och_gpu_trace_batch(och_gpu_pool *p, const float *origin, int origin_stride, const float *dirs,
                                 uint32_t n, int32_t *hit_dir, uint32_t *hit_voxel, float *hit_time)
 {
@@ -694,8 +716,10 @@ OCH_API int och_shard_rows(int height, int row_chunk, int n_shards)
     return ((chunks + n_shards - 1) / n_shards) * row_chunk;
 }
 
-OCH_API int och_gpu_render_views_dev(och_gpu_pool *p, const och_camera *cams, int n_views, uint32_t *rgba_slices,
-                                     int row_chunk, int shard, int n_shards)
+namespace {
+
+int render_views(och_gpu_pool *p, const och_camera *cams, int n_views, uint32_t *rgba_slices, int row_chunk, int shard,
+                 int n_shards, bool bounce)
 {
     if (!p || !cams || !rgba_slices) return fail(OCH_E_INVALID, "NULL argument");
     if (n_views < 1 || n_views > OCH_MAX_VIEWS) return fail(OCH_E_INVALID, "n_views %d outside 1..%d", n_views, OCH_MAX_VIEWS);
@@ -719,10 +743,27 @@ OCH_API int och_gpu_render_views_dev(och_gpu_pool *p, const och_camera *cams, in
     f.n_shards = n_shards;
     f.slice_rows = och_shard_rows(cams[0].height, row_chunk, n_shards);
     OCH_HIP(hipEventRecord(p->ev_start, p->stream()));
-    OCH_HIP(och::launch_render(p->dev(), f, p->schedule(), p->stream()));
+    if (bounce)
+        OCH_HIP(och::launch_render_bounce(p->dev(), f, p->schedule(), p->stream()));
+    else
+        OCH_HIP(och::launch_render(p->dev(), f, p->schedule(), p->stream()));
     OCH_HIP(hipEventRecord(p->ev_stop, p->stream()));
     p->timed = true;
     return OCH_OK;
+}
+
+}  // namespace
+
+OCH_API int och_gpu_render_views_dev(och_gpu_pool *p, const och_camera *cams, int n_views, uint32_t *rgba_slices,
+                                     int row_chunk, int shard, int n_shards)
+{
+    return render_views(p, cams, n_views, rgba_slices, row_chunk, shard, n_shards, false);
+}
+
+OCH_API int och_gpu_render_bounce_views_dev(och_gpu_pool *p, const och_camera *cams, int n_views, uint32_t *rgba_slices,
+                                            int row_chunk, int shard, int n_shards)
+{
+    return render_views(p, cams, n_views, rgba_slices, row_chunk, shard, n_shards, true);
 }
 
 OCH_API int och_gpu_render_dev(och_gpu_pool *p, const och_camera *cam, uint32_t *rgba_slice, int row_chunk, int shard,

@@ -26,6 +26,7 @@ struct DevPool {
     int32_t depth;
     int32_t lut_shift;
     uint32_t miss_bits;     // hit_time bits of a miss (+INF or +0.0)
+    float half_voxel;       // voxel_dim / 2 = 2^-(depth+1) (ORT/och_h_octree.h:28), bounce origins
 };
 
 struct DevFrame {
@@ -56,6 +57,14 @@ hipError_t launch_trace_batch(const DevPool &p, const float *origin, int origin_
 // hipOccupancyMaxActiveBlocksPerMultiprocessor of kind 0 render-grid,
 // 1 render-persistent, 2 trace-grid, at this block size and stack depth.
 hipError_t occupancy_blocks_per_cu(int kind, int block, int depth, int *blocks);
+// Config 5: primary ray, then one mirrored secondary ray per hit (see
+// bounce_ray in och_kernels.hip); secondary records get direction -1 when the
+// primary ray did not hit.
+hipError_t launch_trace_bounce_batch(const DevPool &p, const float *origin, int origin_stride, const float *dirs,
+                                     uint32_t n, int32_t *hit_dir, uint32_t *hit_voxel, uint32_t *hit_time,
+                                     int32_t *bounce_dir, uint32_t *bounce_voxel, uint32_t *bounce_time,
+                                     uint32_t *push_count, const Schedule &sc, hipStream_t stream);
+hipError_t launch_render_bounce(const DevPool &p, const DevFrame &f, const Schedule &sc, hipStream_t stream);
 hipError_t launch_raygen(const och_camera &cam, float *dirs, hipStream_t stream);
 hipError_t launch_render(const DevPool &p, const DevFrame &f, const Schedule &sc, hipStream_t stream);
 hipError_t launch_unshard(const uint32_t *gathered, uint32_t *frames, int width, int height, int row_chunk,

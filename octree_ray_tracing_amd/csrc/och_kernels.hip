@@ -248,6 +248,25 @@ __device__ __forceinline__ Hit ray_result(const Ray &r, const DevPool &P)
     return h;
 }
 
+// Secondary ray of a hit, config 5 (BASELINE configs[4]; build-defined, as
+// SURVEY §8(a) A10 proposes): from the point half a voxel in front of the hit
+// face -- o + d * t - offset, the editor's placement point
+// (ORT/test_och_h_octree.cpp:385, :418) with get_directional_hit_offset's
+// +-voxel_dim / 2 on the hit axis (:487-502) -- along d mirrored on that axis.
+// Products rounded, then sums, as float3's operators evaluate them.
+__device__ __forceinline__ void bounce_ray(const float *o, const float *d, const Hit &h, float half, float *o2, float *d2)
+{
+    const float t = ffrom(h.t);
+    const int axis = h.dir % 3;
+    const float off = h.dir < 3 ? half : -half;
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        const float q = __fadd_rn(o[a], __fmul_rn(d[a], t));
+        o2[a] = __fsub_rn(q, a == axis ? off : 0.0F);
+        d2[a] = a == axis ? -d[a] : d[a];
+    }
+}
+
 // ---------------------------------------------------------------- sources
 
 // Rays from arrays: shared (stride 0) or per-ray (stride 3) origin, AoS float3 dirs.
@@ -343,18 +362,65 @@ struct HitSink {
 };
 
 // trace_pixel's colour choice (ORT/test_och_h_octree.cpp:76-84) as olc::Pixel RGBA8.
+__device__ __forceinline__ uint32_t pixel_colour(const Hit &h, const uint32_t *palette, uint32_t n_voxels)
+{
+    if (h.dir == OCH_EXIT) return 0xFFFEBF00u;            // {0x00, 0xBF, 0xFE}
+    if (h.dir == OCH_INSIDE) return 0xFF07193Fu;          // {0x3F, 0x19, 0x07}
+    if (h.voxel == 0 || h.voxel > n_voxels) return 0xFFFF00FFu;
+    return palette[6u * (h.voxel - 1u) + (uint32_t)h.dir];
+}
+
 struct FrameSink {
     uint32_t *out;
     const uint32_t *palette;
     uint32_t n_voxels;
-    __device__ __forceinline__ void put(uint32_t i, const Hit &h) const
+    __device__ __forceinline__ void put(uint32_t i, const Hit &h) const { out[i] = pixel_colour(h, palette, n_voxels); }
+};
+
+// Config 5 sinks.  put_primary stores what is final for a ray without a
+// bounce and returns the payload its secondary ray carries; put_secondary
+// completes a bounced ray.
+// Shading of a bounced pixel (build-defined): the hit face's colour when the
+// mirrored ray escapes to the sky, half of it (RGB >> 1) when it is blocked.
+struct BounceFrameSink {
+    FrameSink f;
+    __device__ __forceinline__ uint32_t put_primary(uint32_t i, const Hit &h, bool bounced) const
     {
-        uint32_t c;
-        if (h.dir == OCH_EXIT) c = 0xFFFEBF00u;           // {0x00, 0xBF, 0xFE}
-        else if (h.dir == OCH_INSIDE) c = 0xFF07193Fu;    // {0x3F, 0x19, 0x07}
-        else if (h.voxel == 0 || h.voxel > n_voxels) c = 0xFFFF00FFu;
-        else c = palette[6u * (h.voxel - 1u) + (uint32_t)h.dir];
-        out[i] = c;
+        const uint32_t c = pixel_colour(h, f.palette, f.n_voxels);
+        if (!bounced) f.out[i] = c;
+        return c;
+    }
+    __device__ __forceinline__ void put_secondary(uint32_t i, uint32_t c, const Hit &h2) const
+    {
+        f.out[i] = h2.dir == OCH_EXIT ? c : (((c >> 1) & 0x007F7F7Fu) | (c & 0xFF000000u));
+    }
+};
+
+template <bool kCount>
+struct BounceHitSink {
+    HitSink<kCount> h;
+    int32_t *dir2;
+    uint32_t *voxel2;
+    uint32_t *t2;
+    __device__ __forceinline__ uint32_t put_primary(uint32_t i, const Hit &h1, bool bounced) const
+    {
+        h.dir[i] = h1.dir;
+        h.voxel[i] = h1.voxel;
+        h.t[i] = h1.t;
+        if (!bounced) {
+            dir2[i] = -1;
+            voxel2[i] = 0;
+            t2[i] = 0;
+            if (kCount) h.push[i] = h1.push;
+        }
+        return h1.push;
+    }
+    __device__ __forceinline__ void put_secondary(uint32_t i, uint32_t push1, const Hit &h2) const
+    {
+        dir2[i] = h2.dir;
+        voxel2[i] = h2.voxel;
+        t2[i] = h2.t;
+        if (kCount) h.push[i] = push1 + h2.push;
     }
 };
 
@@ -417,6 +483,73 @@ __global__ void k_trace_grid(DevPool P, Src S, Sink K, uint32_t xcd_group, uint6
         K.put(out, ray_result(r, P));
     }
     if (stamps) stamp(stamps, stamp_cap, t0, 64);
+}
+
+// Config 5: primary rays, then wavefront compaction -- the block's hit
+// lanes (ballot + popcount per wave, wave offsets through LDS) write their
+// secondary rays into an LDS queue, and the first lanes of the block trace
+// them, so waves whose tiles mostly missed retire instead of idling beside
+// a few bounced lanes.  stack_words: LDS words of the parent stacks; the
+// queue (8 words per thread, SoA) follows them.
+template <class Src, class Sink, bool kPacked, bool kCount>
+__global__ void k_trace_bounce(DevPool P, Src S, Sink K, uint32_t stack_words, uint64_t *stamps, uint32_t stamp_cap)
+{
+    extern __shared__ uint32_t lds_stack[];
+    __shared__ uint32_t wave_count[16];
+    const uint64_t t0 = stamps ? realtime() : 0;
+    uint32_t *stack = lds_stack + threadIdx.x;
+    uint32_t *queue = lds_stack + stack_words;
+    const uint32_t nb = blockDim.x;
+    const uint32_t i = blockIdx.x * nb + threadIdx.x;
+    float o[3], d[3], o2[3], d2[3];
+    uint32_t out = 0, payload = 0;
+    bool want = false;
+    if (i < S.count() && S.get(i, o, d, out)) {
+        Ray r;
+        ray_init<kPacked>(r, P, o, d);
+        do {
+            ray_iterate<kPacked, kCount>(r, P, stack, nb);
+        } while (ray_active(r, P));
+        const Hit h1 = ray_result(r, P);
+        want = h1.dir < OCH_EXIT;
+        if (want) bounce_ray(o, d, h1, P.half_voxel, o2, d2);
+        payload = K.put_primary(out, h1, want);
+    }
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+    const uint64_t bal = __ballot(want);
+    if (lane == 0) wave_count[wave] = (uint32_t)__popcll(bal);
+    __syncthreads();
+    uint32_t base = 0, total = 0;
+    for (uint32_t w = 0; w < (nb >> 6); ++w) {
+        const uint32_t cnt = wave_count[w];
+        base += w < wave ? cnt : 0u;
+        total += cnt;
+    }
+    if (want) {
+        const uint32_t q = base + (uint32_t)__popcll(bal & ((1ull << lane) - 1ull));
+        queue[0 * nb + q] = fbits(o2[0]);
+        queue[1 * nb + q] = fbits(o2[1]);
+        queue[2 * nb + q] = fbits(o2[2]);
+        queue[3 * nb + q] = fbits(d2[0]);
+        queue[4 * nb + q] = fbits(d2[1]);
+        queue[5 * nb + q] = fbits(d2[2]);
+        queue[6 * nb + q] = out;
+        queue[7 * nb + q] = payload;
+    }
+    __syncthreads();
+    if (threadIdx.x < total) {
+        const uint32_t q = threadIdx.x;
+        const float so[3] = {ffrom(queue[0 * nb + q]), ffrom(queue[1 * nb + q]), ffrom(queue[2 * nb + q])};
+        const float sd[3] = {ffrom(queue[3 * nb + q]), ffrom(queue[4 * nb + q]), ffrom(queue[5 * nb + q])};
+        const uint32_t sout = queue[6 * nb + q], spay = queue[7 * nb + q];
+        Ray r;
+        ray_init<kPacked>(r, P, so, sd);
+        do {
+            ray_iterate<kPacked, kCount>(r, P, stack, nb);
+        } while (ray_active(r, P));
+        K.put_secondary(sout, spay, ray_result(r, P));
+    }
+    if (stamps) stamp(stamps, stamp_cap, t0, total);
 }
 
 template <class Src, class Sink, bool kPacked, bool kCount>
@@ -528,6 +661,45 @@ hipError_t launch(const DevPool &p, const Src &s, const Sink &k, uint32_t n, con
                     : launch_as<Src, Sink, false, kCount>(p, s, k, n, sc, stream, supertile_rays);
 }
 
+constexpr int kBounceBlock = 256;   // compaction spans the block's 4 waves
+
+template <class Src, class Sink, bool kCount>
+hipError_t launch_bounce(const DevPool &p, const Src &s, const Sink &k, uint32_t n, const Schedule &sc, hipStream_t stream)
+{
+    if (n == 0) return hipSuccess;
+    const int block = sc.block > kBounceBlock ? sc.block : kBounceBlock;
+    const uint32_t stack_words = (uint32_t)(stack_bytes(p.depth, block) / sizeof(uint32_t));
+    const size_t lds = (stack_words + 8u * (uint32_t)block) * sizeof(uint32_t);
+    const dim3 grid((n + block - 1) / block);
+    if (p.packed)
+        hipLaunchKernelGGL((k_trace_bounce<Src, Sink, true, kCount>), grid, dim3(block), lds, stream, p, s, k,
+                           stack_words, sc.stamps, sc.stamp_cap);
+    else
+        hipLaunchKernelGGL((k_trace_bounce<Src, Sink, false, kCount>), grid, dim3(block), lds, stream, p, s, k,
+                           stack_words, sc.stamps, sc.stamp_cap);
+    return hipGetLastError();
+}
+
+CameraSource camera_source(const DevFrame &f, const Schedule &sc)
+{
+    CameraSource src;
+    for (int v = 0; v < f.n_views; ++v) src.cam[v] = f.cams[v];
+    src.n_views = f.n_views;
+    src.row_chunk = f.row_chunk;
+    src.shard = f.shard;
+    src.n_shards = f.n_shards;
+    src.slice_rows = f.slice_rows;
+    src.width = f.cams[0].width;
+    src.height = f.cams[0].height;
+    src.tiles_x = (uint32_t)(src.width + 7) / 8;
+    src.order = sc.tile_order;
+    const uint32_t tiles_y = (uint32_t)(f.slice_rows + 7) / 8;
+    src.supertiles_x = (src.tiles_x + 7) / 8;
+    src.per_view = sc.tile_order == 1 ? src.supertiles_x * ((tiles_y + 7) / 8) * 64u * 64u : src.tiles_x * tiles_y * 64u;
+    src.slice_pixels = (uint32_t)f.slice_rows * (uint32_t)src.width;
+    return src;
+}
+
 }  // namespace
 
 hipError_t occupancy_blocks_per_cu(int kind, int block, int depth, int *blocks)
@@ -569,23 +741,34 @@ hipError_t launch_raygen(const och_camera &cam, float *dirs, hipStream_t stream)
 hipError_t launch_render(const DevPool &p, const DevFrame &f, const Schedule &sc, hipStream_t stream)
 {
     if (f.n_views < 1 || f.n_views > kMaxViews) return hipErrorInvalidValue;
-    CameraSource src;
-    for (int v = 0; v < f.n_views; ++v) src.cam[v] = f.cams[v];
-    src.n_views = f.n_views;
-    src.row_chunk = f.row_chunk;
-    src.shard = f.shard;
-    src.n_shards = f.n_shards;
-    src.slice_rows = f.slice_rows;
-    src.width = f.cams[0].width;
-    src.height = f.cams[0].height;
-    src.tiles_x = (uint32_t)(src.width + 7) / 8;
-    src.order = sc.tile_order;
-    const uint32_t tiles_y = (uint32_t)(f.slice_rows + 7) / 8;
-    src.supertiles_x = (src.tiles_x + 7) / 8;
-    src.per_view = sc.tile_order == 1 ? src.supertiles_x * ((tiles_y + 7) / 8) * 64u * 64u : src.tiles_x * tiles_y * 64u;
-    src.slice_pixels = (uint32_t)f.slice_rows * (uint32_t)src.width;
+    const CameraSource src = camera_source(f, sc);
     return launch<CameraSource, FrameSink, false>(p, src, FrameSink{f.out, f.palette, f.n_voxels}, src.count(), sc,
                                                   stream, sc.tile_order == 1 ? 64u * 64u : 0u);
+}
+
+hipError_t launch_render_bounce(const DevPool &p, const DevFrame &f, const Schedule &sc, hipStream_t stream)
+{
+    if (f.n_views < 1 || f.n_views > kMaxViews) return hipErrorInvalidValue;
+    const CameraSource src = camera_source(f, sc);
+    return launch_bounce<CameraSource, BounceFrameSink, false>(
+        p, src, BounceFrameSink{FrameSink{f.out, f.palette, f.n_voxels}}, src.count(), sc, stream);
+}
+
+hipError_t launch_trace_bounce_batch(const DevPool &p, const float *origin, int origin_stride, const float *dirs,
+                                     uint32_t n, int32_t *hit_dir, uint32_t *hit_voxel, uint32_t *hit_time,
+                                     int32_t *bounce_dir, uint32_t *bounce_voxel, uint32_t *bounce_time,
+                                     uint32_t *push_count, const Schedule &sc, hipStream_t stream)
+{
+    const ArraySource src{origin, dirs, origin_stride, n};
+    if (push_count)
+        return launch_bounce<ArraySource, BounceHitSink<true>, true>(
+            p, src, BounceHitSink<true>{HitSink<true>{hit_dir, hit_voxel, hit_time, push_count}, bounce_dir, bounce_voxel,
+                                        bounce_time},
+            n, sc, stream);
+    return launch_bounce<ArraySource, BounceHitSink<false>, false>(
+        p, src, BounceHitSink<false>{HitSink<false>{hit_dir, hit_voxel, hit_time, nullptr}, bounce_dir, bounce_voxel,
+                                     bounce_time},
+        n, sc, stream);
 }
 
 hipError_t launch_unshard(const uint32_t *gathered, uint32_t *frames, int width, int height, int row_chunk,

@@ -199,6 +199,16 @@ class GpuPool:
              _dev_ptr(hit_dir), _dev_ptr(hit_voxel), _dev_ptr(hit_time),
              None if push is None else _dev_ptr(push))
 
+    def trace_bounce_batch_dev(self, origins, dirs, hit_dir, hit_voxel, hit_time, bounce_dir, bounce_voxel,
+                               bounce_time, push=None, n=None):
+        """Config 5: primary + one mirrored secondary ray per hit (device tensors, async)."""
+        if n is None:
+            n = dirs.numel() // 3
+        stride = 0 if origins.numel() == 3 else 3
+        call("och_gpu_trace_bounce_batch_dev", self._h, _dev_ptr(origins), stride, _dev_ptr(dirs), int(n),
+             _dev_ptr(hit_dir), _dev_ptr(hit_voxel), _dev_ptr(hit_time), _dev_ptr(bounce_dir),
+             _dev_ptr(bounce_voxel), _dev_ptr(bounce_time), None if push is None else _dev_ptr(push))
+
     # -- frame path
     def raygen_dev(self, cam: Camera, dirs):
         call("och_gpu_raygen_dev", self._h, C.byref(cam), _dev_ptr(dirs))
@@ -222,6 +232,15 @@ class GpuPool:
         if row_chunk is None:
             row_chunk = cams[0].height
         call("och_gpu_render_views_dev", self._h, C.cast(arr, C.c_void_p), len(cams), _dev_ptr(rgba_slices),
+             int(row_chunk), int(shard), int(n_shards))
+
+    def render_bounce_views_dev(self, cams, rgba_slices, row_chunk: int | None = None, shard: int = 0,
+                                n_shards: int = 1):
+        """Config 5 frames: one bounce per hit pixel, shaded (see och_gpu_render_bounce_views_dev)."""
+        arr = (Camera * len(cams))(*cams)
+        if row_chunk is None:
+            row_chunk = cams[0].height
+        call("och_gpu_render_bounce_views_dev", self._h, C.cast(arr, C.c_void_p), len(cams), _dev_ptr(rgba_slices),
              int(row_chunk), int(shard), int(n_shards))
 
     def unshard_dev(self, gathered, frame, width: int, height: int, row_chunk: int, n_shards: int, n_views: int = 1):

@@ -217,6 +217,78 @@ ORA_API void ora_trace_batch(const ora_pool *P, const ora_rcp *R,
     }
 }
 
+/* ------------------------------------------------------- secondary rays */
+
+/* Config 5's bounce (build-defined; the reference traces primary rays only):
+ * origin o + d*t - offset, with get_directional_hit_offset's +-voxel_dim/2 on
+ * the hit axis (ORT/test_och_h_octree.cpp:487-502; voxel_dim = 1.0F / dim,
+ * ORT/och_h_octree.h:28) subtracted as for the editor's placement point
+ * (:385, :418); direction mirrored on the hit axis.  float3 arithmetic:
+ * products rounded, then sums (-ffp-contract=off). */
+ORA_API void ora_bounce_ray(const float *o, const float *d, int32_t dir, float t, int depth, float *o2, float *d2)
+{
+    const float half = (1.0F / (float)(1 << depth)) / 2;
+    const int axis = dir % 3;
+    const float off = dir < 3 ? half : -half;
+    for (int a = 0; a < 3; ++a) {
+        const float q = o[a] + d[a] * t;
+        o2[a] = q - (a == axis ? off : 0.0F);
+        d2[a] = a == axis ? -d[a] : d[a];
+    }
+}
+
+typedef struct ora_bounce_job {
+    const ora_pool *P; const ora_rcp *R;
+    const float *origin; int origin_stride; const float *dirs;
+    int32_t *hd; uint32_t *hv; float *ht; int32_t *hd2; uint32_t *hv2; float *ht2; uint32_t *push;
+    uint64_t begin, end;
+    ora_counts cnt;
+} ora_bounce_job;
+
+static void *ora_bounce_worker(void *arg)
+{
+    ora_bounce_job *j = (ora_bounce_job *)arg;
+    memset(&j->cnt, 0, sizeof j->cnt);
+    for (uint64_t i = j->begin; i < j->end; ++i) {
+        const float *o = j->origin + (size_t)i * j->origin_stride;
+        const float *d = j->dirs + 3 * i;
+        const uint64_t p0 = j->cnt.push;
+        ora_trace(j->P, j->R, o[0], o[1], o[2], d[0], d[1], d[2], &j->hd[i], &j->hv[i], &j->ht[i], &j->cnt);
+        if (j->hd[i] < 6) {
+            float o2[3], d2[3];
+            ora_bounce_ray(o, d, j->hd[i], j->ht[i], j->P->depth, o2, d2);
+            ora_trace(j->P, j->R, o2[0], o2[1], o2[2], d2[0], d2[1], d2[2], &j->hd2[i], &j->hv2[i], &j->ht2[i], &j->cnt);
+        } else {
+            j->hd2[i] = -1; j->hv2[i] = 0; j->ht2[i] = 0.0F;
+        }
+        if (j->push) j->push[i] = (uint32_t)(j->cnt.push - p0);
+    }
+    return NULL;
+}
+
+/* Primary + secondary records of a batch (the GPU's och_gpu_trace_bounce_batch_dev). */
+ORA_API void ora_trace_bounce_batch(const ora_pool *P, const ora_rcp *R, const float *origin, int origin_stride,
+                                    const float *dirs, uint64_t n, int32_t *hd, uint32_t *hv, float *ht,
+                                    int32_t *hd2, uint32_t *hv2, float *ht2, uint32_t *push, int nthreads,
+                                    ora_counts *total)
+{
+    if (nthreads < 1) nthreads = 1;
+    if (nthreads > 256) nthreads = 256;
+    ora_bounce_job jobs[256];
+    pthread_t th[256];
+    for (int k = 0; k < nthreads; ++k) {
+        jobs[k] = (ora_bounce_job){P, R, origin, origin_stride, dirs, hd, hv, ht, hd2, hv2, ht2, push,
+                                   n * k / nthreads, n * (k + 1) / nthreads, {0, 0, 0}};
+        if (nthreads == 1) ora_bounce_worker(&jobs[k]);
+        else pthread_create(&th[k], NULL, ora_bounce_worker, &jobs[k]);
+    }
+    if (total) memset(total, 0, sizeof *total);
+    for (int k = 0; k < nthreads; ++k) {
+        if (nthreads > 1) pthread_join(th[k], NULL);
+        if (total) { total->push += jobs[k].cnt.push; total->step += jobs[k].cnt.step; total->pop += jobs[k].cnt.pop; }
+    }
+}
+
 /* ---------------------------------------------------------------- camera */
 
 /* tree_camera::update_position, ORT/test_och_h_octree.cpp:87-138.
@@ -256,6 +328,15 @@ ORA_API uint32_t ora_shade(int32_t dir, uint32_t voxel, const uint32_t *palette,
     if (dir == 7) return 0xFF07193Fu;                               /* inside colour 3F 19 07 */
     if (voxel == 0 || voxel > n_voxels || dir < 0 || dir > 5) return 0xFFFF00FFu;
     return palette[6 * (voxel - 1) + (uint32_t)dir];
+}
+
+/* Config 5 pixel: the primary colour, halved (RGB >> 1, alpha kept) when
+ * the pixel's secondary ray is blocked (anything but exit). */
+ORA_API uint32_t ora_shade_bounce(int32_t dir, uint32_t voxel, int32_t dir2, const uint32_t *palette, uint32_t n_voxels)
+{
+    const uint32_t c = ora_shade(dir, voxel, palette, n_voxels);
+    if (dir < 0 || dir > 5 || dir2 == 6) return c;
+    return ((c >> 1) & 0x007F7F7Fu) | (c & 0xFF000000u);
 }
 
 /* ----------------------------------------------------------------- noise */

@@ -60,6 +60,13 @@ def lib():
         L.ora_trace_batch.argtypes = [C.POINTER(_Pool), C.POINTER(_Rcp), C.c_void_p, C.c_int, C.c_void_p,
                                       C.c_uint64, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
                                       C.c_int, C.POINTER(_Counts)]
+        L.ora_bounce_ray.restype = None
+        L.ora_bounce_ray.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.c_float, C.c_int, C.c_void_p, C.c_void_p]
+        L.ora_trace_bounce_batch.restype = None
+        L.ora_trace_bounce_batch.argtypes = [C.POINTER(_Pool), C.POINTER(_Rcp), C.c_void_p, C.c_int, C.c_void_p,
+                                             C.c_uint64] + [C.c_void_p] * 7 + [C.c_int, C.POINTER(_Counts)]
+        L.ora_shade_bounce.restype = C.c_uint32
+        L.ora_shade_bounce.argtypes = [C.c_int32, C.c_uint32, C.c_int32, C.c_void_p, C.c_uint32]
         L.ora_raygen.restype = None
         L.ora_raygen.argtypes = [C.c_float, C.c_float, C.c_float, C.c_int, C.c_int, C.c_void_p]
         L.ora_shade.restype = C.c_uint32
@@ -137,6 +144,55 @@ def trace_batch(pool: OraclePool, rcp: Rcp, origins: np.ndarray, dirs: np.ndarra
                           int(nthreads), C.byref(tot))
     return {"dir": hd, "voxel": hv, "t": ht, "push": push,
             "counts": (tot.push, tot.step, tot.pop)}
+
+
+def bounce_ray(o, d, direction: int, t: float, depth: int):
+    """Config 5's secondary ray of a hit (ora_bounce_ray)."""
+    o = np.ascontiguousarray(o, np.float32)
+    d = np.ascontiguousarray(d, np.float32)
+    o2, d2 = np.empty(3, np.float32), np.empty(3, np.float32)
+    lib().ora_bounce_ray(_ptr(o), _ptr(d), int(direction), float(t), int(depth), _ptr(o2), _ptr(d2))
+    return o2, d2
+
+
+def trace_bounce_batch(pool: OraclePool, rcp: Rcp, origins: np.ndarray, dirs: np.ndarray,
+                       nthreads: int = 1, want_push: bool = False):
+    """Primary and secondary records (config 5), as och_gpu_trace_bounce_batch_dev."""
+    dirs = np.ascontiguousarray(dirs, dtype=np.float32).reshape(-1, 3)
+    n = dirs.shape[0]
+    origins = np.ascontiguousarray(origins, dtype=np.float32)
+    stride = 0 if origins.size == 3 else 3
+    out = {"dir": np.empty(n, np.int32), "voxel": np.empty(n, np.uint32), "t": np.empty(n, np.float32),
+           "dir2": np.empty(n, np.int32), "voxel2": np.empty(n, np.uint32), "t2": np.empty(n, np.float32),
+           "push": np.empty(n, np.uint32) if want_push else None}
+    tot = _Counts()
+    lib().ora_trace_bounce_batch(C.byref(pool._c), C.byref(rcp._c), _ptr(origins), stride, _ptr(dirs), n,
+                                 _ptr(out["dir"]), _ptr(out["voxel"]), _ptr(out["t"]), _ptr(out["dir2"]),
+                                 _ptr(out["voxel2"]), _ptr(out["t2"]),
+                                 None if out["push"] is None else _ptr(out["push"]), int(nthreads), C.byref(tot))
+    out["counts"] = (tot.push, tot.step, tot.pop)
+    return out
+
+
+def shade_fast(dirs: np.ndarray, voxels: np.ndarray, palette: np.ndarray) -> np.ndarray:
+    """Vectorised ora_shade (trace_pixel's colour choice)."""
+    palette = np.ascontiguousarray(palette, dtype=np.uint32)
+    nvox = palette.size // 6
+    dirs = np.asarray(dirs, np.int64)
+    voxels = np.asarray(voxels, np.int64)
+    ok = (voxels >= 1) & (voxels <= nvox) & (dirs >= 0) & (dirs <= 5)
+    idx = np.where(ok, 6 * (voxels - 1) + dirs, 0)
+    c = np.where(ok, palette[idx], np.uint32(0xFFFF00FF))
+    c = np.where(dirs == 6, np.uint32(0xFFFEBF00), c)
+    c = np.where(dirs == 7, np.uint32(0xFF07193F), c)
+    return c.astype(np.uint32)
+
+
+def shade_bounce(dirs: np.ndarray, voxels: np.ndarray, dirs2: np.ndarray, palette: np.ndarray) -> np.ndarray:
+    """Config 5 pixels (vectorised restatement of ora_shade_bounce)."""
+    c = shade_fast(dirs, voxels, palette)
+    dark = (np.asarray(dirs) >= 0) & (np.asarray(dirs) <= 5) & (np.asarray(dirs2) != 6)
+    return np.where(dark, ((c >> 1) & np.uint32(0x007F7F7F)) | (c & np.uint32(0xFF000000)), c).astype(np.uint32)
 
 
 def raygen(yaw: float, pitch: float, fov: float, W: int, H: int) -> np.ndarray:

@@ -294,3 +294,79 @@ def test_depth12_camera_frame(ort, O, gpu_device):
         ref = O.trace_batch(ref_pool, O.Rcp(None), ORIGIN, rays, nthreads=16, want_push=True)
         assert_same(gpu_trace_dev(pool, ORIGIN, rays), ref)
     pool.close()
+
+
+def gpu_trace_bounce_dev(pool, origins, dirs):
+    import torch
+    dev = torch.device("cuda", 0)
+    dirs = np.ascontiguousarray(dirs, np.float32).reshape(-1, 3)
+    n = dirs.shape[0]
+    o = torch.from_numpy(np.ascontiguousarray(origins, np.float32).reshape(-1)).to(dev)
+    d = torch.from_numpy(dirs.reshape(-1)).to(dev)
+    bufs = [torch.empty(n, dtype=t, device=dev) for t in
+            (torch.int32, torch.int32, torch.float32, torch.int32, torch.int32, torch.float32, torch.int32)]
+    pool.set_stream(torch.cuda.current_stream())
+    pool.trace_bounce_batch_dev(o, d, *bufs[:6], push=bufs[6], n=n)
+    torch.cuda.synchronize()
+    hd, hv, ht, hd2, hv2, ht2, hp = (b.cpu().numpy() for b in bufs)
+    return {"dir": hd, "voxel": hv.view(np.uint32), "t": ht.view(np.uint32), "dir2": hd2,
+            "voxel2": hv2.view(np.uint32), "t2": ht2.view(np.uint32), "push": hp.view(np.uint32)}
+
+
+def assert_same_bounce(gpu, ref):
+    for k in ("dir", "voxel", "dir2", "voxel2", "push"):
+        assert np.array_equal(gpu[k], np.asarray(ref[k]).view(gpu[k].dtype)), (k, _first_diff(gpu[k], np.asarray(ref[k])))
+    for k in ("t", "t2"):
+        assert np.array_equal(gpu[k], np.asarray(ref[k]).view(np.uint32)), k
+
+
+@pytest.mark.parametrize("depth", [8, 10])
+def test_bounce_records(ort, O, gpu_device, depth):
+    """Config 5: primary and secondary hit records, bit for bit, camera frame and random rays."""
+    tree = ort.build_terrain(depth)
+    pool = ort.HOctree(tree.nodes, tree.root, depth, device=0)
+    ref_pool = O.OraclePool(tree.nodes, tree.root, depth, 1)
+    rays = O.raygen(0.3, -0.6, 1.25, 1920, 1080)
+    rng = np.random.default_rng(5)
+    ro = rng.uniform(1.01, 1.99, (100000, 3)).astype(np.float32)
+    rd = rng.uniform(-1, 1, (100000, 3)).astype(np.float32)
+    rd /= np.linalg.norm(rd, axis=1, keepdims=True)
+    for layout in (1, 0):
+        pool.set_option("layout", layout)
+        for origins, dirs in ((ORIGIN, rays), (ro, rd)):
+            ref = O.trace_bounce_batch(ref_pool, O.Rcp(None), origins, dirs, nthreads=16, want_push=True)
+            assert_same_bounce(gpu_trace_bounce_dev(pool, origins, dirs), ref)
+    pool.close()
+
+
+def test_render_bounce_frames(ort, O, gpu_device):
+    """Config 5 frames (two views, one launch), whole and row-sharded, vs the oracle's shading."""
+    import torch
+    tree = ort.build_terrain(9)
+    pal = ort.VoxelData().get_colours()
+    pool = ort.HOctree(tree.nodes, tree.root, 9, device=0)
+    pool.set_palette(pal)
+    pool.set_stream(torch.cuda.current_stream())
+    ref_pool = O.OraclePool(tree.nodes, tree.root, 9, 1)
+    W, H = 800, 450
+    cams = [ort.camera((1.5, 1.5, 1.5), 0.3, p, 1.25, W, H) for p in (0.0, -0.6)]
+    want = []
+    for p in (0.0, -0.6):
+        r = O.trace_bounce_batch(ref_pool, O.Rcp(None), ORIGIN, O.raygen(0.3, p, 1.25, W, H), nthreads=16)
+        want.append(O.shade_bounce(r["dir"], r["voxel"], r["dir2"], pal).reshape(H, W))
+    frames = torch.zeros((2, H, W), dtype=torch.int32, device="cuda")
+    pool.render_bounce_views_dev(cams, frames)
+    torch.cuda.synchronize()
+    for v in range(2):
+        assert np.array_equal(frames[v].cpu().numpy().view(np.uint32), want[v])
+    n, chunk = 3, 8
+    rows = ort.shard_rows(H, chunk, n)
+    gathered = torch.zeros((n, 2, rows, W), dtype=torch.int32, device="cuda")
+    for s_ in range(n):
+        pool.render_bounce_views_dev(cams, gathered[s_], chunk, s_, n)
+    full = torch.empty((2, H, W), dtype=torch.int32, device="cuda")
+    pool.unshard_dev(gathered, full, W, H, chunk, n, 2)
+    torch.cuda.synchronize()
+    for v in range(2):
+        assert np.array_equal(full[v].cpu().numpy().view(np.uint32), want[v])
+    pool.close()
