@@ -130,6 +130,9 @@ def main():
     ap.add_argument("--row-chunk", type=int, default=8)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=8.0)
+    ap.add_argument("--opt", action="append", default=[], metavar="NAME=VALUE",
+                    help="pool launch option (och_gpu_set_option), e.g. tile_order=1")
+    ap.add_argument("--no-bounce", action="store_true", help="skip the config-5 (secondary rays) measurement")
     ap.add_argument("--inflight", type=int, default=3,
                     help="frames in flight: steps alternate over this many HIP streams, so one step's "
                          "slowest rays overlap the next step's bulk (1 = serialised)")
@@ -156,6 +159,9 @@ def main():
     nodes, root, tree_nodes, build_s = build_pool_nodes(a.depth, rank, world, dev)
     pool = ort.HOctree(nodes, root, a.depth, device=local)
     pool.set_palette(ort.VoxelData().get_colours())
+    for kv in a.opt:
+        k, v = kv.split("=")
+        pool.set_option(k, int(v))
     stream = torch.cuda.current_stream()
     pool.set_stream(stream)
     cams = [ort.camera(ORIGIN, YAW, p, FOV, W, H) for p in PITCHES]
@@ -207,7 +213,7 @@ def main():
                       "bytes_per_ray": 12 + 12 + 4 * push_total / (W * H * len(cams))}
         del hd, hv, ht, hp
 
-    def step(k, ev=None):
+    def step(k, ev=None, bounce=False):
         """One step: render both views of this rank's rows, all-gather, unshard --
         on stream k % inflight, into that stream's own frame buffers."""
         s_, f_ = streams[k % len(streams)], sfs[k % len(sfs)]
@@ -216,7 +222,7 @@ def main():
             if ev is not None:
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record(s_)
-            f_.render_local(cams)
+            f_.render_local(cams, bounce)
             if ev is not None:
                 e1.record(s_)
                 ev.append((e0, e1))
@@ -250,6 +256,49 @@ def main():
     if world > 1:
         dist.all_reduce(t_max, op=dist.ReduceOp.MAX)
     elapsed = float(t_max.item())
+
+    # Config 5 (BASELINE configs[4]): the same frames with one mirrored
+    # secondary ray per hit pixel, in-block wavefront compaction on; same
+    # pipelining and timing discipline.  Rays = primary + secondary.
+    bounce = None
+    if not a.no_bounce:
+        def timed_steps(n, bounce_on=True):
+            for k in range(2):
+                step(k, None, bounce_on)
+            torch.cuda.synchronize()
+            if world > 1:
+                dist.barrier()
+            torch.cuda.synchronize()
+            bev = []
+            tb = time.perf_counter()
+            for k in range(n):
+                step(k, bev, bounce_on)
+            torch.cuda.synchronize()
+            if world > 1:
+                dist.barrier()
+            torch.cuda.synchronize()
+            el = torch.tensor([time.perf_counter() - tb], dtype=torch.float64, device=dev)
+            if world > 1:
+                dist.all_reduce(el, op=dist.ReduceOp.MAX)
+            return float(el.item()), float(np.mean([x.elapsed_time(y) for x, y in bev]))
+        b_el, b_kms = timed_steps(a.steps)
+        pool.set_option("bounce_compact", 0)
+        nc_el, nc_kms = timed_steps(max(a.steps // 2, 3))
+        pool.set_option("bounce_compact", 1)
+        pool.set_stream(stream)
+        hits = torch.tensor([hits_total], dtype=torch.int64, device=dev)
+        if world > 1:
+            dist.all_reduce(hits)
+        secondary = int(hits.item())
+        primary = W * H * len(cams)
+        bounce = {"workload": "configs[4]: depth-12, primary + 1-bounce secondary rays (divergent), "
+                              "wavefront compaction on" + ("" if world == 1 else f", {world} GPUs"),
+                  "value": round((primary + secondary) * a.steps / b_el / 1e6, 2), "unit": "Mrays/s",
+                  "primary_mrays_s": round(primary * a.steps / b_el / 1e6, 2),
+                  "ms_per_step": round(b_el / a.steps * 1e3, 4), "secondary_rays_per_step": secondary,
+                  "kernel_ms": round(b_kms, 4),
+                  "compaction_off_ms_per_step": round(nc_el / max(a.steps // 2, 3) * 1e3, 4),
+                  "compaction_off_kernel_ms": round(nc_kms, 4)}
 
     frames = a.steps * len(cams)
     total_rays = W * H * frames
@@ -287,7 +336,8 @@ def main():
                        "pitches": list(PITCHES), "yaw": YAW, "fov": FOV, "row_chunk": a.row_chunk,
                        "dag_nodes": int(nodes.shape[0]), "tree_nodes": tree_nodes,
                        "pool_mb": round(nodes.nbytes / 2**20, 1), "build_s": round(build_s, 2),
-                       "parallelism": f"rows{world}"},
+                       "parallelism": f"rows{world}",
+                       "options": {k: pool.get_option(k) for k in pool.OPTIONS}},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 5),
                          "traffic": None if pmc is None else pmc.get("hbm_bytes_per_launch"),
@@ -298,6 +348,7 @@ def main():
                          "note": "pointer-chase over an L2/MALL-resident DAG: latency/VALU-bound, not HBM-bound"},
             "cpu_baseline": cpu,
             "trace_batch": trace_only,
+            "bounce": bounce,
         }
         print(json.dumps(line), flush=True)
     pool.close()

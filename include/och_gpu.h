@@ -134,8 +134,10 @@ typedef enum och_option {
     OCH_OPT_LAYOUT = 4,        /* 0 = the caller's node layout; 1 = packed (default when the DAG has < 2^24
                                   (node, level) pairs): per-level breadth-first ids, interior slots carry the
                                   child's occupancy mask so only descents and hits touch memory */
-    OCH_OPT_TILE_ORDER = 5     /* camera rays (render): 0 = 8x8-pixel tiles row-major; 1 = 64x64-pixel supertiles,
+    OCH_OPT_TILE_ORDER = 5,    /* camera rays (render): 0 = 8x8-pixel tiles row-major; 1 = 64x64-pixel supertiles,
                                   each handed to one XCD so neighbouring rays share that XCD's L2 */
+    OCH_OPT_BOUNCE_COMPACT = 6 /* config 5: 1 (default) = compact each block's secondary rays into its first lanes
+                                  (wave ballot/popcount + LDS queue) before tracing them; 0 = trace in place */
 } och_option;
 OCH_API int och_gpu_set_option(och_gpu_pool *pool, int option, int value);
 OCH_API int och_gpu_get_option(const och_gpu_pool *pool, int option, int *value);

@@ -146,6 +146,7 @@ struct och_gpu_pool {
     uint32_t packed_nodes = 0;
     int opt_layout = 1;
     int opt_tile_order = 0;
+    int opt_bounce_compact = 1;
     // host-call staging
     void *d_scratch = nullptr;
     size_t scratch_bytes = 0;
@@ -160,6 +161,7 @@ struct och_gpu_pool {
         sc.waves_per_cu = opt_waves_per_cu;
         sc.refill_min = opt_refill;
         sc.tile_order = opt_tile_order;
+        sc.bounce_compact = opt_bounce_compact;
         sc.cus = cus;
         sc.counter = d_counter;
         sc.stamps = stamps;
@@ -541,6 +543,10 @@ OCH_API int och_gpu_set_option(och_gpu_pool *p, int option, int value)
         if (value != 0 && value != 1) return fail(OCH_E_INVALID, "tile order must be 0 or 1");
         p->opt_tile_order = value;
         return OCH_OK;
+    case OCH_OPT_BOUNCE_COMPACT:
+        if (value != 0 && value != 1) return fail(OCH_E_INVALID, "bounce compaction must be 0 or 1");
+        p->opt_bounce_compact = value;
+        return OCH_OK;
     default:
         return fail(OCH_E_INVALID, "unknown option %d", option);
     }
@@ -556,6 +562,7 @@ OCH_API int och_gpu_get_option(const och_gpu_pool *p, int option, int *value)
     case OCH_OPT_REFILL: *value = p->opt_refill; return OCH_OK;
     case OCH_OPT_LAYOUT: *value = (p->opt_layout == 1 && p->d_packed) ? 1 : 0; return OCH_OK;
     case OCH_OPT_TILE_ORDER: *value = p->opt_tile_order; return OCH_OK;
+    case OCH_OPT_BOUNCE_COMPACT: *value = p->opt_bounce_compact; return OCH_OK;
     default: return fail(OCH_E_INVALID, "unknown option %d", option);
     }
 }

@@ -45,6 +45,7 @@ struct Schedule {
     int waves_per_cu;       // persistent grid size per CU
     int refill_min;         // refill once this many lanes of a wave are idle
     int tile_order;         // camera rays: 0 row-major 8x8 tiles, 1 supertiles grouped per XCD
+    int bounce_compact;     // config 5: compact the block's secondary rays into its first lanes
     int cus;                // compute units of the device
     uint32_t *counter;      // device ray counter (persistent)
     uint64_t *stamps;       // optional per-wave residency records

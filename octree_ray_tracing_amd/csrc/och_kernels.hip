@@ -492,7 +492,8 @@ __global__ void k_trace_grid(DevPool P, Src S, Sink K, uint32_t xcd_group, uint6
 // a few bounced lanes.  stack_words: LDS words of the parent stacks; the
 // queue (8 words per thread, SoA) follows them.
 template <class Src, class Sink, bool kPacked, bool kCount>
-__global__ void k_trace_bounce(DevPool P, Src S, Sink K, uint32_t stack_words, uint64_t *stamps, uint32_t stamp_cap)
+__global__ void k_trace_bounce(DevPool P, Src S, Sink K, uint32_t stack_words, int compact, uint64_t *stamps,
+                               uint32_t stamp_cap)
 {
     extern __shared__ uint32_t lds_stack[];
     __shared__ uint32_t wave_count[16];
@@ -514,6 +515,17 @@ __global__ void k_trace_bounce(DevPool P, Src S, Sink K, uint32_t stack_words, u
         want = h1.dir < OCH_EXIT;
         if (want) bounce_ray(o, d, h1, P.half_voxel, o2, d2);
         payload = K.put_primary(out, h1, want);
+        if (want && !compact) {                                             // in place, no compaction
+            ray_init<kPacked>(r, P, o2, d2);
+            do {
+                ray_iterate<kPacked, kCount>(r, P, stack, nb);
+            } while (ray_active(r, P));
+            K.put_secondary(out, payload, ray_result(r, P));
+        }
+    }
+    if (!compact) {
+        if (stamps) stamp(stamps, stamp_cap, t0, 0);
+        return;
     }
     const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
     const uint64_t bal = __ballot(want);
@@ -673,10 +685,10 @@ hipError_t launch_bounce(const DevPool &p, const Src &s, const Sink &k, uint32_t
     const dim3 grid((n + block - 1) / block);
     if (p.packed)
         hipLaunchKernelGGL((k_trace_bounce<Src, Sink, true, kCount>), grid, dim3(block), lds, stream, p, s, k,
-                           stack_words, sc.stamps, sc.stamp_cap);
+                           stack_words, sc.bounce_compact, sc.stamps, sc.stamp_cap);
     else
         hipLaunchKernelGGL((k_trace_bounce<Src, Sink, false, kCount>), grid, dim3(block), lds, stream, p, s, k,
-                           stack_words, sc.stamps, sc.stamp_cap);
+                           stack_words, sc.bounce_compact, sc.stamps, sc.stamp_cap);
     return hipGetLastError();
 }
 

@@ -61,11 +61,14 @@ class ShardedFrame:
         self.frames = torch.empty((n_views, height, width), dtype=torch.int32, device=dev)
         pool.set_stream(torch.cuda.current_stream())
 
-    def render_local(self, cams):
+    def render_local(self, cams, bounce: bool = False):
+        """This rank's rows of every view; bounce=True renders config 5 (one
+        mirrored secondary ray per hit pixel)."""
         if not isinstance(cams, (list, tuple)):
             cams = [cams]
         assert len(cams) == self.n_views
-        self.pool.render_views_dev(list(cams), self.slice, self.row_chunk, self.rank, self.world)
+        render = self.pool.render_bounce_views_dev if bounce else self.pool.render_views_dev
+        render(list(cams), self.slice, self.row_chunk, self.rank, self.world)
         return self.slice
 
     def exchange(self):
@@ -78,6 +81,6 @@ class ShardedFrame:
         self.pool.unshard_dev(src, self.frames, self.width, self.height, self.row_chunk, self.world, self.n_views)
         return self.frames
 
-    def render(self, cams):
-        self.render_local(cams)
+    def render(self, cams, bounce: bool = False):
+        self.render_local(cams, bounce)
         return self.exchange()

@@ -142,7 +142,8 @@ class GpuPool:
         nodes = np.ascontiguousarray(nodes, np.uint32).reshape(-1, 8)
         call("och_gpu_pool_update", self._h, int(first), nodes.shape[0], _np_ptr(nodes), int(root))
 
-    OPTIONS = {"schedule": 0, "block": 1, "waves_per_cu": 2, "refill": 3, "layout": 4, "tile_order": 5}
+    OPTIONS = {"schedule": 0, "block": 1, "waves_per_cu": 2, "refill": 3, "layout": 4, "tile_order": 5,
+               "bounce_compact": 6}
 
     def set_option(self, name: str, value: int):
         """Launch schedule: schedule (0 grid / 1 persistent), block, waves_per_cu, refill."""
