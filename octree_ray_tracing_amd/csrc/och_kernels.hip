@@ -59,8 +59,8 @@ struct Ray {
     uint32_t inv;         // direction-sign mask (1 = positive)
     uint32_t idx;         // child index bits at the current level
     uint32_t dim;         // mantissa bit of the current child size
-    uint32_t node;
-    uint32_t mask;        // packed layout: non-empty children of `node`
+    uint32_t cur;         // the current node: packed slot word (id | child mask << 24), or raw index
+    uint32_t *sp;         // this lane's LDS stack slot for the current level (parents below it)
     uint32_t t_min;       // bits of the entry t of the current cell
     uint32_t min_axis;    // 1, 2, 4 (last STEP axis) or 8 (none yet)
     uint32_t voxel;       // the hit voxel id (valid once level > depth)
@@ -73,9 +73,27 @@ struct Ray {
 
 constexpr uint32_t kIdMask = 0x00FFFFFFu;
 
-// Setup, ORT/och_h_octree.h:294-338.
-template <bool kPacked>
-__device__ __forceinline__ void ray_init(Ray &r, const DevPool &P, const float *o, const float *d)
+// The PUSH test and slot fetch (ORT/och_h_octree.h:342-344): the packed
+// layout tests presence with the child mask held in the node's slot word and
+// loads only present children; the raw layout loads every slot and tests it
+// when the load has landed (ray_phase_descend).
+template <bool kPacked, bool kCount>
+__device__ __forceinline__ void ray_push(Ray &r, const DevPool &P)
+{
+    if (kCount) ++r.push;
+    const uint32_t c = r.idx ^ r.inv;
+    if (!kPacked || ((r.cur >> 24 >> c) & 1u)) {
+        r.child = P.nodes[8u * (kPacked ? (r.cur & kIdMask) : r.cur) + c];
+        r.pending = true;
+    } else {
+        r.stepping = true;
+    }
+}
+
+// Setup, ORT/och_h_octree.h:294-338, then the first PUSH at the root.
+// stack: this lane's first LDS slot.
+template <bool kPacked, bool kCount>
+__device__ __forceinline__ void ray_init(Ray &r, const DevPool &P, const float *o, const float *d, uint32_t *stack)
 {
     r.inv = 0;
     r.idx = 0;
@@ -96,8 +114,8 @@ __device__ __forceinline__ void ray_init(Ray &r, const DevPool &P, const float *
         r.idx |= (uint32_t)(r.p[a] == 0x3FC00000u) << a;                    // :324
     }
     r.dim = 1u << 22;                                                       // :326
-    r.node = kPacked ? (P.root & kIdMask) : P.root;
-    r.mask = P.root >> 24;
+    r.cur = P.root;
+    r.sp = stack;
     r.t_min = 0;                                                            // +0.0F
     r.level = 1;
     r.min_axis = 8;
@@ -106,14 +124,7 @@ __device__ __forceinline__ void ray_init(Ray &r, const DevPool &P, const float *
     r.pending = false;
     r.child = 0;
     r.push = 0;
-    const uint32_t c = r.idx ^ r.inv;                                       // the first PUSH, at the root
-    r.push = 1;
-    if (!kPacked || ((r.mask >> c) & 1u)) {
-        r.child = P.nodes[8u * r.node + c];
-        r.pending = true;
-    } else {
-        r.stepping = true;
-    }
+    ray_push<kPacked, true>(r, P);
 }
 
 // The PUSH / STEP / POP machine (ORT/och_h_octree.h:342-446,
@@ -124,111 +135,89 @@ __device__ __forceinline__ void ray_init(Ray &r, const DevPool &P, const float *
 //              previous iteration's push) hit or descend;
 //   push    -- every lane now at a PUSH tests its child and, if present,
 //              issues the load of the child's slot word.
-// The packed layout tests presence with the child mask held since the node
-// was entered, so only present children are loaded and the order is
-// step, descend, push.  The raw layout must load every PUSH's slot to test it,
-// so it resolves the slot first (descend, step, push): an empty child then
-// STEPs in the same iteration.
-// stack: this lane's first LDS slot, levels `stride` words apart.
-template <bool kPacked, bool kCount>
-__device__ __forceinline__ void ray_phase_step(Ray &r, const DevPool &P, uint32_t *stack, uint32_t stride)
+// The packed layout orders them step, descend, push.  The raw layout must
+// load every PUSH's slot to test it, so it resolves the slot first (descend,
+// step, push): an empty child then STEPs in the same iteration.
+// stride: words between two levels of one lane's LDS stack.
+template <bool kPacked>
+__device__ __forceinline__ void ray_phase_step(Ray &r, uint32_t stride)
 {
-    if (r.stepping) {
-        // STEP :378-419.  The reference's cascade (x if tx <= ty && tx <= tz,
-        // else y if ty < tx && ty <= tz, else z) picks the first axis holding
-        // the unsigned minimum.
-        const uint32_t tx = fbits(__builtin_fmaf(ffrom(r.p[0]), r.c[0], r.b[0])) | r.nan_or[0];
-        const uint32_t ty = fbits(__builtin_fmaf(ffrom(r.p[1]), r.c[1], r.b[1])) | r.nan_or[1];
-        const uint32_t tz = fbits(__builtin_fmaf(ffrom(r.p[2]), r.c[2], r.b[2])) | r.nan_or[2];
-        const uint32_t tm = min(min(tx, ty), tz);
-        const bool sx = tx == tm;
-        const bool sy = !sx && ty == tm;
-        const bool sz = !sx && !sy;
-        const uint32_t axis = sx ? 1u : (sy ? 2u : 4u);
-        r.min_axis = axis;
-        r.t_min = tm;
-        const bool adv = r.idx & axis;
-        r.stepping = !adv;
-        if (adv) {                                                          // advance :413-419
-            const uint32_t clr = ~r.dim;
-            r.p[0] &= sx ? clr : 0xFFFFFFFFu;
-            r.p[1] &= sy ? clr : 0xFFFFFFFFu;
-            r.p[2] &= sz ? clr : 0xFFFFFFFFu;
-            r.idx ^= axis;
-        } else if (--r.level != 0) {                                        // POP :421-446 (0: MISS :423-431)
-            const uint32_t e = stack[(uint32_t)(r.level - 1) * stride];      // :434
-            r.node = kPacked ? (e & kIdMask) : e;
-            r.mask = e >> 24;
+    // STEP :378-419.  The reference's cascade (x if tx <= ty && tx <= tz, else
+    // y if ty < tx && ty <= tz, else z) picks the first axis holding the
+    // unsigned minimum.
+    const uint32_t tx = fbits(__builtin_fmaf(ffrom(r.p[0]), r.c[0], r.b[0])) | r.nan_or[0];
+    const uint32_t ty = fbits(__builtin_fmaf(ffrom(r.p[1]), r.c[1], r.b[1])) | r.nan_or[1];
+    const uint32_t tz = fbits(__builtin_fmaf(ffrom(r.p[2]), r.c[2], r.b[2])) | r.nan_or[2];
+    const uint32_t tm = min(min(tx, ty), tz);
+    const bool sx = tx == tm;
+    const bool sy = !sx && ty == tm;
+    const bool sz = !sx && !sy;
+    const uint32_t axis = sx ? 1u : (sy ? 2u : 4u);
+    r.min_axis = axis;
+    r.t_min = tm;
+    const bool adv = r.idx & axis;
+    r.stepping = !adv;
+    if (adv) {                                                              // advance :413-419
+        const uint32_t clr = ~r.dim;
+        r.p[0] &= sx ? clr : 0xFFFFFFFFu;
+        r.p[1] &= sy ? clr : 0xFFFFFFFFu;
+        r.p[2] &= sz ? clr : 0xFFFFFFFFu;
+        r.idx ^= axis;
+    } else if (--r.level != 0) {                                            // POP :421-446 (0: MISS :423-431)
+        r.sp -= stride;
+        r.cur = *r.sp;                                                      // :434
 #pragma unroll
-            for (int a = 0; a < 3; ++a) r.p[a] &= ~r.dim;                   // :436
-            r.dim <<= 1;                                                    // :438
-            r.idx = (uint32_t)((r.p[0] & r.dim) != 0) | ((uint32_t)((r.p[1] & r.dim) != 0) << 1) |
-                    ((uint32_t)((r.p[2] & r.dim) != 0) << 2);               // :440-444
-        }
+        for (int a = 0; a < 3; ++a) r.p[a] &= ~r.dim;                       // :436
+        r.dim <<= 1;                                                        // :438
+        r.idx = (uint32_t)((r.p[0] & r.dim) != 0) | ((uint32_t)((r.p[1] & r.dim) != 0) << 1) |
+                ((uint32_t)((r.p[2] & r.dim) != 0) << 2);                   // :440-444
     }
 }
 
-template <bool kPacked, bool kCount>
-__device__ __forceinline__ void ray_phase_descend(Ray &r, const DevPool &P, uint32_t *stack, uint32_t stride)
+template <bool kPacked>
+__device__ __forceinline__ void ray_phase_descend(Ray &r, const DevPool &P, uint32_t stride)
 {
-    if (r.pending) {
-        r.pending = false;
-        const uint32_t child = r.child;
-        if (kPacked || child != 0) {
-            if (r.level == P.depth) {                                       // HIT :346-355
-                r.voxel = child;
-                r.level = P.depth + 1;
-            } else {
-                stack[(uint32_t)(r.level - 1) * stride] = kPacked ? (r.node | (r.mask << 24)) : r.node;   // :357
-                ++r.level;
-                r.node = kPacked ? (child & kIdMask) : child;
-                r.mask = child >> 24;
-                r.dim >>= 1;                                                // :361
-                const float tm = ffrom(r.t_min);
-                uint32_t nidx = 0;
+    r.pending = false;
+    const uint32_t child = r.child;
+    if (!kPacked && child == 0) {                                           // raw layout: empty child
+        r.stepping = true;
+        return;
+    }
+    if (r.level == P.depth) {                                               // HIT :346-355
+        r.voxel = child;
+        r.level = P.depth + 1;
+        return;
+    }
+    *r.sp = r.cur;                                                          // :357
+    r.sp += stride;
+    ++r.level;
+    r.cur = child;
+    r.dim >>= 1;                                                            // :361
+    const float tm = ffrom(r.t_min);
+    uint32_t nidx = 0;
 #pragma unroll
-                for (int a = 0; a < 3; ++a) {                               // :363-373
-                    const float t_mid = __builtin_fmaf(ffrom(r.p[a] | r.dim), r.c[a], r.b[a]);
-                    const bool upper = t_mid >= tm;
-                    nidx |= (uint32_t)upper << a;
-                    r.p[a] |= upper ? r.dim : 0u;
-                }
-                r.idx = nidx;
-            }
-        } else {
-            r.stepping = true;                                              // raw layout: empty child
-        }
+    for (int a = 0; a < 3; ++a) {                                           // :363-373
+        const float t_mid = __builtin_fmaf(ffrom(r.p[a] | r.dim), r.c[a], r.b[a]);
+        const bool upper = t_mid >= tm;
+        nidx |= (uint32_t)upper << a;
+        r.p[a] |= upper ? r.dim : 0u;
     }
-}
-
-template <bool kPacked, bool kCount>
-__device__ __forceinline__ void ray_phase_push(Ray &r, const DevPool &P, uint32_t *stack, uint32_t stride)
-{
-    if (!r.stepping && (uint32_t)(r.level - 1) < (uint32_t)P.depth) {       // PUSH :342-344
-        if (kCount) ++r.push;
-        const uint32_t c = (r.idx ^ r.inv) & 7u;
-        if (!kPacked || ((r.mask >> c) & 1u)) {
-            r.child = P.nodes[8u * r.node + c];
-            r.pending = true;
-        } else {
-            r.stepping = true;
-        }
-    }
-}
-
-template <bool kPacked, bool kCount>
-__device__ __forceinline__ void ray_iterate(Ray &r, const DevPool &P, uint32_t *stack, uint32_t stride)
-{
-    if (!kPacked) ray_phase_descend<kPacked, kCount>(r, P, stack, stride);
-    ray_phase_step<kPacked, kCount>(r, P, stack, stride);
-    if (kPacked) ray_phase_descend<kPacked, kCount>(r, P, stack, stride);
-    ray_phase_push<kPacked, kCount>(r, P, stack, stride);
+    r.idx = nidx;
 }
 
 // Still walking: level in 1..depth (0 = missed, depth + 1 = hit).
 __device__ __forceinline__ bool ray_active(const Ray &r, const DevPool &P)
 {
     return (uint32_t)(r.level - 1) < (uint32_t)P.depth;
+}
+
+template <bool kPacked, bool kCount>
+__device__ __forceinline__ void ray_iterate(Ray &r, const DevPool &P, uint32_t stride)
+{
+    if (!kPacked && r.pending) ray_phase_descend<kPacked>(r, P, stride);
+    if (r.stepping) ray_phase_step<kPacked>(r, stride);
+    if (kPacked && r.pending) ray_phase_descend<kPacked>(r, P, stride);
+    if (!r.stepping && ray_active(r, P)) ray_push<kPacked, kCount>(r, P);   // PUSH :342-344
 }
 
 // The hit record of a finished ray (:346-355 hit, :423-431 miss).
@@ -476,9 +465,9 @@ __global__ void k_trace_grid(DevPool P, Src S, Sink K, uint32_t xcd_group, uint6
     uint32_t out;
     if (i < S.count() && S.get(i, o, d, out)) {
         Ray r;
-        ray_init<kPacked>(r, P, o, d);
+        ray_init<kPacked, kCount>(r, P, o, d, lds_stack + threadIdx.x);
         do {
-            ray_iterate<kPacked, kCount>(r, P, lds_stack + threadIdx.x, blockDim.x);
+            ray_iterate<kPacked, kCount>(r, P, blockDim.x);
         } while (ray_active(r, P));
         K.put(out, ray_result(r, P));
     }
@@ -507,18 +496,18 @@ __global__ void k_trace_bounce(DevPool P, Src S, Sink K, uint32_t stack_words, i
     bool want = false;
     if (i < S.count() && S.get(i, o, d, out)) {
         Ray r;
-        ray_init<kPacked>(r, P, o, d);
+        ray_init<kPacked, kCount>(r, P, o, d, stack);
         do {
-            ray_iterate<kPacked, kCount>(r, P, stack, nb);
+            ray_iterate<kPacked, kCount>(r, P, nb);
         } while (ray_active(r, P));
         const Hit h1 = ray_result(r, P);
         want = h1.dir < OCH_EXIT;
         if (want) bounce_ray(o, d, h1, P.half_voxel, o2, d2);
         payload = K.put_primary(out, h1, want);
         if (want && !compact) {                                             // in place, no compaction
-            ray_init<kPacked>(r, P, o2, d2);
+            ray_init<kPacked, kCount>(r, P, o2, d2, stack);
             do {
-                ray_iterate<kPacked, kCount>(r, P, stack, nb);
+                ray_iterate<kPacked, kCount>(r, P, nb);
             } while (ray_active(r, P));
             K.put_secondary(out, payload, ray_result(r, P));
         }
@@ -555,9 +544,9 @@ __global__ void k_trace_bounce(DevPool P, Src S, Sink K, uint32_t stack_words, i
         const float sd[3] = {ffrom(queue[3 * nb + q]), ffrom(queue[4 * nb + q]), ffrom(queue[5 * nb + q])};
         const uint32_t sout = queue[6 * nb + q], spay = queue[7 * nb + q];
         Ray r;
-        ray_init<kPacked>(r, P, so, sd);
+        ray_init<kPacked, kCount>(r, P, so, sd, stack);
         do {
-            ray_iterate<kPacked, kCount>(r, P, stack, nb);
+            ray_iterate<kPacked, kCount>(r, P, nb);
         } while (ray_active(r, P));
         K.put_secondary(sout, spay, ray_result(r, P));
     }
@@ -591,7 +580,7 @@ __global__ void k_trace_persistent(DevPool P, Src S, Sink K, uint32_t *counter, 
                 const uint32_t i = base + (uint32_t)__popcll(idle & below);
                 float o[3], d[3];
                 if (i < n && S.get(i, o, d, out)) {
-                    ray_init<kPacked>(r, P, o, d);
+                    ray_init<kPacked, kCount>(r, P, o, d, stack);
                     active = true;
                 }
             }
@@ -601,7 +590,7 @@ __global__ void k_trace_persistent(DevPool P, Src S, Sink K, uint32_t *counter, 
             continue;
         }
         if (active) {
-            ray_iterate<kPacked, kCount>(r, P, stack, blockDim.x);
+            ray_iterate<kPacked, kCount>(r, P, blockDim.x);
             if (!ray_active(r, P)) {
                 K.put(out, ray_result(r, P));
                 active = false;
