@@ -54,7 +54,6 @@ struct Hit {
 // Traversal state of one ray between iterations.
 struct Ray {
     float c[3], b[3];     // coefficient (RCPPS of -|d|) and bias (-c * o') per axis
-    uint32_t nan_or[3];   // 0xFFC00000 where c is +-inf (t is NaN at every STEP), else 0
     uint32_t p[3];        // position bits in the reflected frame
     uint32_t inv;         // direction-sign mask (1 = positive)
     uint32_t idx;         // child index bits at the current level
@@ -106,10 +105,16 @@ __device__ __forceinline__ void ray_init(Ray &r, const DevPool &P, const float *
         const uint32_t cb = rcpps(db | 0x80000000u, P.lut, P.lut_shift);     // :312, :316
         r.c[a] = ffrom(cb);
         r.b[a] = ffrom(fbits(__fmul_rn(r.c[a], refl)) ^ 0x80000000u);       // :318
-        // fma(p, -inf, +inf) is NaN for every p: x86 gives 0xFFC00000, gfx950
-        // 0x7FC00000; OR-ing 0xFFC00000 into t restores x86's pattern for the
-        // unsigned compare of STEP (:384-406).  A finite c never yields NaN.
-        r.nan_or[a] = ((cb & 0x7FFFFFFFu) == 0x7F800000u) ? kX86DefaultNaN : 0u;
+        // A zero or denormal d gives c = -inf, b = +inf and t = fma(p, -inf,
+        // +inf) = NaN at every STEP, which the unsigned compare (:384-406)
+        // must see as x86's default NaN 0xFFC00000.  Pin it independently of
+        // the GPU's default NaN: fma(p, 0, NaN) returns its NaN operand
+        // (measured on gfx950, tools/probes/nan_probe.hip), so c = 0 and
+        // b = 0xFFC00000 give that pattern at every STEP and every t_mid.
+        if ((cb & 0x7FFFFFFFu) == 0x7F800000u) {
+            r.c[a] = 0.0F;
+            r.b[a] = ffrom(kX86DefaultNaN);
+        }
         r.p[a] = fbits(refl) & 0x3FC00000u;                                 // :320
         r.idx |= (uint32_t)(r.p[a] == 0x3FC00000u) << a;                    // :324
     }
@@ -145,9 +150,9 @@ __device__ __forceinline__ void ray_phase_step(Ray &r, uint32_t stride)
     // STEP :378-419.  The reference's cascade (x if tx <= ty && tx <= tz, else
     // y if ty < tx && ty <= tz, else z) picks the first axis holding the
     // unsigned minimum.
-    const uint32_t tx = fbits(__builtin_fmaf(ffrom(r.p[0]), r.c[0], r.b[0])) | r.nan_or[0];
-    const uint32_t ty = fbits(__builtin_fmaf(ffrom(r.p[1]), r.c[1], r.b[1])) | r.nan_or[1];
-    const uint32_t tz = fbits(__builtin_fmaf(ffrom(r.p[2]), r.c[2], r.b[2])) | r.nan_or[2];
+    const uint32_t tx = fbits(__builtin_fmaf(ffrom(r.p[0]), r.c[0], r.b[0]));
+    const uint32_t ty = fbits(__builtin_fmaf(ffrom(r.p[1]), r.c[1], r.b[1]));
+    const uint32_t tz = fbits(__builtin_fmaf(ffrom(r.p[2]), r.c[2], r.b[2]));
     const uint32_t tm = min(min(tx, ty), tz);
     const bool sx = tx == tm;
     const bool sy = !sx && ty == tm;
