@@ -13,8 +13,17 @@ rows are dealt in 8-row chunks round-robin over ranks, and every frame ends
 with an RCCL all-gather of the framebuffer slices plus an on-device unshard.
 The node pool is built once on rank 0 and broadcast over RCCL.
 
+Steps alternate over --inflight (default 3) HIP streams with their own frame
+buffers, so one step's slowest rays (a few grazing tiles)
+overlap the next step's bulk; every step is rendered in full.  The serial
+frame latency is reported beside it (roofline.kernel_ms_idle_gpu).
+
 value = rays of all frames of all ranks / (max over ranks of the timed wall
 time), timed between barrier + synchronize on both sides.
+
+The same line carries config 5 (BASELINE configs[4]) under "bounce": the same
+frames with one mirrored secondary ray per hit pixel, in-block wavefront
+compaction on, rays = primary + secondary.
 """
 from __future__ import annotations
 
