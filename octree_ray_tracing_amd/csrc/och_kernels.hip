@@ -163,10 +163,11 @@ __device__ __forceinline__ void ray_phase_step(Ray &r, uint32_t stride)
     const bool adv = r.idx & axis;
     r.stepping = !adv;
     if (adv) {                                                              // advance :413-419
-        const uint32_t clr = ~r.dim;
-        r.p[0] &= sx ? clr : 0xFFFFFFFFu;
-        r.p[1] &= sy ? clr : 0xFFFFFFFFu;
-        r.p[2] &= sz ? clr : 0xFFFFFFFFu;
+        // idx bit `axis` set <=> that axis's position has the dim bit set, so
+        // clearing it (:415) is a toggle.
+        r.p[0] ^= sx ? r.dim : 0u;
+        r.p[1] ^= sy ? r.dim : 0u;
+        r.p[2] ^= sz ? r.dim : 0u;
         r.idx ^= axis;
     } else if (--r.level != 0) {                                            // POP :421-446 (0: MISS :423-431)
         r.sp -= stride;
@@ -174,8 +175,9 @@ __device__ __forceinline__ void ray_phase_step(Ray &r, uint32_t stride)
 #pragma unroll
         for (int a = 0; a < 3; ++a) r.p[a] &= ~r.dim;                       // :436
         r.dim <<= 1;                                                        // :438
-        r.idx = (uint32_t)((r.p[0] & r.dim) != 0) | ((uint32_t)((r.p[1] & r.dim) != 0) << 1) |
-                ((uint32_t)((r.p[2] & r.dim) != 0) << 2);                   // :440-444
+        const uint32_t k = __builtin_ctz(r.dim);                            // :440-444, bit k of each position
+        r.idx = __builtin_amdgcn_ubfe(r.p[0], k, 1) | (__builtin_amdgcn_ubfe(r.p[1], k, 1) << 1) |
+                (__builtin_amdgcn_ubfe(r.p[2], k, 1) << 2);
     }
 }
 
@@ -202,10 +204,10 @@ __device__ __forceinline__ void ray_phase_descend(Ray &r, const DevPool &P, uint
     uint32_t nidx = 0;
 #pragma unroll
     for (int a = 0; a < 3; ++a) {                                           // :363-373
-        const float t_mid = __builtin_fmaf(ffrom(r.p[a] | r.dim), r.c[a], r.b[a]);
-        const bool upper = t_mid >= tm;
+        const uint32_t mid = r.p[a] | r.dim;
+        const bool upper = __builtin_fmaf(ffrom(mid), r.c[a], r.b[a]) >= tm;
         nidx |= (uint32_t)upper << a;
-        r.p[a] |= upper ? r.dim : 0u;
+        r.p[a] = upper ? mid : r.p[a];
     }
     r.idx = nidx;
 }
