@@ -147,9 +147,9 @@ __device__ __forceinline__ void ray_init(Ray &r, const DevPool &P, const float *
 template <bool kPacked>
 __device__ __forceinline__ void ray_phase_step(Ray &r, uint32_t stride)
 {
-    // STEP :378-419.  The reference's cascade (x if tx <= ty && tx <= tz, else
-    // y if ty < tx && ty <= tz, else z) picks the first axis holding the
-    // unsigned minimum.
+    // STEP :378-419.  The reference's cascade (x if tx <= ty && tx <= tz,
+    // else y if ty < tx && ty <= tz, else z) picks the first axis holding
+    // the unsigned minimum.
     const uint32_t tx = fbits(__builtin_fmaf(ffrom(r.p[0]), r.c[0], r.b[0]));
     const uint32_t ty = fbits(__builtin_fmaf(ffrom(r.p[1]), r.c[1], r.b[1]));
     const uint32_t tz = fbits(__builtin_fmaf(ffrom(r.p[2]), r.c[2], r.b[2]));
@@ -160,25 +160,25 @@ __device__ __forceinline__ void ray_phase_step(Ray &r, uint32_t stride)
     const uint32_t axis = sx ? 1u : (sy ? 2u : 4u);
     r.min_axis = axis;
     r.t_min = tm;
-    const bool adv = r.idx & axis;
-    r.stepping = !adv;
-    if (adv) {                                                              // advance :413-419
-        // idx bit `axis` set <=> that axis's position has the dim bit set, so
-        // clearing it (:415) is a toggle.
+    if (r.idx & axis) {                                                 // advance :413-419
+        // idx bit `axis` set <=> that axis's position has the dim bit set,
+        // so clearing it (:415) is a toggle.
         r.p[0] ^= sx ? r.dim : 0u;
         r.p[1] ^= sy ? r.dim : 0u;
         r.p[2] ^= sz ? r.dim : 0u;
         r.idx ^= axis;
-    } else if (--r.level != 0) {                                            // POP :421-446 (0: MISS :423-431)
-        r.sp -= stride;
-        r.cur = *r.sp;                                                      // :434
-#pragma unroll
-        for (int a = 0; a < 3; ++a) r.p[a] &= ~r.dim;                       // :436
-        r.dim <<= 1;                                                        // :438
-        const uint32_t k = __builtin_ctz(r.dim);                            // :440-444, bit k of each position
-        r.idx = __builtin_amdgcn_ubfe(r.p[0], k, 1) | (__builtin_amdgcn_ubfe(r.p[1], k, 1) << 1) |
-                (__builtin_amdgcn_ubfe(r.p[2], k, 1) << 2);
+        r.stepping = false;
+        return;
     }
+    if (--r.level == 0) return;                                         // MISS :423-431
+    r.sp -= stride;                                                     // POP :421-446
+    r.cur = *r.sp;                                                      // :434
+#pragma unroll
+    for (int a = 0; a < 3; ++a) r.p[a] &= ~r.dim;                       // :436
+    r.dim <<= 1;                                                        // :438
+    const uint32_t k = __builtin_ctz(r.dim);                            // :440-444, bit k of each position
+    r.idx = __builtin_amdgcn_ubfe(r.p[0], k, 1) | (__builtin_amdgcn_ubfe(r.p[1], k, 1) << 1) |
+            (__builtin_amdgcn_ubfe(r.p[2], k, 1) << 2);
 }
 
 template <bool kPacked>
@@ -302,6 +302,12 @@ __device__ __forceinline__ void camera_ray(const och_camera &C, int col, int row
     d[2] = __fmul_rn(-rv, rmag);
 }
 
+// Pixel tile of one wave: kTileW x kTileH = 64 pixels.
+#ifndef OCH_TILE_W
+#define OCH_TILE_W 8
+#endif
+constexpr uint32_t kTileW = OCH_TILE_W, kTileH = 64 / OCH_TILE_W;
+
 // Camera rays of one shard's slice for up to kMaxViews cameras of equal size,
 // enumerated view after view, 8x8 pixel tile after tile, so a wave's 64 rays
 // are one tile of one view (ray i -> tile i / 64, pixel i % 64).  Tiles run
@@ -326,8 +332,8 @@ struct CameraSource {
             tx = tile % tiles_x;
             ty = tile / tiles_x;
         }
-        const int col = (int)(tx * 8u + (lane & 7u));
-        const int srow = (int)(ty * 8u + (lane >> 3));
+        const int col = (int)(tx * kTileW + lane % kTileW);
+        const int srow = (int)(ty * kTileH + lane / kTileW);
         if (col >= width || srow >= slice_rows) return false;
         const int chunk = srow / row_chunk, within = srow - chunk * row_chunk;
         const int row = (chunk * n_shards + shard) * row_chunk + within;
@@ -699,9 +705,9 @@ CameraSource camera_source(const DevFrame &f, const Schedule &sc)
     src.slice_rows = f.slice_rows;
     src.width = f.cams[0].width;
     src.height = f.cams[0].height;
-    src.tiles_x = (uint32_t)(src.width + 7) / 8;
+    src.tiles_x = (uint32_t)(src.width + kTileW - 1) / kTileW;
     src.order = sc.tile_order;
-    const uint32_t tiles_y = (uint32_t)(f.slice_rows + 7) / 8;
+    const uint32_t tiles_y = (uint32_t)(f.slice_rows + kTileH - 1) / kTileH;
     src.supertiles_x = (src.tiles_x + 7) / 8;
     src.per_view = sc.tile_order == 1 ? src.supertiles_x * ((tiles_y + 7) / 8) * 64u * 64u : src.tiles_x * tiles_y * 64u;
     src.slice_pixels = (uint32_t)f.slice_rows * (uint32_t)src.width;
