@@ -57,6 +57,20 @@ def frame_size(n_gpus: int, width: int | None, height: int | None):
     return int(round(1920 * s)), int(round(1080 * s))
 
 
+def coll(fn, t, *args, **kw):
+    """Run a collective on `t`.  RCCL takes device tensors; the gloo rehearsal
+    backend (OCH_DIST_BACKEND=gloo, several ranks on one GPU) goes through the
+    host."""
+    import torch.distributed as dist
+
+    if dist.get_backend() == "gloo" and t.is_cuda:
+        h = t.cpu()
+        fn(h, *args, **kw)
+        t.copy_(h)
+    else:
+        fn(t, *args, **kw)
+
+
 def build_pool_nodes(depth: int, rank: int, world: int, dev):
     """Rank 0 builds the DAG; the node array is broadcast to the other ranks."""
     import torch
@@ -67,17 +81,28 @@ def build_pool_nodes(depth: int, rank: int, world: int, dev):
     nodes = None
     build_s = 0.0
     if rank == 0:
-        tree = ort.build_terrain(depth)
-        nodes, build_s = tree.nodes, tree.build_seconds
-        meta[:] = torch.tensor([tree.n_nodes, tree.root, tree.tree_nodes])
+        # OCH_TREE_CACHE=<file.npz>: reuse a DAG built by an earlier run in the
+        # same job (A/B tooling); off by default, every bench builds its tree.
+        cache = os.environ.get("OCH_TREE_CACHE")
+        if cache and os.path.exists(cache) and int(np.load(cache)["depth"]) == depth:
+            z = np.load(cache)
+            nodes, build_s = z["nodes"], float(z["build_s"])
+            meta[:] = torch.tensor([nodes.shape[0], int(z["root"]), int(z["tree_nodes"])])
+        else:
+            tree = ort.build_terrain(depth)
+            nodes, build_s = tree.nodes, tree.build_seconds
+            meta[:] = torch.tensor([tree.n_nodes, tree.root, tree.tree_nodes])
+            if cache:
+                np.savez(cache, nodes=nodes, root=tree.root, depth=depth, tree_nodes=tree.tree_nodes,
+                         build_s=build_s)
     if world > 1:
-        dist.broadcast(meta, 0)
+        coll(dist.broadcast, meta, 0)
     n, root, tree_nodes = (int(v) for v in meta.tolist())
     buf = torch.empty(n * 8, dtype=torch.int32, device=dev)
     if rank == 0:
         buf.copy_(torch.from_numpy(nodes.reshape(-1).view(np.int32)))
     if world > 1:
-        dist.broadcast(buf, 0)
+        coll(dist.broadcast, buf, 0)
     if rank != 0:
         nodes = buf.cpu().numpy().view(np.uint32).reshape(n, 8)
     return nodes, root, tree_nodes, build_s
@@ -153,13 +178,21 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    backend = os.environ.get("OCH_DIST_BACKEND", "nccl")
+    if backend == "gloo":
+        # Rehearsal of the N > 1 path on a box with fewer GPUs than ranks:
+        # ranks share devices round-robin and collectives go through the host.
+        local %= max(1, torch.cuda.device_count())
     if world != a.gpus:
         log(f"warning: --gpus {a.gpus} but WORLD_SIZE {world}; using WORLD_SIZE")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", device_id=dev)
+        if backend == "gloo":
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=dev)
 
     import octree_ray_tracing_amd as ort
     from octree_ray_tracing_amd.frame import ShardedFrame, slice_row_map
@@ -263,7 +296,7 @@ def main():
     kms = np.array([x.elapsed_time(y) for x, y in ev])
     t_max = torch.tensor([elapsed], dtype=torch.float64, device=dev)
     if world > 1:
-        dist.all_reduce(t_max, op=dist.ReduceOp.MAX)
+        coll(dist.all_reduce, t_max, op=dist.ReduceOp.MAX)
     elapsed = float(t_max.item())
 
     # Config 5 (BASELINE configs[4]): the same frames with one mirrored
@@ -288,7 +321,7 @@ def main():
             torch.cuda.synchronize()
             el = torch.tensor([time.perf_counter() - tb], dtype=torch.float64, device=dev)
             if world > 1:
-                dist.all_reduce(el, op=dist.ReduceOp.MAX)
+                coll(dist.all_reduce, el, op=dist.ReduceOp.MAX)
             return float(el.item()), float(np.mean([x.elapsed_time(y) for x, y in bev]))
         b_el, b_kms = timed_steps(a.steps)
         pool.set_option("bounce_compact", 0)
@@ -297,7 +330,7 @@ def main():
         pool.set_stream(stream)
         hits = torch.tensor([hits_total], dtype=torch.int64, device=dev)
         if world > 1:
-            dist.all_reduce(hits)
+            coll(dist.all_reduce, hits)
         secondary = int(hits.item())
         primary = W * H * len(cams)
         bounce = {"workload": "configs[4]: depth-12, primary + 1-bounce secondary rays (divergent), "

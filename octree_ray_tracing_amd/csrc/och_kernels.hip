@@ -27,6 +27,7 @@ namespace och {
 namespace {
 
 constexpr uint32_t kX86DefaultNaN = 0xFFC00000u;
+
 constexpr int kMaxViews = OCH_MAX_VIEWS;
 
 __device__ __forceinline__ uint32_t fbits(float f) { return __float_as_uint(f); }
@@ -55,20 +56,34 @@ struct Hit {
 struct Ray {
     float c[3], b[3];     // coefficient (RCPPS of -|d|) and bias (-c * o') per axis
     uint32_t p[3];        // position bits in the reflected frame
-    uint32_t inv;         // direction-sign mask (1 = positive)
+    uint32_t inv;         // direction-sign mask (1 = positive) | 24: idx ^ inv = 24 + child index,
+                          // the bit of that child in a packed slot word
     uint32_t idx;         // child index bits at the current level
     uint32_t dim;         // mantissa bit of the current child size
     uint32_t cur;         // the current node: packed slot word (id | child mask << 24), or raw index
     uint32_t *sp;         // this lane's LDS stack slot for the current level (parents below it)
     uint32_t t_min;       // bits of the entry t of the current cell
     uint32_t min_axis;    // 1, 2, 4 (last STEP axis) or 8 (none yet)
-    uint32_t voxel;       // the hit voxel id (valid once level > depth)
-    uint32_t child;       // slot word loaded by the last PUSH (pending)
+    uint32_t child;       // slot word loaded by the last PUSH (pending); the voxel id after a hit
     int level;            // 1..depth while walking; 0 after a miss, depth + 1 after a hit
-    bool stepping;        // next iteration starts at STEP (after a failed PUSH or a POP)
-    bool pending;         // a PUSH found its child; the slot word is in flight
+    uint32_t mode;        // kAtPush (or finished), kStepping, kPending
     uint32_t push;
 };
+
+// Ray phase: due to PUSH (or finished), due to STEP (after a failed PUSH or a
+// POP), or a PUSH found its child and the slot word is in flight.
+constexpr uint32_t kAtPush = 0, kStepping = 1, kPending = 2;
+
+__device__ __forceinline__ void set_mode(Ray &r, uint32_t m) { r.mode = m; }
+
+// The phase is one VGPR value, opaque to the compiler at each test, so a
+// phase test is one compare; as two bools the compiler carried lane masks
+// through every join of the loop body (1.5x the SALU instructions, measured).
+__device__ __forceinline__ bool in_mode(Ray &r, uint32_t m)
+{
+    asm volatile("" : "+v"(r.mode));
+    return r.mode == m;
+}
 
 constexpr uint32_t kIdMask = 0x00FFFFFFu;
 
@@ -80,12 +95,12 @@ template <bool kPacked, bool kCount>
 __device__ __forceinline__ void ray_push(Ray &r, const DevPool &P)
 {
     if (kCount) ++r.push;
-    const uint32_t c = r.idx ^ r.inv;
-    if (!kPacked || ((r.cur >> 24 >> c) & 1u)) {
-        r.child = P.nodes[8u * (kPacked ? (r.cur & kIdMask) : r.cur) + c];
-        r.pending = true;
+    const uint32_t c24 = r.idx ^ r.inv;                                     // 24 + child index
+    if (!kPacked || __builtin_amdgcn_ubfe(r.cur, c24, 1u)) {
+        r.child = (P.nodes - 24)[8u * (kPacked ? (r.cur & kIdMask) : r.cur) + c24];
+        set_mode(r, kPending);
     } else {
-        r.stepping = true;
+        set_mode(r, kStepping);
     }
 }
 
@@ -94,7 +109,7 @@ __device__ __forceinline__ void ray_push(Ray &r, const DevPool &P)
 template <bool kPacked, bool kCount>
 __device__ __forceinline__ void ray_init(Ray &r, const DevPool &P, const float *o, const float *d, uint32_t *stack)
 {
-    r.inv = 0;
+    r.inv = 24;
     r.idx = 0;
 #pragma unroll
     for (int a = 0; a < 3; ++a) {
@@ -124,9 +139,7 @@ __device__ __forceinline__ void ray_init(Ray &r, const DevPool &P, const float *
     r.t_min = 0;                                                            // +0.0F
     r.level = 1;
     r.min_axis = 8;
-    r.voxel = 0;
-    r.stepping = false;
-    r.pending = false;
+    set_mode(r, kAtPush);
     r.child = 0;
     r.push = 0;
     ray_push<kPacked, true>(r, P);
@@ -167,7 +180,7 @@ __device__ __forceinline__ void ray_phase_step(Ray &r, uint32_t stride)
         r.p[1] ^= sy ? r.dim : 0u;
         r.p[2] ^= sz ? r.dim : 0u;
         r.idx ^= axis;
-        r.stepping = false;
+        set_mode(r, kAtPush);
         return;
     }
     if (--r.level == 0) return;                                         // MISS :423-431
@@ -184,20 +197,18 @@ __device__ __forceinline__ void ray_phase_step(Ray &r, uint32_t stride)
 template <bool kPacked>
 __device__ __forceinline__ void ray_phase_descend(Ray &r, const DevPool &P, uint32_t stride)
 {
-    r.pending = false;
+    set_mode(r, kAtPush);
     const uint32_t child = r.child;
     if (!kPacked && child == 0) {                                           // raw layout: empty child
-        r.stepping = true;
+        set_mode(r, kStepping);
         return;
     }
-    if (r.level == P.depth) {                                               // HIT :346-355
-        r.voxel = child;
-        r.level = P.depth + 1;
-        return;
-    }
+    // HIT :346-355 when the PUSH was at the leaf level: level becomes
+    // depth + 1 (finished) exactly as a descent increments it, and the voxel
+    // id stays in r.child (no later load overwrites a finished lane's).
+    if (++r.level > P.depth) return;
     *r.sp = r.cur;                                                          // :357
     r.sp += stride;
-    ++r.level;
     r.cur = child;
     r.dim >>= 1;                                                            // :361
     const float tm = ffrom(r.t_min);
@@ -221,10 +232,10 @@ __device__ __forceinline__ bool ray_active(const Ray &r, const DevPool &P)
 template <bool kPacked, bool kCount>
 __device__ __forceinline__ void ray_iterate(Ray &r, const DevPool &P, uint32_t stride)
 {
-    if (!kPacked && r.pending) ray_phase_descend<kPacked>(r, P, stride);
-    if (r.stepping) ray_phase_step<kPacked>(r, stride);
-    if (kPacked && r.pending) ray_phase_descend<kPacked>(r, P, stride);
-    if (!r.stepping && ray_active(r, P)) ray_push<kPacked, kCount>(r, P);   // PUSH :342-344
+    if (!kPacked && in_mode(r, kPending)) ray_phase_descend<kPacked>(r, P, stride);
+    if (in_mode(r, kStepping)) ray_phase_step<kPacked>(r, stride);
+    if (kPacked && in_mode(r, kPending)) ray_phase_descend<kPacked>(r, P, stride);
+    if (in_mode(r, kAtPush) && ray_active(r, P)) ray_push<kPacked, kCount>(r, P);   // PUSH :342-344
 }
 
 // The hit record of a finished ray (:346-355 hit, :423-431 miss).
@@ -236,8 +247,8 @@ __device__ __forceinline__ Hit ray_result(const Ray &r, const DevPool &P)
         h.voxel = 0;
         h.t = P.miss_bits;
     } else {
-        h.dir = (int32_t)((r.min_axis >> 1) + 3u * ((r.inv & r.min_axis) == 0));
-        h.voxel = r.voxel;
+        h.dir = (int32_t)((r.min_axis >> 1) + 3u * ((r.inv & r.min_axis & 7u) == 0));
+        h.voxel = r.child;
         h.t = r.t_min;
     }
     h.push = r.push;
@@ -281,6 +292,10 @@ struct ArraySource {
         out = i;
         return true;
     }
+    __device__ __forceinline__ bool get_wave(uint32_t wave_base, uint32_t lane, float *o, float *d, uint32_t &out) const
+    {
+        return get(wave_base + lane, o, d, out);
+    }
 };
 
 // tree_camera::update_position per pixel (ORT/test_och_h_octree.cpp:119-136):
@@ -319,11 +334,11 @@ struct CameraSource {
     int32_t n_views, row_chunk, shard, n_shards, slice_rows, width, height, order;
     uint32_t tiles_x, supertiles_x, per_view, slice_pixels;
     __host__ __device__ __forceinline__ uint32_t count() const { return per_view * (uint32_t)n_views; }
-    __device__ __forceinline__ bool get(uint32_t i, float *o, float *d, uint32_t &out) const
+    // Tile of ray i (tile-granular index math, identical in get and get_wave).
+    __device__ __forceinline__ void tile_of(uint32_t i, uint32_t &view, uint32_t &tx, uint32_t &ty) const
     {
-        const uint32_t view = i / per_view, j = i - view * per_view;
-        const uint32_t tile = j >> 6, lane = j & 63u;
-        uint32_t tx, ty;
+        view = i / per_view;
+        const uint32_t tile = (i - view * per_view) >> 6;
         if (order == 1) {
             const uint32_t st = tile >> 6, sub = tile & 63u;
             tx = (st % supertiles_x) * 8u + (sub & 7u);
@@ -332,17 +347,50 @@ struct CameraSource {
             tx = tile % tiles_x;
             ty = tile / tiles_x;
         }
-        const int col = (int)(tx * kTileW + lane % kTileW);
-        const int srow = (int)(ty * kTileH + lane / kTileW);
-        if (col >= width || srow >= slice_rows) return false;
-        const int chunk = srow / row_chunk, within = srow - chunk * row_chunk;
-        const int row = (chunk * n_shards + shard) * row_chunk + within;
+    }
+    __device__ __forceinline__ bool finish(uint32_t view, int col, int srow, int row, float *o, float *d,
+                                           uint32_t &out) const
+    {
         if (row >= height) return false;
         const och_camera &C = cam[view];
         o[0] = C.pos[0]; o[1] = C.pos[1]; o[2] = C.pos[2];
         camera_ray(C, col, row, d);
         out = view * slice_pixels + (uint32_t)srow * (uint32_t)width + (uint32_t)col;
         return true;
+    }
+    // Any ray index (the persistent schedule hands out arbitrary indices).
+    __device__ __forceinline__ bool get(uint32_t i, float *o, float *d, uint32_t &out) const
+    {
+        uint32_t view, tx, ty;
+        tile_of(i, view, tx, ty);
+        const uint32_t lane = i & 63u;
+        const int col = (int)(tx * kTileW + lane % kTileW);
+        const int srow = (int)(ty * kTileH + lane / kTileW);
+        if (col >= width || srow >= slice_rows) return false;
+        const int chunk = srow / row_chunk, within = srow - chunk * row_chunk;
+        return finish(view, col, srow, (chunk * n_shards + shard) * row_chunk + within, o, d, out);
+    }
+    // One wave's tile: wave_base (a multiple of 64, wave-uniform) moves the
+    // tile arithmetic, divisions included, to the scalar unit.
+    __device__ __forceinline__ bool get_wave(uint32_t wave_base, uint32_t lane, float *o, float *d, uint32_t &out) const
+    {
+        uint32_t view, tx, ty;
+        tile_of(__builtin_amdgcn_readfirstlane(wave_base), view, tx, ty);
+        view = __builtin_amdgcn_readfirstlane(view);
+        tx = __builtin_amdgcn_readfirstlane(tx);
+        ty = __builtin_amdgcn_readfirstlane(ty);
+        const int col = (int)(tx * kTileW + lane % kTileW);
+        const int srow0 = (int)(ty * kTileH), srow = srow0 + (int)(lane / kTileW);
+        if (col >= width || srow >= slice_rows) return false;
+        int row;
+        if (row_chunk % (int)kTileH == 0) {                // the tile lies inside one row chunk
+            const int chunk = __builtin_amdgcn_readfirstlane(srow0 / row_chunk);
+            row = (chunk * n_shards + shard) * row_chunk + (srow - chunk * row_chunk);
+        } else {
+            const int chunk = srow / row_chunk;
+            row = (chunk * n_shards + shard) * row_chunk + (srow - chunk * row_chunk);
+        }
+        return finish(view, col, srow, row, o, d, out);
     }
 };
 
@@ -473,10 +521,11 @@ __global__ void k_trace_grid(DevPool P, Src S, Sink K, uint32_t xcd_group, uint6
 {
     extern __shared__ uint32_t lds_stack[];
     const uint64_t t0 = stamps ? realtime() : 0;
-    const uint32_t i = xcd_block(blockIdx.x, gridDim.x, xcd_group) * blockDim.x + threadIdx.x;
+    const uint32_t wave_base = xcd_block(blockIdx.x, gridDim.x, xcd_group) * blockDim.x + (threadIdx.x & ~63u);
+    const uint32_t lane = threadIdx.x & 63u;
     float o[3], d[3];
     uint32_t out;
-    if (i < S.count() && S.get(i, o, d, out)) {
+    if (wave_base + lane < S.count() && S.get_wave(wave_base, lane, o, d, out)) {
         Ray r;
         ray_init<kPacked, kCount>(r, P, o, d, lds_stack + threadIdx.x);
         do {
@@ -503,11 +552,11 @@ __global__ void k_trace_bounce(DevPool P, Src S, Sink K, uint32_t stack_words, i
     uint32_t *stack = lds_stack + threadIdx.x;
     uint32_t *queue = lds_stack + stack_words;
     const uint32_t nb = blockDim.x;
-    const uint32_t i = blockIdx.x * nb + threadIdx.x;
+    const uint32_t wave_base = blockIdx.x * nb + (threadIdx.x & ~63u);
     float o[3], d[3], o2[3], d2[3];
     uint32_t out = 0, payload = 0;
     bool want = false;
-    if (i < S.count() && S.get(i, o, d, out)) {
+    if (wave_base + (threadIdx.x & 63u) < S.count() && S.get_wave(wave_base, threadIdx.x & 63u, o, d, out)) {
         Ray r;
         ray_init<kPacked, kCount>(r, P, o, d, stack);
         do {
@@ -649,7 +698,10 @@ hipError_t launch_as(const DevPool &p, const Src &s, const Sink &k, uint32_t n, 
 {
     if (n == 0) return hipSuccess;
     const int block = sc.block;
-    const size_t lds = stack_bytes(p.depth, block);
+#ifndef OCH_LDS_MIN
+#define OCH_LDS_MIN 0     // occupancy experiments: pad each block's LDS to this many bytes
+#endif
+    const size_t lds = stack_bytes(p.depth, block) > OCH_LDS_MIN ? stack_bytes(p.depth, block) : OCH_LDS_MIN;
     if (sc.persistent) {
         hipError_t e = hipMemsetAsync(sc.counter, 0, sizeof(uint32_t), stream);
         if (e != hipSuccess) return e;

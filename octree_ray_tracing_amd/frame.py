@@ -76,7 +76,12 @@ class ShardedFrame:
 
         src = self.slice
         if self.world > 1:
-            dist.all_gather_into_tensor(self.gathered, self.slice, group=self.group)
+            if dist.get_backend(self.group) == "gloo":      # host-staged (CPU tests, rehearsal runs)
+                host = self.gathered.new_empty(self.gathered.shape, device="cpu")
+                dist.all_gather(list(host.unbind(0)), self.slice.cpu(), group=self.group)
+                self.gathered.copy_(host)
+            else:
+                dist.all_gather_into_tensor(self.gathered, self.slice, group=self.group)
             src = self.gathered
         self.pool.unshard_dev(src, self.frames, self.width, self.height, self.row_chunk, self.world, self.n_views)
         return self.frames

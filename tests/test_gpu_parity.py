@@ -150,6 +150,15 @@ def test_random_and_edge_rays_d10(ort, O, gpu_device):
     # unnormalised and tiny / huge directions
     d2 = d[:50000] * rng.choice(np.array([1e-20, 1e-5, 3.0, 1e20], np.float32), (50000, 1))
     assert_same(gpu_trace_dev(pool, o[:50000], d2), O.trace_batch(ref_pool, O.Rcp(None), o[:50000], d2, want_push=True))
+    # origins on and just past the cube's faces (a bounce origin can sit half a
+    # voxel outside): setup's root idx (p == 1.5, :324) then disagrees with the
+    # POP's bit formula (:440-444), which the kernel must reproduce
+    oo = rng.uniform(0.9, 2.1, (50000, 3)).astype(np.float32)
+    oo[:10000, rng.integers(0, 3)] = np.float32(2.0000768)
+    for layout in (1, 0):
+        pool.set_option("layout", layout)
+        assert_same(gpu_trace_dev(pool, oo, d[:50000]),
+                    O.trace_batch(ref_pool, O.Rcp(None), oo, d[:50000], nthreads=16, want_push=True))
     pool.set_option("layout", 0)
     assert_same(gpu_trace_dev(pool, eo, ed), O.trace_batch(ref_pool, O.Rcp(None), eo, ed, want_push=True))
     pool.close()

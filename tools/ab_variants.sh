@@ -3,6 +3,7 @@
 # bench per variant, interleaved twice.  Usage: bash tools/ab_variants.sh NAME...
 set -o pipefail
 mkdir -p gpurun_out
+export OCH_TREE_CACHE=/tmp/och_tree_d12.npz
 for round in 1 2; do
   for v in "$@"; do
     lib=build_variants/liboch_gpu_$v.so

@@ -1,0 +1,232 @@
+/* sched_sim.c -- lockstep model of one 64-lane wavefront running the render
+ * kernel's traversal loop (och_kernels.hip ray_iterate, packed layout), to
+ * price schedule changes before writing them in HIP.
+ *
+ * Design tool only (not product, not a checker): it walks the DAG with the
+ * host's own RCPPS, runs 64 rays of an 8x8 tile in lockstep through the
+ * kernel's phases, and charges each phase's VALU instruction count (taken
+ * from the gfx950 ISA of the current kernel, see the table below) whenever
+ * at least one lane of the wave executes it.  Output: VALU instructions per
+ * wave, iterations per wave and per-phase lane utilisation, per schedule.
+ *
+ * Build: gcc -O2 -msse2 -o /tmp/sched_sim tools/sched_sim.c -lm
+ * Input: raw uint32 nodes[n][8] (1-based h_octree pool) from tools/sched_sim.py. */
+#include <immintrin.h>
+#include <math.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+static inline uint32_t f2u(float f) { uint32_t u; memcpy(&u, &f, 4); return u; }
+static inline float u2f(uint32_t u) { float f; memcpy(&f, &u, 4); return f; }
+
+typedef struct {
+    float c[3], b[3];
+    uint32_t p[3], inv, idx, dim, cur, t_min, axis, child;
+    uint32_t stack[32];
+    int sp, level, stepping, pending, done;
+    int iters, push, step, pop;
+} Ray;
+
+static const uint32_t *N;
+static int DEPTH;
+
+static void ray_setup(Ray *r, const float *o, const float *d)
+{
+    memset(r, 0, sizeof *r);
+    for (int a = 0; a < 3; ++a) {
+        const int pos = 0.0F < d[a];
+        r->inv |= pos << a;
+        const float refl = fabsf((pos ? 3.0F : 0.0F) - o[a]);
+        const float dn = u2f(f2u(d[a]) | 0x80000000u);
+        float c = _mm_cvtss_f32(_mm_rcp_ss(_mm_set_ss(dn)));
+        r->c[a] = c;
+        r->b[a] = u2f(f2u(c * refl) ^ 0x80000000u);
+        if ((f2u(c) & 0x7FFFFFFFu) == 0x7F800000u) { r->c[a] = 0.0F; r->b[a] = u2f(0xFFC00000u); }
+        r->p[a] = f2u(refl) & 0x3FC00000u;
+        r->idx |= (r->p[a] == 0x3FC00000u) << a;
+    }
+    r->dim = 1u << 22;
+    r->cur = 1;   /* root id (1-based) */
+    r->level = 1;
+    r->axis = 8;
+}
+
+/* the PUSH test: child of cur at (idx ^ inv) */
+static void push(Ray *r)
+{
+    ++r->push;
+    const uint32_t ch = N[(size_t)(r->cur - 1) * 8 + ((r->idx ^ r->inv) & 7)];
+    if (ch) { r->child = ch; r->pending = 1; }
+    else r->stepping = 1;
+}
+
+static int active(const Ray *r) { return r->level >= 1 && r->level <= DEPTH; }
+
+/* ISA VALU counts per block of the current packed render loop (gfx950). */
+enum { C_STEP = 10, C_ADV = 7, C_POPPRE = 3, C_POP = 14, C_DESCPRE = 3, C_DESC = 22, C_PUSHPRE = 2,
+       C_PUSHTEST = 4, C_PUSHLOAD = 4, C_LOOP = 1 };
+
+typedef struct { double valu, iters, waves, lane_step, lane_desc, lane_push, exec_step, exec_desc, exec_push, rays_it, exec_adv, exec_popper, exec_pop, exec_descbody, exec_load; } Stats;
+
+/* STEP of one lane (+ advance or POP).  Returns 1 advance, 2 POP, 3 MISS. */
+static int step_one(Ray *r)
+{
+    ++r->step;
+    uint32_t t[3];
+    for (int a = 0; a < 3; ++a) t[a] = f2u(fmaf(u2f(r->p[a]), r->c[a], r->b[a]));
+    uint32_t tm = t[0] < t[1] ? t[0] : t[1]; tm = tm < t[2] ? tm : t[2];
+    const int ax = t[0] == tm ? 0 : (t[1] == tm ? 1 : 2);
+    r->axis = 1u << ax; r->t_min = tm;
+    if (r->idx & r->axis) { r->p[ax] ^= r->dim; r->idx ^= r->axis; r->stepping = 0; return 1; }
+    ++r->pop;
+    if (--r->level == 0) return 3;
+    r->cur = r->stack[--r->sp];
+    for (int a = 0; a < 3; ++a) r->p[a] &= ~r->dim;
+    r->dim <<= 1;
+    r->idx = 0;
+    for (int a = 0; a < 3; ++a) r->idx |= ((r->p[a] & r->dim) != 0) << a;
+    return 2;
+}
+
+static int SCHED = 0;
+
+/* schedule 0: the current kernel (step, descend, push; each phase skipped when no lane needs it) */
+static void wave_sched0(Ray *R, int n, Stats *S)
+{
+    for (int i = 0; i < n; ++i) push(&R[i]);
+    for (;;) {
+        int any = 0;
+        for (int i = 0; i < n; ++i) any |= active(&R[i]);
+        if (!any) break;
+        S->iters += 1;
+        int ns = 0, nadv = 0, npopper = 0, npop = 0, nd = 0, ndesc = 0, np = 0, nload = 0;
+        for (int i = 0; i < n; ++i) {
+            Ray *r = &R[i];
+            if (!active(r)) continue;
+            ++r->iters;
+            if (r->stepping) {
+                ++ns; ++r->step;
+                uint32_t t[3];
+                for (int a = 0; a < 3; ++a) t[a] = f2u(fmaf(u2f(r->p[a]), r->c[a], r->b[a]));
+                uint32_t tm = t[0] < t[1] ? t[0] : t[1]; tm = tm < t[2] ? tm : t[2];
+                const int ax = t[0] == tm ? 0 : (t[1] == tm ? 1 : 2);
+                r->axis = 1u << ax; r->t_min = tm;
+                if (r->idx & r->axis) { ++nadv; r->p[ax] ^= r->dim; r->idx ^= r->axis; r->stepping = 0; }
+                else {
+                    ++npopper; ++r->pop;
+                    if (--r->level == 0) continue;
+                    ++npop;
+                    r->cur = r->stack[--r->sp];
+                    for (int a = 0; a < 3; ++a) r->p[a] &= ~r->dim;
+                    r->dim <<= 1;
+                    r->idx = 0;
+                    for (int a = 0; a < 3; ++a) r->idx |= ((r->p[a] & r->dim) != 0) << a;
+                }
+            }
+        }
+        for (int i = 0; i < n; ++i) {
+            Ray *r = &R[i];
+            if (!r->pending) continue;
+            r->pending = 0; ++nd;
+            if (r->level == DEPTH) { r->level = DEPTH + 1; continue; }
+            ++ndesc;
+            r->stack[r->sp++] = r->cur; ++r->level; r->cur = r->child; r->dim >>= 1;
+            uint32_t ni = 0;
+            for (int a = 0; a < 3; ++a) {
+                const uint32_t mid = r->p[a] | r->dim;
+                const int up = fmaf(u2f(mid), r->c[a], r->b[a]) >= u2f(r->t_min);
+                ni |= up << a; if (up) r->p[a] = mid;
+            }
+            r->idx = ni;
+        }
+        int fresh[64] = {0};
+        for (int i = 0; i < n; ++i) {
+            Ray *r = &R[i];
+            if (r->stepping || !active(r)) continue;
+            ++np; push(r); nload += r->pending;
+            fresh[i] = r->stepping;
+        }
+        if (SCHED == 1) {     /* second STEP + PUSH test in the same iteration for lanes whose PUSH failed */
+            int n2 = 0, nadv2 = 0, npop2 = 0, np2 = 0, nload2 = 0;
+            for (int i = 0; i < n; ++i) {
+                Ray *r = &R[i];
+                if (!fresh[i] || !active(r)) continue;
+                ++n2;
+                const int k = step_one(r);
+                nadv2 += k == 1; npop2 += k == 2;
+                if (k == 1) { ++np2; push(r); nload2 += r->pending; }
+            }
+            if (n2) S->valu += C_STEP + C_POPPRE;
+            if (nadv2) S->valu += C_ADV;
+            if (npop2) S->valu += C_POP;
+            if (np2) S->valu += C_PUSHTEST;
+            if (nload2) S->valu += C_PUSHLOAD;
+        }
+        S->valu += C_LOOP + C_PUSHPRE;
+        if (ns) { S->valu += C_STEP; S->exec_step += 1; S->lane_step += ns; }
+        if (nadv) { S->valu += C_ADV; S->exec_adv += 1; }
+        if (npopper) { S->valu += C_POPPRE; S->exec_popper += 1; }
+        if (npop) { S->valu += C_POP; S->exec_pop += 1; }
+        if (nd) { S->valu += C_DESCPRE; S->exec_desc += 1; S->lane_desc += nd; }
+        if (ndesc) { S->valu += C_DESC; S->exec_descbody += 1; }
+        if (np) { S->valu += C_PUSHTEST; S->exec_push += 1; S->lane_push += np; }
+        if (nload) { S->valu += C_PUSHLOAD; S->exec_load += 1; }
+    }
+    for (int i = 0; i < n; ++i) S->rays_it += R[i].iters;
+    S->waves += 1;
+}
+
+static void camera(float yaw, float pitch, int W, int H, int col, int row, float *d)
+{
+    /* tree_camera::update_position (ORT/test_och_h_octree.cpp:87-138), float math */
+    const float aspect = (float)W / (float)H, fov = 1.25F;
+    const float f = 1.0F / tanf(fov / 2);
+    const float sb = sinf(yaw), cb = cosf(yaw), sc = sinf(pitch), cc = cosf(pitch);
+    const float m[9] = {cb, sb * sc, sb * cc, 0, cc, -sc, -sb, cb * sc, cb * cc};
+    const float u = aspect * ((2.0F / W) * col - 1.0F), v = (2.0F / H) * row - 1.0F;
+    const float ru = u * m[0] + v * m[1] + f * m[2];
+    const float rv = u * m[3] + v * m[4] + f * m[5];
+    const float rw = u * m[6] + v * m[7] + f * m[8];
+    const float rm = 1.0F / sqrtf(ru * ru + rv * rv + rw * rw);
+    d[0] = rw * rm; d[1] = ru * rm; d[2] = -rv * rm;
+}
+
+int main(int argc, char **argv)
+{
+    if (argc < 4) { fprintf(stderr, "usage: sched_sim nodes.bin depth pitch [tile_stride]\n"); return 2; }
+    FILE *fp = fopen(argv[1], "rb");
+    fseek(fp, 0, SEEK_END); long sz = ftell(fp); fseek(fp, 0, SEEK_SET);
+    uint32_t *buf = malloc(sz);
+    if (fread(buf, 1, sz, fp) != (size_t)sz) return 1;
+    fclose(fp);
+    N = buf; DEPTH = atoi(argv[2]);
+    const float pitch = (float)atof(argv[3]);
+    const int stride = argc > 4 ? atoi(argv[4]) : 1;
+    SCHED = argc > 5 ? atoi(argv[5]) : 0;
+    const int W = 1920, H = 1080;
+    const float o[3] = {1.5F, 1.5F, 1.5F};
+    Stats S = {0};
+    Ray R[64];
+    int tile = 0;
+    for (int ty = 0; ty < H / 8; ++ty)
+        for (int tx = 0; tx < W / 8; ++tx, ++tile) {
+            if (tile % stride) continue;
+            for (int l = 0; l < 64; ++l) {
+                float d[3];
+                camera(0.3F, pitch, W, H, tx * 8 + l % 8, ty * 8 + l / 8, d);
+                ray_setup(&R[l], o, d);
+            }
+            wave_sched0(R, 64, &S);
+        }
+    printf("{\"waves\": %.0f, \"valu_per_wave\": %.1f, \"iters_per_wave\": %.2f, \"ray_iters\": %.2f, "
+           "\"lane_util_iter\": %.3f, \"step_util\": %.3f, \"desc_util\": %.3f, \"push_util\": %.3f, "
+           "\"step_exec_frac\": %.3f, \"desc_exec_frac\": %.3f, \"adv_frac\": %.3f, \"pop_frac\": %.3f, "
+           "\"load_frac\": %.3f}\n",
+           S.waves, S.valu / S.waves, S.iters / S.waves, S.rays_it / S.waves / 64, S.rays_it / S.iters / 64,
+           S.lane_step / S.exec_step / 64, S.lane_desc / S.exec_desc / 64, S.lane_push / S.exec_push / 64,
+           S.exec_step / S.iters, S.exec_desc / S.iters, S.exec_adv / S.iters, S.exec_popper / S.iters,
+           S.exec_load / S.iters);
+    return 0;
+}
