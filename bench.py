@@ -167,6 +167,8 @@ def main():
     ap.add_argument("--opt", action="append", default=[], metavar="NAME=VALUE",
                     help="pool launch option (och_gpu_set_option), e.g. tile_order=1")
     ap.add_argument("--no-bounce", action="store_true", help="skip the config-5 (secondary rays) measurement")
+    ap.add_argument("--rgba-frames", action="store_true",
+                    help="render and exchange RGBA8 slices instead of 1-byte indexed-colour codes")
     ap.add_argument("--inflight", type=int, default=3,
                     help="frames in flight: steps alternate over this many HIP streams, so one step's "
                          "slowest rays overlap the next step's bulk (1 = serialised)")
@@ -206,13 +208,16 @@ def main():
         pool.set_option(k, int(v))
     stream = torch.cuda.current_stream()
     pool.set_stream(stream)
+    # Frames travel between ranks as 1-byte colour codes and are shaded after
+    # the gather (same RGBA8 frames, a quarter of the bytes on xGMI).
+    indexed = not a.rgba_frames and ort.VoxelData().get_colours().size // 6 <= pool.CODE_MAX_VOXELS
     cams = [ort.camera(ORIGIN, YAW, p, FOV, W, H) for p in PITCHES]
     # One frame buffer set and one HIP stream per frame in flight.
     streams = [stream] + [torch.cuda.Stream(device=dev) for _ in range(max(1, a.inflight) - 1)]
     sfs = []
     for s_ in streams:
         with torch.cuda.stream(s_):
-            sfs.append(ShardedFrame(pool, W, H, a.row_chunk, n_views=len(PITCHES)))
+            sfs.append(ShardedFrame(pool, W, H, a.row_chunk, n_views=len(PITCHES), indexed=indexed))
     pool.set_stream(stream)
     sf = sfs[0]
 
@@ -346,9 +351,12 @@ def main():
     total_rays = W * H * frames
     value = total_rays / elapsed / 1e6
     # Algorithmic bytes of the dominant kernel (the render launch, both views)
-    # on this rank: 4 B pixel store per ray + 4 B per child-slot read (PUSH,
-    # SURVEY 8d) + 4 B palette read per hit ray.
-    bytes_per_launch = 4 * rays_rank + 4 * push_total + 4 * hits_total
+    # on this rank: the pixel store per ray (1 B code, or 4 B RGBA8 + a 4 B
+    # palette read per hit ray) + 4 B per child-slot read (PUSH).
+    if indexed:
+        bytes_per_launch = 1 * rays_rank + 4 * push_total
+    else:
+        bytes_per_launch = 4 * rays_rank + 4 * push_total + 4 * hits_total
     k_avg_ms = float(kms.mean())
     achieved = bytes_per_launch / (k_avg_ms * 1e-3) / 1e9
     pmc = load_pmc("k_render", f"d{a.depth}_{W}x{H}_n{world}")
@@ -379,11 +387,13 @@ def main():
                        "dag_nodes": int(nodes.shape[0]), "tree_nodes": tree_nodes,
                        "pool_mb": round(nodes.nbytes / 2**20, 1), "build_s": round(build_s, 2),
                        "parallelism": f"rows{world}",
+                       "frames": "indexed-colour codes, shaded after the exchange" if indexed else "rgba8",
                        "options": {k: pool.get_option(k) for k in pool.OPTIONS}},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 5),
                          "traffic": None if pmc is None else pmc.get("hbm_bytes_per_launch"),
-                         "kernel": "k_trace_grid<CameraSource,FrameSink> (2 views per launch)", "kernel_ms": round(k_avg_ms, 4),
+                         "kernel": f"k_trace_grid<CameraSource,{'CodeSink' if indexed else 'FrameSink'}> (2 views per launch)",
+                         "kernel_ms": round(k_avg_ms, 4),
                          "kernel_ms_idle_gpu": round(latency_ms, 4), "frames_in_flight": len(streams),
                          "bytes_per_launch": int(bytes_per_launch),
                          "push_per_ray": round(push_total / rays_rank, 3),

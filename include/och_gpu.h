@@ -55,6 +55,18 @@ typedef enum och_direction {
     OCH_EXIT = 6, OCH_INSIDE = 7, OCH_ERROR = 8
 } och_direction;
 
+/* Indexed-colour frame codes (1 byte per pixel, the multi-GPU exchange format
+ * of och_gpu_render_codes_views_dev): 6 * (voxel - 1) + direction for a hit
+ * face with a palette entry, the three fixed colours of trace_pixel
+ * (ORT/test_och_h_octree.cpp:76-84, magenta for an id without a palette
+ * entry), | OCH_CODE_BLOCKED when a config-5 secondary ray was blocked.
+ * Needs a palette of at most OCH_CODE_MAX_VOXELS voxel ids. */
+#define OCH_CODE_MAGENTA 125
+#define OCH_CODE_INSIDE 126
+#define OCH_CODE_SKY 127
+#define OCH_CODE_BLOCKED 128
+#define OCH_CODE_MAX_VOXELS 20
+
 typedef struct och_gpu_pool och_gpu_pool;
 
 /* Camera uniforms of tree_camera::update_position (ORT/test_och_h_octree.cpp:87-115),
@@ -220,6 +232,18 @@ OCH_API int och_gpu_unshard_dev(och_gpu_pool *pool, const uint32_t *gathered, ui
  * och_gpu_render_views_dev output, all-gathered), frames = [n_views][H][W]. */
 OCH_API int och_gpu_unshard_views_dev(och_gpu_pool *pool, const uint32_t *gathered, uint32_t *frames,
                                       int width, int height, int row_chunk, int n_shards, int n_views);
+
+/* Indexed-colour form of och_gpu_render_views_dev / _bounce_views_dev (bounce
+ * = 0 / 1): the same pixels as OCH_CODE_* bytes, a quarter of the RGBA8 bytes
+ * to all-gather between ranks.  OCH_E_INVALID when the pool's palette has
+ * more than OCH_CODE_MAX_VOXELS ids. */
+OCH_API int och_gpu_render_codes_views_dev(och_gpu_pool *pool, const och_camera *cams, int n_views,
+                                           uint8_t *code_slices, int row_chunk, int shard, int n_shards,
+                                           int bounce);
+/* och_gpu_unshard_views_dev for gathered code slices, shading each code to
+ * the RGBA8 word the RGBA render would have written (bit-identical frames). */
+OCH_API int och_gpu_shade_unshard_views_dev(och_gpu_pool *pool, const uint8_t *gathered, uint32_t *frames,
+                                            int width, int height, int row_chunk, int n_shards, int n_views);
 
 /* ------------------------------------------------------------ builder */
 /* The demo terrain (ORT/test_och_h_octree.cpp:561-787) built in parallel

@@ -85,6 +85,8 @@ PROTOTYPES = {
     "och_gpu_render_bounce_views_dev": (C.c_int, [_P, _P, C.c_int, _P, C.c_int, C.c_int, C.c_int]),
     "och_gpu_unshard_dev": (C.c_int, [_P, _P, _P, C.c_int, C.c_int, C.c_int, C.c_int]),
     "och_gpu_unshard_views_dev": (C.c_int, [_P, _P, _P, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int]),
+    "och_gpu_render_codes_views_dev": (C.c_int, [_P, _P, C.c_int, _P, C.c_int, C.c_int, C.c_int, C.c_int]),
+    "och_gpu_shade_unshard_views_dev": (C.c_int, [_P, _P, _P, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int]),
     "och_build_terrain": (C.c_int, [C.POINTER(TerrainParams), C.POINTER(HostPool)]),
     "och_host_pool_free": (None, [C.POINTER(HostPool)]),
     "och_pool_pack": (C.c_int, [_P, _u32, _u32, C.c_int, C.c_int, _P, _u32, C.POINTER(_u32), C.POINTER(_u32)]),

@@ -127,6 +127,7 @@ struct och_gpu_pool {
     int lut_log2 = 0;
     uint32_t *d_palette = nullptr;
     uint32_t n_voxels = 0;
+    uint32_t *d_code_table = nullptr;   // OCH_CODE_* -> RGBA8 (256 words), when n_voxels <= OCH_CODE_MAX_VOXELS
     hipStream_t own_stream = nullptr;
     hipStream_t ext_stream = nullptr;
     bool use_ext = false;           // och_gpu_set_stream called: ext_stream (NULL = null stream)
@@ -433,6 +434,7 @@ OCH_API int och_gpu_pool_destroy(och_gpu_pool *p)
     if (p->d_packed) (void)hipFree(p->d_packed);
     if (p->d_lut) (void)hipFree(p->d_lut);
     if (p->d_palette) (void)hipFree(p->d_palette);
+    if (p->d_code_table) (void)hipFree(p->d_code_table);
     if (p->d_scratch) (void)hipFree(p->d_scratch);
     if (p->d_counter) (void)hipFree(p->d_counter);
     if (p->ev_start) (void)hipEventDestroy(p->ev_start);
@@ -497,8 +499,22 @@ OCH_API int och_gpu_set_palette(och_gpu_pool *p, const uint32_t *rgba, uint32_t 
     DeviceGuard g(p->device);
     OCH_HIP(hipStreamSynchronize(p->stream()));
     if (p->d_palette) OCH_HIP(hipFree(p->d_palette));
+    if (p->d_code_table) OCH_HIP(hipFree(p->d_code_table));
     p->d_palette = nullptr;
+    p->d_code_table = nullptr;
     p->n_voxels = 0;
+    if (n_voxels <= OCH_CODE_MAX_VOXELS) {
+        // Indexed-colour frames: trace_pixel's colour per code
+        // (ORT/test_och_h_octree.cpp:76-84), then config 5's blocked (halved) variants.
+        std::vector<uint32_t> t(256, 0xFFFF00FFu);
+        for (uint32_t c = 0; c < 6 * n_voxels; ++c) t[c] = rgba[c];
+        t[OCH_CODE_INSIDE] = 0xFF07193Fu;
+        t[OCH_CODE_SKY] = 0xFFFEBF00u;
+        for (uint32_t c = 0; c < OCH_CODE_BLOCKED; ++c)
+            t[c | OCH_CODE_BLOCKED] = ((t[c] >> 1) & 0x007F7F7Fu) | (t[c] & 0xFF000000u);
+        OCH_HIP(hipMalloc(&p->d_code_table, 256 * 4));
+        OCH_HIP(hipMemcpy(p->d_code_table, t.data(), 256 * 4, hipMemcpyHostToDevice));
+    }
     if (!n_voxels) return OCH_OK;
     OCH_HIP(hipMalloc(&p->d_palette, (size_t)n_voxels * 6 * 4));
     OCH_HIP(hipMemcpy(p->d_palette, rgba, (size_t)n_voxels * 6 * 4, hipMemcpyHostToDevice));
@@ -726,9 +742,12 @@ OCH_API int och_shard_rows(int height, int row_chunk, int n_shards)
 namespace {
 
 int render_views(och_gpu_pool *p, const och_camera *cams, int n_views, uint32_t *rgba_slices, int row_chunk, int shard,
-                 int n_shards, bool bounce)
+                 int n_shards, bool bounce, uint8_t *code_slices = nullptr)
 {
-    if (!p || !cams || !rgba_slices) return fail(OCH_E_INVALID, "NULL argument");
+    if (!p || !cams || (!rgba_slices && !code_slices)) return fail(OCH_E_INVALID, "NULL argument");
+    if (code_slices && (p->n_voxels > OCH_CODE_MAX_VOXELS || !p->d_code_table))
+        return fail(OCH_E_INVALID, "indexed-colour frames need a palette (och_gpu_set_palette) of at most %d voxel ids",
+                    OCH_CODE_MAX_VOXELS);
     if (n_views < 1 || n_views > OCH_MAX_VIEWS) return fail(OCH_E_INVALID, "n_views %d outside 1..%d", n_views, OCH_MAX_VIEWS);
     if (row_chunk <= 0 || n_shards <= 0 || shard < 0 || shard >= n_shards)
         return fail(OCH_E_INVALID, "bad sharding (%d, %d, %d)", row_chunk, shard, n_shards);
@@ -745,12 +764,15 @@ int render_views(och_gpu_pool *p, const och_camera *cams, int n_views, uint32_t 
     f.palette = p->d_palette;
     f.n_voxels = p->n_voxels;
     f.out = rgba_slices;
+    f.codes = code_slices;
     f.row_chunk = row_chunk;
     f.shard = shard;
     f.n_shards = n_shards;
     f.slice_rows = och_shard_rows(cams[0].height, row_chunk, n_shards);
     OCH_HIP(hipEventRecord(p->ev_start, p->stream()));
-    if (bounce)
+    if (code_slices)
+        OCH_HIP(och::launch_render_codes(p->dev(), f, p->schedule(), bounce, p->stream()));
+    else if (bounce)
         OCH_HIP(och::launch_render_bounce(p->dev(), f, p->schedule(), p->stream()));
     else
         OCH_HIP(och::launch_render(p->dev(), f, p->schedule(), p->stream()));
@@ -771,6 +793,26 @@ OCH_API int och_gpu_render_bounce_views_dev(och_gpu_pool *p, const och_camera *c
                                             int row_chunk, int shard, int n_shards)
 {
     return render_views(p, cams, n_views, rgba_slices, row_chunk, shard, n_shards, true);
+}
+
+OCH_API int och_gpu_render_codes_views_dev(och_gpu_pool *p, const och_camera *cams, int n_views, uint8_t *code_slices,
+                                           int row_chunk, int shard, int n_shards, int bounce)
+{
+    if (!code_slices) return fail(OCH_E_INVALID, "NULL argument");
+    return render_views(p, cams, n_views, nullptr, row_chunk, shard, n_shards, bounce != 0, code_slices);
+}
+
+OCH_API int och_gpu_shade_unshard_views_dev(och_gpu_pool *p, const uint8_t *gathered, uint32_t *frames, int width,
+                                            int height, int row_chunk, int n_shards, int n_views)
+{
+    if (!p || !gathered || !frames || width <= 0 || height <= 0 || row_chunk <= 0 || n_shards <= 0 || n_views < 1)
+        return fail(OCH_E_INVALID, "bad unshard arguments");
+    if (!p->d_code_table)
+        return fail(OCH_E_INVALID, "no code table: set a palette of at most %d voxel ids", OCH_CODE_MAX_VOXELS);
+    DeviceGuard g(p->device);
+    OCH_HIP(och::launch_shade_unshard(gathered, frames, p->d_code_table, width, height, row_chunk, n_shards,
+                                      och_shard_rows(height, row_chunk, n_shards), n_views, p->stream()));
+    return OCH_OK;
 }
 
 OCH_API int och_gpu_render_dev(och_gpu_pool *p, const och_camera *cam, uint32_t *rgba_slice, int row_chunk, int shard,

@@ -34,7 +34,8 @@ struct DevFrame {
     int32_t n_views;
     const uint32_t *palette;  // 6 * n_voxels RGBA8
     uint32_t n_voxels;
-    uint32_t *out;            // n_views compact slices, each slice_rows x width
+    uint32_t *out;            // n_views compact slices, each slice_rows x width (RGBA8)
+    uint8_t *codes;           // or the same slices as indexed colour (launch_render_codes)
     int32_t row_chunk, shard, n_shards, slice_rows;
 };
 
@@ -68,6 +69,11 @@ hipError_t launch_trace_bounce_batch(const DevPool &p, const float *origin, int 
 hipError_t launch_render_bounce(const DevPool &p, const DevFrame &f, const Schedule &sc, hipStream_t stream);
 hipError_t launch_raygen(const och_camera &cam, float *dirs, hipStream_t stream);
 hipError_t launch_render(const DevPool &p, const DevFrame &f, const Schedule &sc, hipStream_t stream);
+// Indexed-colour frames (OCH_CODE_*): render into f.codes, and turn gathered
+// code slices into RGBA8 frames through a 256-entry table.
+hipError_t launch_render_codes(const DevPool &p, const DevFrame &f, const Schedule &sc, bool bounce, hipStream_t stream);
+hipError_t launch_shade_unshard(const uint8_t *gathered, uint32_t *frames, const uint32_t *table, int width, int height,
+                                int row_chunk, int n_shards, int slice_rows, int n_views, hipStream_t stream);
 hipError_t launch_unshard(const uint32_t *gathered, uint32_t *frames, int width, int height, int row_chunk,
                           int n_shards, int slice_rows, int n_views, hipStream_t stream);
 

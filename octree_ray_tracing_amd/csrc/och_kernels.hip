@@ -446,6 +446,39 @@ struct BounceFrameSink {
     }
 };
 
+// Indexed-colour frames (the multi-GPU exchange format, 1 B per pixel): the
+// palette index 6 * (voxel - 1) + dir of a hit face, OCH_CODE_MAGENTA /
+// _INSIDE / _SKY for the other cases of pixel_colour, + OCH_CODE_BLOCKED
+// when a config-5 secondary ray is blocked.  k_shade_unshard turns codes
+// into the same RGBA8 words pixel_colour and BounceFrameSink produce.
+__device__ __forceinline__ uint32_t pixel_code(const Hit &h, uint32_t n_voxels)
+{
+    if (h.dir == OCH_EXIT) return OCH_CODE_SKY;
+    if (h.dir == OCH_INSIDE) return OCH_CODE_INSIDE;
+    if (h.voxel == 0 || h.voxel > n_voxels) return OCH_CODE_MAGENTA;
+    return 6u * (h.voxel - 1u) + (uint32_t)h.dir;
+}
+
+struct CodeSink {
+    uint8_t *out;
+    uint32_t n_voxels;
+    __device__ __forceinline__ void put(uint32_t i, const Hit &h) const { out[i] = (uint8_t)pixel_code(h, n_voxels); }
+};
+
+struct BounceCodeSink {
+    CodeSink f;
+    __device__ __forceinline__ uint32_t put_primary(uint32_t i, const Hit &h, bool bounced) const
+    {
+        const uint32_t c = pixel_code(h, f.n_voxels);
+        if (!bounced) f.out[i] = (uint8_t)c;
+        return c;
+    }
+    __device__ __forceinline__ void put_secondary(uint32_t i, uint32_t c, const Hit &h2) const
+    {
+        f.out[i] = (uint8_t)(h2.dir == OCH_EXIT ? c : c | OCH_CODE_BLOCKED);
+    }
+};
+
 template <bool kCount>
 struct BounceHitSink {
     HitSink<kCount> h;
@@ -690,6 +723,25 @@ __global__ __launch_bounds__(256) void k_unshard(const uint32_t *__restrict__ ga
     frames[((size_t)view * height + row) * width + col] = gathered[src];
 }
 
+// gathered codes [n_shards][n_views][slice_rows][width] -> RGBA8 frames
+// [n_views][height][width] through the 256-entry code table (och_api.cpp
+// code_table: palette words, the fixed colours, the halved blocked variants).
+__global__ __launch_bounds__(256) void k_shade_unshard(const uint8_t *__restrict__ gathered, uint32_t *__restrict__ frames,
+                                                       const uint32_t *__restrict__ table, int width, int height,
+                                                       int row_chunk, int n_shards, int slice_rows, int n_views)
+{
+    __shared__ uint32_t lut[256];
+    lut[threadIdx.x] = table[threadIdx.x];
+    __syncthreads();
+    const int col = blockIdx.x * 256 + threadIdx.x;
+    const int row = blockIdx.y, view = blockIdx.z;
+    if (col >= width || row >= height) return;
+    const int gchunk = row / row_chunk, within = row - gchunk * row_chunk;
+    const int shard = gchunk % n_shards, lchunk = gchunk / n_shards;
+    const size_t src = (((size_t)shard * n_views + view) * slice_rows + (size_t)lchunk * row_chunk + within) * width + col;
+    frames[((size_t)view * height + row) * width + col] = lut[gathered[src]];
+}
+
 size_t stack_bytes(int depth, int block) { return (size_t)(depth > 1 ? depth - 1 : 1) * block * sizeof(uint32_t); }
 
 template <class Src, class Sink, bool kPacked, bool kCount>
@@ -818,6 +870,25 @@ hipError_t launch_render_bounce(const DevPool &p, const DevFrame &f, const Sched
     const CameraSource src = camera_source(f, sc);
     return launch_bounce<CameraSource, BounceFrameSink, false>(
         p, src, BounceFrameSink{FrameSink{f.out, f.palette, f.n_voxels}}, src.count(), sc, stream);
+}
+
+hipError_t launch_render_codes(const DevPool &p, const DevFrame &f, const Schedule &sc, bool bounce, hipStream_t stream)
+{
+    if (f.n_views < 1 || f.n_views > kMaxViews) return hipErrorInvalidValue;
+    const CameraSource src = camera_source(f, sc);
+    const CodeSink k{f.codes, f.n_voxels};
+    if (bounce) return launch_bounce<CameraSource, BounceCodeSink, false>(p, src, BounceCodeSink{k}, src.count(), sc, stream);
+    return launch<CameraSource, CodeSink, false>(p, src, k, src.count(), sc, stream,
+                                                 sc.tile_order == 1 ? 64u * 64u : 0u);
+}
+
+hipError_t launch_shade_unshard(const uint8_t *gathered, uint32_t *frames, const uint32_t *table, int width, int height,
+                                int row_chunk, int n_shards, int slice_rows, int n_views, hipStream_t stream)
+{
+    const dim3 grid((width + 255) / 256, height, n_views);
+    hipLaunchKernelGGL(k_shade_unshard, grid, dim3(256), 0, stream, gathered, frames, table, width, height, row_chunk,
+                       n_shards, slice_rows, n_views);
+    return hipGetLastError();
 }
 
 hipError_t launch_trace_bounce_batch(const DevPool &p, const float *origin, int origin_stride, const float *dirs,

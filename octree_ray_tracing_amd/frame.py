@@ -46,7 +46,8 @@ class ShardedFrame:
     collective and unsharded by one kernel.
     """
 
-    def __init__(self, pool: GpuPool, width: int, height: int, row_chunk: int = 8, n_views: int = 1, group=None):
+    def __init__(self, pool: GpuPool, width: int, height: int, row_chunk: int = 8, n_views: int = 1, group=None,
+                 indexed: bool = False):
         import torch
         import torch.distributed as dist
 
@@ -55,9 +56,14 @@ class ShardedFrame:
         self.rank = dist.get_rank(group) if dist.is_initialized() else 0
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
         self.rows = shard_rows(height, row_chunk, self.world)
+        # indexed=True: ranks render and exchange 1-byte colour codes (OCH_CODE_*)
+        # and shade after the gather -- a quarter of the RGBA8 bytes on xGMI,
+        # the same frames (needs a palette of <= CODE_MAX_VOXELS ids).
+        self.indexed = indexed
         dev = torch.device("cuda", torch.cuda.current_device())
-        self.slice = torch.empty((n_views, self.rows, width), dtype=torch.int32, device=dev)
-        self.gathered = torch.empty((self.world, n_views, self.rows, width), dtype=torch.int32, device=dev)
+        dt = torch.uint8 if indexed else torch.int32
+        self.slice = torch.empty((n_views, self.rows, width), dtype=dt, device=dev)
+        self.gathered = torch.empty((self.world, n_views, self.rows, width), dtype=dt, device=dev)
         self.frames = torch.empty((n_views, height, width), dtype=torch.int32, device=dev)
         pool.set_stream(torch.cuda.current_stream())
 
@@ -67,6 +73,9 @@ class ShardedFrame:
         if not isinstance(cams, (list, tuple)):
             cams = [cams]
         assert len(cams) == self.n_views
+        if self.indexed:
+            self.pool.render_codes_views_dev(list(cams), self.slice, self.row_chunk, self.rank, self.world, bounce)
+            return self.slice
         render = self.pool.render_bounce_views_dev if bounce else self.pool.render_views_dev
         render(list(cams), self.slice, self.row_chunk, self.rank, self.world)
         return self.slice
@@ -83,7 +92,11 @@ class ShardedFrame:
             else:
                 dist.all_gather_into_tensor(self.gathered, self.slice, group=self.group)
             src = self.gathered
-        self.pool.unshard_dev(src, self.frames, self.width, self.height, self.row_chunk, self.world, self.n_views)
+        if self.indexed:
+            self.pool.shade_unshard_dev(src, self.frames, self.width, self.height, self.row_chunk, self.world,
+                                        self.n_views)
+        else:
+            self.pool.unshard_dev(src, self.frames, self.width, self.height, self.row_chunk, self.world, self.n_views)
         return self.frames
 
     def render(self, cams, bounce: bool = False):

@@ -248,6 +248,23 @@ class GpuPool:
         call("och_gpu_unshard_views_dev", self._h, _dev_ptr(gathered), _dev_ptr(frame), int(width), int(height),
              int(row_chunk), int(n_shards), int(n_views))
 
+    # Indexed-colour frames (include/och_gpu.h OCH_CODE_*): one byte per pixel,
+    # the multi-GPU exchange format; shade_unshard_dev yields the RGBA8 frames.
+    CODE_MAX_VOXELS = 20
+
+    def render_codes_views_dev(self, cams, code_slices, row_chunk: int | None = None, shard: int = 0,
+                               n_shards: int = 1, bounce: bool = False):
+        arr = (Camera * len(cams))(*cams)
+        if row_chunk is None:
+            row_chunk = cams[0].height
+        call("och_gpu_render_codes_views_dev", self._h, C.cast(arr, C.c_void_p), len(cams), _dev_ptr(code_slices),
+             int(row_chunk), int(shard), int(n_shards), int(bool(bounce)))
+
+    def shade_unshard_dev(self, gathered_codes, frames, width: int, height: int, row_chunk: int, n_shards: int,
+                          n_views: int = 1):
+        call("och_gpu_shade_unshard_views_dev", self._h, _dev_ptr(gathered_codes), _dev_ptr(frames), int(width),
+             int(height), int(row_chunk), int(n_shards), int(n_views))
+
 
 def shard_rows(height: int, row_chunk: int, n_shards: int) -> int:
     return call("och_shard_rows", int(height), int(row_chunk), int(n_shards))

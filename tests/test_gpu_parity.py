@@ -379,3 +379,45 @@ def test_render_bounce_frames(ort, O, gpu_device):
     for v in range(2):
         assert np.array_equal(full[v].cpu().numpy().view(np.uint32), want[v])
     pool.close()
+
+
+@pytest.mark.parametrize("bounce", [False, True])
+def test_indexed_colour_frames(ort, O, gpu_device, bounce):
+    """The multi-GPU exchange format: 1-byte colour codes per pixel, gathered
+    and shaded on the device, give the oracle's RGBA8 frames bit for bit
+    (primary and config-5 shading), whole and row-sharded over 3 shards."""
+    import torch
+    tree = ort.build_terrain(9)
+    pal = ort.VoxelData().get_colours()
+    pool = ort.HOctree(tree.nodes, tree.root, 9, device=0)
+    pool.set_palette(pal)
+    pool.set_stream(torch.cuda.current_stream())
+    ref_pool = O.OraclePool(tree.nodes, tree.root, 9, 1)
+    W, H = 803, 451
+    pitches = (0.0, -0.6)
+    cams = [ort.camera((1.5, 1.5, 1.5), 0.3, p, 1.25, W, H) for p in pitches]
+    want = []
+    for p in pitches:
+        rays = O.raygen(0.3, p, 1.25, W, H)
+        if bounce:
+            r = O.trace_bounce_batch(ref_pool, O.Rcp(None), ORIGIN, rays, nthreads=16)
+            want.append(O.shade_bounce(r["dir"], r["voxel"], r["dir2"], pal).reshape(H, W))
+        else:
+            r = O.trace_batch(ref_pool, O.Rcp(None), ORIGIN, rays, nthreads=16)
+            want.append(O.shade(r["dir"], r["voxel"], pal).reshape(H, W))
+    for n, chunk in ((1, H), (3, 8), (2, 5)):
+        rows = ort.shard_rows(H, chunk, n)
+        gathered = torch.full((n, 2, rows, W), 255, dtype=torch.uint8, device="cuda")
+        for s_ in range(n):
+            pool.render_codes_views_dev(cams, gathered[s_], chunk, s_, n, bounce)
+        full = torch.empty((2, H, W), dtype=torch.int32, device="cuda")
+        pool.shade_unshard_dev(gathered, full, W, H, chunk, n, 2)
+        torch.cuda.synchronize()
+        for v in range(2):
+            assert np.array_equal(full[v].cpu().numpy().view(np.uint32), want[v]), (n, chunk, v)
+    # a palette too large for one-byte codes is refused
+    big = np.resize(np.asarray(pal, np.uint32).reshape(-1), 6 * 21)
+    pool.set_palette(big)
+    with pytest.raises(ort.OchError):
+        pool.render_codes_views_dev(cams, gathered[0], chunk, 0, n, bounce)
+    pool.close()
