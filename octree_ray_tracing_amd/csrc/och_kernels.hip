@@ -96,18 +96,18 @@ __device__ __forceinline__ void ray_push(Ray &r, const DevPool &P)
 {
     if (kCount) ++r.push;
     const uint32_t c24 = r.idx ^ r.inv;                                     // 24 + child index
-    if (!kPacked || __builtin_amdgcn_ubfe(r.cur, c24, 1u)) {
-        r.child = (P.nodes - 24)[8u * (kPacked ? (r.cur & kIdMask) : r.cur) + c24];
-        set_mode(r, kPending);
-    } else {
-        set_mode(r, kStepping);
-    }
+    const uint32_t present = kPacked ? __builtin_amdgcn_ubfe(r.cur, c24, 1u) : 1u;
+    set_mode(r, kStepping + present);                                       // kStepping or kPending
+    asm volatile("" : "+v"(r.mode));                                        // one add, not a move per branch
+    if (present) r.child = (P.nodes - 24)[8u * (kPacked ? (r.cur & kIdMask) : r.cur) + c24];
 }
 
 // Setup, ORT/och_h_octree.h:294-338, then the first PUSH at the root.
 // stack: this lane's first LDS slot.
+// stack: this lane's LDS column, depth + 1 slots `stride` words apart.
 template <bool kPacked, bool kCount>
-__device__ __forceinline__ void ray_init(Ray &r, const DevPool &P, const float *o, const float *d, uint32_t *stack)
+__device__ __forceinline__ void ray_init(Ray &r, const DevPool &P, const float *o, const float *d, uint32_t *stack,
+                                         uint32_t stride)
 {
     r.inv = 24;
     r.idx = 0;
@@ -135,7 +135,7 @@ __device__ __forceinline__ void ray_init(Ray &r, const DevPool &P, const float *
     }
     r.dim = 1u << 22;                                                       // :326
     r.cur = P.root;
-    r.sp = stack;
+    r.sp = stack + stride;                                                  // slot 0: the miss POP's dummy read
     r.t_min = 0;                                                            // +0.0F
     r.level = 1;
     r.min_axis = 8;
@@ -183,8 +183,11 @@ __device__ __forceinline__ void ray_phase_step(Ray &r, uint32_t stride)
         set_mode(r, kAtPush);
         return;
     }
-    if (--r.level == 0) return;                                         // MISS :423-431
-    r.sp -= stride;                                                     // POP :421-446
+    // POP :421-446.  At the root this is the MISS (:423-431): level 0 ends
+    // the ray, and the rest of the POP runs on dead state (its stack read
+    // lands in the column's spare slot 0) rather than behind a branch.
+    --r.level;
+    r.sp -= stride;
     r.cur = *r.sp;                                                      // :434
 #pragma unroll
     for (int a = 0; a < 3; ++a) r.p[a] &= ~r.dim;                       // :436
@@ -204,9 +207,11 @@ __device__ __forceinline__ void ray_phase_descend(Ray &r, const DevPool &P, uint
         return;
     }
     // HIT :346-355 when the PUSH was at the leaf level: level becomes
-    // depth + 1 (finished) exactly as a descent increments it, and the voxel
-    // id stays in r.child (no later load overwrites a finished lane's).
-    if (++r.level > P.depth) return;
+    // depth + 1 (finished) exactly as a descent increments it, the voxel id
+    // stays in r.child (no later load overwrites a finished lane's), and the
+    // rest of the descent runs on dead state (its stack write lands in the
+    // column's spare top slot) rather than behind a branch.
+    ++r.level;
     *r.sp = r.cur;                                                          // :357
     r.sp += stride;
     r.cur = child;
@@ -560,7 +565,7 @@ __global__ void k_trace_grid(DevPool P, Src S, Sink K, uint32_t xcd_group, uint6
     uint32_t out;
     if (wave_base + lane < S.count() && S.get_wave(wave_base, lane, o, d, out)) {
         Ray r;
-        ray_init<kPacked, kCount>(r, P, o, d, lds_stack + threadIdx.x);
+        ray_init<kPacked, kCount>(r, P, o, d, lds_stack + threadIdx.x, blockDim.x);
         do {
             ray_iterate<kPacked, kCount>(r, P, blockDim.x);
         } while (ray_active(r, P));
@@ -573,17 +578,16 @@ __global__ void k_trace_grid(DevPool P, Src S, Sink K, uint32_t xcd_group, uint6
 // lanes (ballot + popcount per wave, wave offsets through LDS) write their
 // secondary rays into an LDS queue, and the first lanes of the block trace
 // them, so waves whose tiles mostly missed retire instead of idling beside
-// a few bounced lanes.  stack_words: LDS words of the parent stacks; the
-// queue (8 words per thread, SoA) follows them.
+// a few bounced lanes.  The queue (8 words per thread, SoA) reuses the
+// parent stacks' LDS between the passes.
 template <class Src, class Sink, bool kPacked, bool kCount>
-__global__ void k_trace_bounce(DevPool P, Src S, Sink K, uint32_t stack_words, int compact, uint64_t *stamps,
-                               uint32_t stamp_cap)
+__global__ void k_trace_bounce(DevPool P, Src S, Sink K, int compact, uint64_t *stamps, uint32_t stamp_cap)
 {
     extern __shared__ uint32_t lds_stack[];
     __shared__ uint32_t wave_count[16];
     const uint64_t t0 = stamps ? realtime() : 0;
     uint32_t *stack = lds_stack + threadIdx.x;
-    uint32_t *queue = lds_stack + stack_words;
+    uint32_t *queue = lds_stack;
     const uint32_t nb = blockDim.x;
     const uint32_t wave_base = blockIdx.x * nb + (threadIdx.x & ~63u);
     float o[3], d[3], o2[3], d2[3];
@@ -591,7 +595,7 @@ __global__ void k_trace_bounce(DevPool P, Src S, Sink K, uint32_t stack_words, i
     bool want = false;
     if (wave_base + (threadIdx.x & 63u) < S.count() && S.get_wave(wave_base, threadIdx.x & 63u, o, d, out)) {
         Ray r;
-        ray_init<kPacked, kCount>(r, P, o, d, stack);
+        ray_init<kPacked, kCount>(r, P, o, d, stack, nb);
         do {
             ray_iterate<kPacked, kCount>(r, P, nb);
         } while (ray_active(r, P));
@@ -600,7 +604,7 @@ __global__ void k_trace_bounce(DevPool P, Src S, Sink K, uint32_t stack_words, i
         if (want) bounce_ray(o, d, h1, P.half_voxel, o2, d2);
         payload = K.put_primary(out, h1, want);
         if (want && !compact) {                                             // in place, no compaction
-            ray_init<kPacked, kCount>(r, P, o2, d2, stack);
+            ray_init<kPacked, kCount>(r, P, o2, d2, stack, nb);
             do {
                 ray_iterate<kPacked, kCount>(r, P, nb);
             } while (ray_active(r, P));
@@ -633,13 +637,20 @@ __global__ void k_trace_bounce(DevPool P, Src S, Sink K, uint32_t stack_words, i
         queue[7 * nb + q] = payload;
     }
     __syncthreads();
-    if (threadIdx.x < total) {
+    float so[3], sd[3];
+    uint32_t sout = 0, spay = 0;
+    const bool has = threadIdx.x < total;
+    if (has) {
         const uint32_t q = threadIdx.x;
-        const float so[3] = {ffrom(queue[0 * nb + q]), ffrom(queue[1 * nb + q]), ffrom(queue[2 * nb + q])};
-        const float sd[3] = {ffrom(queue[3 * nb + q]), ffrom(queue[4 * nb + q]), ffrom(queue[5 * nb + q])};
-        const uint32_t sout = queue[6 * nb + q], spay = queue[7 * nb + q];
+        so[0] = ffrom(queue[0 * nb + q]); so[1] = ffrom(queue[1 * nb + q]); so[2] = ffrom(queue[2 * nb + q]);
+        sd[0] = ffrom(queue[3 * nb + q]); sd[1] = ffrom(queue[4 * nb + q]); sd[2] = ffrom(queue[5 * nb + q]);
+        sout = queue[6 * nb + q];
+        spay = queue[7 * nb + q];
+    }
+    __syncthreads();                                  // the queue is read: its LDS becomes stacks again
+    if (has) {
         Ray r;
-        ray_init<kPacked, kCount>(r, P, so, sd, stack);
+        ray_init<kPacked, kCount>(r, P, so, sd, stack, nb);
         do {
             ray_iterate<kPacked, kCount>(r, P, nb);
         } while (ray_active(r, P));
@@ -675,7 +686,7 @@ __global__ void k_trace_persistent(DevPool P, Src S, Sink K, uint32_t *counter, 
                 const uint32_t i = base + (uint32_t)__popcll(idle & below);
                 float o[3], d[3];
                 if (i < n && S.get(i, o, d, out)) {
-                    ray_init<kPacked, kCount>(r, P, o, d, stack);
+                    ray_init<kPacked, kCount>(r, P, o, d, stack, blockDim.x);
                     active = true;
                 }
             }
@@ -742,7 +753,9 @@ __global__ __launch_bounds__(256) void k_shade_unshard(const uint8_t *__restrict
     frames[((size_t)view * height + row) * width + col] = lut[gathered[src]];
 }
 
-size_t stack_bytes(int depth, int block) { return (size_t)(depth > 1 ? depth - 1 : 1) * block * sizeof(uint32_t); }
+// Per lane: parents of levels 1..depth-1 in slots 1..depth-1, plus a spare
+// slot below (the miss POP's read) and above (the hit descent's write).
+size_t stack_bytes(int depth, int block) { return (size_t)(depth + 1) * block * sizeof(uint32_t); }
 
 template <class Src, class Sink, bool kPacked, bool kCount>
 hipError_t launch_as(const DevPool &p, const Src &s, const Sink &k, uint32_t n, const Schedule &sc, hipStream_t stream,
@@ -786,15 +799,15 @@ hipError_t launch_bounce(const DevPool &p, const Src &s, const Sink &k, uint32_t
 {
     if (n == 0) return hipSuccess;
     const int block = sc.block > kBounceBlock ? sc.block : kBounceBlock;
-    const uint32_t stack_words = (uint32_t)(stack_bytes(p.depth, block) / sizeof(uint32_t));
-    const size_t lds = (stack_words + 8u * (uint32_t)block) * sizeof(uint32_t);
+    const size_t queue = 8u * (size_t)block * sizeof(uint32_t);
+    const size_t lds = stack_bytes(p.depth, block) > queue ? stack_bytes(p.depth, block) : queue;
     const dim3 grid((n + block - 1) / block);
     if (p.packed)
         hipLaunchKernelGGL((k_trace_bounce<Src, Sink, true, kCount>), grid, dim3(block), lds, stream, p, s, k,
-                           stack_words, sc.bounce_compact, sc.stamps, sc.stamp_cap);
+                           sc.bounce_compact, sc.stamps, sc.stamp_cap);
     else
         hipLaunchKernelGGL((k_trace_bounce<Src, Sink, false, kCount>), grid, dim3(block), lds, stream, p, s, k,
-                           stack_words, sc.bounce_compact, sc.stamps, sc.stamp_cap);
+                           sc.bounce_compact, sc.stamps, sc.stamp_cap);
     return hipGetLastError();
 }
 
