@@ -110,7 +110,11 @@ def build_pool_nodes(depth: int, rank: int, world: int, dev):
 
 def cpu_baseline(nodes, root, depth, width, height, budget_s: float = 8.0):
     """The CPU oracle (a C port of the reference tracer, native RCPPS) on this
-    host: raygen + trace + shade of the same frames, rank 0 only."""
+    host, rank 0 only.  `value`: traversal of the two views' camera rays
+    (generated once, outside the timed region) on every allowed thread for
+    about budget_s; `value_1core`: the same two views once on one thread;
+    `value_frame_path`: raygen + trace + numpy shading of two frames, the
+    whole per-frame job as this harness runs it."""
     from oracle import oracle as O
     import octree_ray_tracing_amd as ort
 
@@ -120,26 +124,58 @@ def cpu_baseline(nodes, root, depth, width, height, budget_s: float = 8.0):
     rcp = O.Rcp(None)
     pal = ort.VoxelData().get_colours()
     origin = np.array(ORIGIN, np.float32)
+    views = [O.raygen(YAW, p, FOV, width, height) for p in PITCHES]
     rays_done, t_total, frames = 0, 0.0, 0
     t_end = time.perf_counter() + budget_s
     while time.perf_counter() < t_end or frames < 2:
-        pitch = PITCHES[frames % 2]
+        rays = views[frames % 2]
         t0 = time.perf_counter()
-        rays = O.raygen(YAW, pitch, FOV, width, height)
-        r = O.trace_batch(pool, rcp, origin, rays, nthreads=threads)
-        sky = r["dir"] == 6
-        rgba = np.where(sky, np.uint32(0xFFFEBF00), pal[np.clip(6 * (r["voxel"].astype(np.int64) - 1) + r["dir"], 0, pal.size - 1)])
-        rgba[r["dir"] == 7] = 0xFF07193F
+        O.trace_batch(pool, rcp, origin, rays, nthreads=threads)
         t_total += time.perf_counter() - t0
         rays_done += rays.shape[0]
         frames += 1
+    # One core (SURVEY 8d asks for 1 thread and all threads).
+    t1 = time.perf_counter()
+    for rays in views:
+        O.trace_batch(pool, rcp, origin, rays, nthreads=1)
+    t1 = time.perf_counter() - t1
+    # The whole frame as this harness runs it (single-threaded raygen, numpy shading).
+    tf = time.perf_counter()
+    for p in PITCHES:
+        r = O.trace_batch(pool, rcp, origin, O.raygen(YAW, p, FOV, width, height), nthreads=threads)
+        O.shade_fast(r["dir"], r["voxel"], pal)
+    tf = time.perf_counter() - tf
     try:
         cpu = next(l.split(":", 1)[1].strip() for l in open("/proc/cpuinfo") if l.startswith("model name"))
     except Exception:
         cpu = "unknown"
+    n2 = width * height * len(PITCHES)
     return {"value": rays_done / t_total / 1e6, "unit": "Mrays/s", "cores": threads, "kind": "port",
-            "sample": f"{frames} full {width}x{height} frames (pitch 0 / -0.6 alternating), depth {depth}, "
-                      f"oracle raygen+trace+shade, {threads} threads on {cpu}, {t_total:.1f}s"}
+            "sample": f"{frames} traversals of full {width}x{height} camera frames (pitch 0 / -0.6 alternating, "
+                      f"rays generated untimed), depth {depth}, {threads} threads on {cpu}, {t_total:.1f}s",
+            "value_1core": n2 / t1 / 1e6,
+            "sample_1core": f"the two views' traversal once on 1 thread, {t1:.1f}s",
+            "value_frame_path": n2 / tf / 1e6,
+            "sample_frame_path": f"raygen (1 thread) + traversal ({threads} threads) + numpy shading of the two views, {tf:.2f}s"}
+
+
+# gfx950 VALU issue: a wave64 VALU instruction takes 2 cycles of its SIMD
+# (MI355X_MICROARCH.md), 4 SIMDs per CU, 256 CUs, 2.4 GHz peak engine clock.
+VALU_PEAK_GINST_S = 256 * 4 * 2.4 / 2
+
+
+def valu_roofline(pmc, step_s: float):
+    """The render kernel's real limiter: VALU wave-instructions per launch
+    (rocprofv3 SQ_INSTS_VALU from profiles/pmc_summary.json, the same config)
+    issued per second of the pipelined step, against the chip's issue peak."""
+    if not pmc or "SQ_INSTS_VALU" not in pmc:
+        return None
+    insts = float(pmc["SQ_INSTS_VALU"])
+    ach = insts / step_s / 1e9
+    return {"bound": "valu-issue", "insts_per_launch": int(insts), "insts_per_wave": pmc.get("valu_insts_per_wave"),
+            "achieved": round(ach, 1), "peak": VALU_PEAK_GINST_S, "unit": "G wave-instructions/s",
+            "frac": round(ach / VALU_PEAK_GINST_S, 4),
+            "source": "rocprofv3 --pmc SQ_INSTS_VALU (profiles/pmc_summary.json) / bench ms_per_step"}
 
 
 def load_pmc(kernel: str, config_key: str):
@@ -397,6 +433,7 @@ def main():
                          "kernel_ms_idle_gpu": round(latency_ms, 4), "frames_in_flight": len(streams),
                          "bytes_per_launch": int(bytes_per_launch),
                          "push_per_ray": round(push_total / rays_rank, 3),
+                         "valu": valu_roofline(pmc, elapsed / a.steps),
                          "note": "pointer-chase over an L2/MALL-resident DAG: latency/VALU-bound, not HBM-bound"},
             "cpu_baseline": cpu,
             "trace_batch": trace_only,

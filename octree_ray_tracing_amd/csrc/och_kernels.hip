@@ -753,6 +753,27 @@ __global__ __launch_bounds__(256) void k_shade_unshard(const uint8_t *__restrict
     frames[((size_t)view * height + row) * width + col] = lut[gathered[src]];
 }
 
+// The same for width % 4 == 0: four pixels per thread, one 4-B code load and
+// one 16-B store, a quarter of the waves (they share the CUs with the render
+// launches of the frames in flight).
+__global__ __launch_bounds__(256) void k_shade_unshard4(const uint8_t *__restrict__ gathered, uint32_t *__restrict__ frames,
+                                                        const uint32_t *__restrict__ table, int width, int height,
+                                                        int row_chunk, int n_shards, int slice_rows, int n_views)
+{
+    __shared__ uint32_t lut[256];
+    lut[threadIdx.x] = table[threadIdx.x];
+    __syncthreads();
+    const int col = (blockIdx.x * 256 + threadIdx.x) * 4;
+    const int row = blockIdx.y, view = blockIdx.z;
+    if (col >= width || row >= height) return;
+    const int gchunk = row / row_chunk, within = row - gchunk * row_chunk;
+    const int shard = gchunk % n_shards, lchunk = gchunk / n_shards;
+    const size_t src = (((size_t)shard * n_views + view) * slice_rows + (size_t)lchunk * row_chunk + within) * width + col;
+    const uint32_t c = *reinterpret_cast<const uint32_t *>(gathered + src);
+    const uint4 px = make_uint4(lut[c & 0xFFu], lut[(c >> 8) & 0xFFu], lut[(c >> 16) & 0xFFu], lut[c >> 24]);
+    *reinterpret_cast<uint4 *>(frames + ((size_t)view * height + row) * width + col) = px;
+}
+
 // Per lane: parents of levels 1..depth-1 in slots 1..depth-1, plus a spare
 // slot below (the miss POP's read) and above (the hit descent's write).
 size_t stack_bytes(int depth, int block) { return (size_t)(depth + 1) * block * sizeof(uint32_t); }
@@ -898,6 +919,13 @@ hipError_t launch_render_codes(const DevPool &p, const DevFrame &f, const Schedu
 hipError_t launch_shade_unshard(const uint8_t *gathered, uint32_t *frames, const uint32_t *table, int width, int height,
                                 int row_chunk, int n_shards, int slice_rows, int n_views, hipStream_t stream)
 {
+    const bool vec4 = width % 4 == 0 && ((uintptr_t)gathered & 3u) == 0 && ((uintptr_t)frames & 15u) == 0;
+    if (vec4) {
+        const dim3 grid((width / 4 + 255) / 256, height, n_views);
+        hipLaunchKernelGGL(k_shade_unshard4, grid, dim3(256), 0, stream, gathered, frames, table, width, height,
+                           row_chunk, n_shards, slice_rows, n_views);
+        return hipGetLastError();
+    }
     const dim3 grid((width + 255) / 256, height, n_views);
     hipLaunchKernelGGL(k_shade_unshard, grid, dim3(256), 0, stream, gathered, frames, table, width, height, row_chunk,
                        n_shards, slice_rows, n_views);

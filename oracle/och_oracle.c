@@ -174,15 +174,30 @@ typedef struct ora_batch_job {
     const ora_pool *P; const ora_rcp *R;
     const float *origin; int origin_stride; const float *dirs;
     int32_t *hit_dir; uint32_t *hit_voxel; float *hit_time; uint32_t *push;
-    uint64_t begin, end;
+    uint64_t *next, n;          /* shared work counter: rays are handed out ORA_GRAIN at a time */
     ora_counts cnt;
 } ora_batch_job;
+
+/* Dynamic hand-out keeps the threads balanced: sky rows trace in a few
+ * steps, terrain rows in hundreds, so contiguous ranges would idle most
+ * threads behind the one holding the horizon. */
+#define ORA_GRAIN 256u
+
+static int ora_next_range(uint64_t *next, uint64_t n, uint64_t *b, uint64_t *e)
+{
+    *b = __atomic_fetch_add(next, ORA_GRAIN, __ATOMIC_RELAXED);
+    if (*b >= n) return 0;
+    *e = *b + ORA_GRAIN < n ? *b + ORA_GRAIN : n;
+    return 1;
+}
 
 static void *ora_batch_worker(void *arg)
 {
     ora_batch_job *j = (ora_batch_job *)arg;
     memset(&j->cnt, 0, sizeof j->cnt);
-    for (uint64_t i = j->begin; i < j->end; ++i) {
+    uint64_t b, e;
+    while (ora_next_range(j->next, j->n, &b, &e))
+    for (uint64_t i = b; i < e; ++i) {
         const float *o = j->origin + (size_t)i * j->origin_stride;
         const float *d = j->dirs + 3 * i;
         uint64_t p0 = j->cnt.push;
@@ -194,7 +209,7 @@ static void *ora_batch_worker(void *arg)
 }
 
 /* The reference's per-pixel loop (ORT/test_och_h_octree.cpp:448-450) traced
- * over a batch; nthreads > 1 splits it into contiguous ranges. */
+ * over a batch; nthreads > 1 shares it out ORA_GRAIN rays at a time. */
 ORA_API void ora_trace_batch(const ora_pool *P, const ora_rcp *R,
                              const float *origin, int origin_stride, const float *dirs, uint64_t n,
                              int32_t *hit_dir, uint32_t *hit_voxel, float *hit_time, uint32_t *push,
@@ -204,9 +219,10 @@ ORA_API void ora_trace_batch(const ora_pool *P, const ora_rcp *R,
     if (nthreads > 256) nthreads = 256;
     ora_batch_job jobs[256];
     pthread_t th[256];
+    uint64_t next = 0;
     for (int k = 0; k < nthreads; ++k) {
         jobs[k] = (ora_batch_job){P, R, origin, origin_stride, dirs, hit_dir, hit_voxel, hit_time, push,
-                                  n * k / nthreads, n * (k + 1) / nthreads, {0, 0, 0}};
+                                  &next, n, {0, 0, 0}};
         if (nthreads == 1) ora_batch_worker(&jobs[k]);
         else pthread_create(&th[k], NULL, ora_batch_worker, &jobs[k]);
     }
@@ -241,7 +257,7 @@ typedef struct ora_bounce_job {
     const ora_pool *P; const ora_rcp *R;
     const float *origin; int origin_stride; const float *dirs;
     int32_t *hd; uint32_t *hv; float *ht; int32_t *hd2; uint32_t *hv2; float *ht2; uint32_t *push;
-    uint64_t begin, end;
+    uint64_t *next, n;
     ora_counts cnt;
 } ora_bounce_job;
 
@@ -249,7 +265,9 @@ static void *ora_bounce_worker(void *arg)
 {
     ora_bounce_job *j = (ora_bounce_job *)arg;
     memset(&j->cnt, 0, sizeof j->cnt);
-    for (uint64_t i = j->begin; i < j->end; ++i) {
+    uint64_t b, e;
+    while (ora_next_range(j->next, j->n, &b, &e))
+    for (uint64_t i = b; i < e; ++i) {
         const float *o = j->origin + (size_t)i * j->origin_stride;
         const float *d = j->dirs + 3 * i;
         const uint64_t p0 = j->cnt.push;
@@ -276,9 +294,10 @@ ORA_API void ora_trace_bounce_batch(const ora_pool *P, const ora_rcp *R, const f
     if (nthreads > 256) nthreads = 256;
     ora_bounce_job jobs[256];
     pthread_t th[256];
+    uint64_t next = 0;
     for (int k = 0; k < nthreads; ++k) {
         jobs[k] = (ora_bounce_job){P, R, origin, origin_stride, dirs, hd, hv, ht, hd2, hv2, ht2, push,
-                                   n * k / nthreads, n * (k + 1) / nthreads, {0, 0, 0}};
+                                   &next, n, {0, 0, 0}};
         if (nthreads == 1) ora_bounce_worker(&jobs[k]);
         else pthread_create(&th[k], NULL, ora_bounce_worker, &jobs[k]);
     }

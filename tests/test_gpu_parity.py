@@ -381,11 +381,12 @@ def test_render_bounce_frames(ort, O, gpu_device):
     pool.close()
 
 
-@pytest.mark.parametrize("bounce", [False, True])
-def test_indexed_colour_frames(ort, O, gpu_device, bounce):
+@pytest.mark.parametrize("bounce,W", [(False, 803), (True, 803), (False, 804)])
+def test_indexed_colour_frames(ort, O, gpu_device, bounce, W):
     """The multi-GPU exchange format: 1-byte colour codes per pixel, gathered
     and shaded on the device, give the oracle's RGBA8 frames bit for bit
-    (primary and config-5 shading), whole and row-sharded over 3 shards."""
+    (primary and config-5 shading), whole and row-sharded over 3 shards.
+    W = 804 takes the four-pixels-per-thread shading kernel."""
     import torch
     tree = ort.build_terrain(9)
     pal = ort.VoxelData().get_colours()
@@ -393,7 +394,7 @@ def test_indexed_colour_frames(ort, O, gpu_device, bounce):
     pool.set_palette(pal)
     pool.set_stream(torch.cuda.current_stream())
     ref_pool = O.OraclePool(tree.nodes, tree.root, 9, 1)
-    W, H = 803, 451
+    H = 451
     pitches = (0.0, -0.6)
     cams = [ort.camera((1.5, 1.5, 1.5), 0.3, p, 1.25, W, H) for p in pitches]
     want = []
