@@ -99,7 +99,13 @@ __device__ __forceinline__ void ray_push(Ray &r, const DevPool &P)
     const uint32_t present = kPacked ? __builtin_amdgcn_ubfe(r.cur, c24, 1u) : 1u;
     set_mode(r, kStepping + present);                                       // kStepping or kPending
     asm volatile("" : "+v"(r.mode));                                        // one add, not a move per branch
+#if OCH_PUSH_UNCOND
+    // The slot exists whether or not the child does (cur names a pool node),
+    // so every PUSH may load it; the word is used only when present.
+    if (kPacked || present) r.child = (P.nodes - 24)[8u * (kPacked ? (r.cur & kIdMask) : r.cur) + c24];
+#else
     if (present) r.child = (P.nodes - 24)[8u * (kPacked ? (r.cur & kIdMask) : r.cur) + c24];
+#endif
 }
 
 // Setup, ORT/och_h_octree.h:294-338, then the first PUSH at the root.
