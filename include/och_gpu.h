@@ -284,6 +284,46 @@ OCH_API int och_pool_pack(const uint32_t *nodes, uint32_t n_nodes, uint32_t root
 OCH_API uint32_t och_pool_at(const uint32_t *nodes, uint32_t root, int depth, int index_base,
                              int x, int y, int z);
 
+/* ------------------------------------------------------------ editor */
+/* Interactive editing (the demo's place/remove, ORT/test_och_h_octree.cpp:
+ * 301-435): h_octree::set / at (ORT/och_h_octree.h:176-258) over a host pool of
+ * `capacity` slots (1-based, slot s at nodes[(s-1)*8]) that a device pool of
+ * the same size mirrors.  An edit path-copies at most `depth` new nodes into
+ * the lowest free slots and frees dead ones; och_editor_flush uploads the
+ * window of slots written since the last flush through och_gpu_pool_update.
+ * Traced records equal the reference's after the same edits (slot numbering
+ * differs: the reference places nodes by hash, :110-160). */
+typedef struct och_editor och_editor;
+
+typedef struct och_editor_stats {
+    uint32_t capacity;      /* slots */
+    uint32_t live_nodes;    /* distinct nodes reachable from the root */
+    uint32_t high_water;    /* highest slot ever handed out */
+    uint32_t root;
+    int32_t depth;
+    uint32_t dirty_first;   /* window written since the last flush (count 0 = none) */
+    uint32_t dirty_count;
+} och_editor_stats;
+
+/* Adopt a 1-based pool (e.g. och_build_terrain's; root 0 = empty tree).
+ * OCH_E_INVALID for an out-of-range child or an empty interior node,
+ * OCH_E_CAPACITY if its nodes do not fit in capacity slots. */
+OCH_API int och_editor_create(const uint32_t *nodes, uint32_t n_nodes, uint32_t root, int depth,
+                              uint32_t capacity, och_editor **out);
+OCH_API int och_editor_destroy(och_editor *editor);
+/* h_octree::set: voxel (x,y,z) := v (0 removes).  Out-of-range coordinates are
+ * ignored, as in the reference.  OCH_E_CAPACITY (tree unchanged) when fewer
+ * than depth slots are free; the reference exit(0)s (ORT/och_h_octree.h:112-116). */
+OCH_API int och_editor_set(och_editor *editor, int x, int y, int z, uint32_t v);
+OCH_API uint32_t och_editor_at(const och_editor *editor, int x, int y, int z);
+OCH_API int och_editor_info(const och_editor *editor, och_editor_stats *info);
+/* The slot array (capacity x 8, valid until the next edit) and root: pass
+ * them to och_gpu_pool_create to make the mirroring device pool. */
+OCH_API int och_editor_nodes(const och_editor *editor, const uint32_t **nodes, uint32_t *n_slots, uint32_t *root);
+/* Upload the dirty window and the root to a pool made from this editor
+ * (index_base 1, same depth, capacity slots). */
+OCH_API int och_editor_flush(och_editor *editor, och_gpu_pool *pool);
+
 #ifdef __cplusplus
 }
 #endif

@@ -38,6 +38,11 @@ class PoolInfo(C.Structure):
                 ("rcp_log2_entries", C.c_int32), ("device", C.c_int32)]
 
 
+class EditorStats(C.Structure):
+    _fields_ = [("capacity", C.c_uint32), ("live_nodes", C.c_uint32), ("high_water", C.c_uint32),
+                ("root", C.c_uint32), ("depth", C.c_int32), ("dirty_first", C.c_uint32), ("dirty_count", C.c_uint32)]
+
+
 class TerrainParams(C.Structure):
     _fields_ = [("depth", C.c_int32), ("tunnels", C.c_int32), ("dedup", C.c_int32),
                 ("rand_kind", C.c_int32), ("threads", C.c_int32), ("use_gpu", C.c_int32)]
@@ -91,6 +96,13 @@ PROTOTYPES = {
     "och_host_pool_free": (None, [C.POINTER(HostPool)]),
     "och_pool_pack": (C.c_int, [_P, _u32, _u32, C.c_int, C.c_int, _P, _u32, C.POINTER(_u32), C.POINTER(_u32)]),
     "och_pool_at": (_u32, [_P, _u32, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int]),
+    "och_editor_create": (C.c_int, [_P, _u32, _u32, C.c_int, _u32, C.POINTER(_P)]),
+    "och_editor_destroy": (C.c_int, [_P]),
+    "och_editor_set": (C.c_int, [_P, C.c_int, C.c_int, C.c_int, _u32]),
+    "och_editor_at": (_u32, [_P, C.c_int, C.c_int, C.c_int]),
+    "och_editor_info": (C.c_int, [_P, C.POINTER(EditorStats)]),
+    "och_editor_nodes": (C.c_int, [_P, C.POINTER(C.POINTER(_u32)), C.POINTER(_u32), C.POINTER(_u32)]),
+    "och_editor_flush": (C.c_int, [_P, _P]),
 }
 
 # Functions whose int return value is data, not a status.

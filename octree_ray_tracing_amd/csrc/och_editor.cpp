@@ -1,0 +1,272 @@
+// Host-side DAG editor: h_octree::set / at (ORT/och_h_octree.h:176-258) over a
+// compact, capacity-bounded slot pool that a device pool mirrors slot for slot.
+//
+// The reference edits its node_hashtable in place: set() walks root -> voxel,
+// then path-copies bottom-up, remove_node()-ing each old path node and
+// register_node()-ing the new one (hash-consed, refcounted; :110-174).  Slot
+// placement follows the FNV hash, so an edit touches slots scattered over the
+// whole 2^L table.  Here a node keeps its slot until it dies, new nodes take
+// the lowest free slots, and every written slot is recorded, so
+// och_editor_flush re-uploads one [first, last] window of dirty slots through
+// och_gpu_pool_update instead of the pool.
+//
+// Differences from the reference that do not change any traced record (the
+// tracer reads children only, never slot positions or counts):
+//  * nodes are interned per level (content + level key), so refcounts are
+//    exact parent counts and a dead node releases its children recursively;
+//    the reference's per-registration counts (:144, :166) never release a
+//    dead node's children and can share one slot between levels.
+//  * a full pool is reported (OCH_E_CAPACITY) before the edit starts and the
+//    tree is left unchanged; the reference exit(0)s mid-edit (:112-116).
+#include "och_internal.h"
+
+#include <array>
+#include <cstring>
+#include <new>
+#include <unordered_map>
+#include <vector>
+
+namespace {
+
+using Key = std::array<uint32_t, 9>;   // 8 children + level
+
+struct KeyHash {
+    size_t operator()(const Key &k) const noexcept
+    {
+        uint64_t h = 0xCBF29CE484222325ull;   // FNV-1a over the 36 bytes
+        for (uint32_t w : k)
+            for (int b = 0; b < 4; ++b) h = (h ^ ((w >> (8 * b)) & 0xFF)) * 0x100000001B3ull;
+        return (size_t)h;
+    }
+};
+
+inline int child_of(int x, int y, int z, int level)   // z_encode_16 digit, ORT/och_z_order.cpp
+{
+    return ((x >> level) & 1) | (((y >> level) & 1) << 1) | (((z >> level) & 1) << 2);
+}
+
+}  // namespace
+
+struct och_editor {
+    int depth = 0;
+    uint32_t capacity = 0;                // slots 1..capacity
+    uint32_t root = 0;
+    uint32_t next_unused = 1;             // slots >= next_unused were never handed out
+    uint32_t live = 0;
+    std::vector<uint32_t> nodes;          // capacity x 8, slot s at (s-1)*8
+    std::vector<uint32_t> refs;           // parent count (+1 for the root)
+    std::vector<uint8_t> level;
+    std::vector<uint32_t> free_slots;
+    std::unordered_map<Key, uint32_t, KeyHash> index;
+    uint32_t dirty_lo = UINT32_MAX, dirty_hi = 0;
+    bool root_dirty = false;
+
+    uint32_t *slot(uint32_t s) { return nodes.data() + (size_t)(s - 1) * 8; }
+    const uint32_t *slot(uint32_t s) const { return nodes.data() + (size_t)(s - 1) * 8; }
+    void mark(uint32_t s)
+    {
+        if (s < dirty_lo) dirty_lo = s;
+        if (s > dirty_hi) dirty_hi = s;
+    }
+    uint32_t headroom() const { return (uint32_t)free_slots.size() + (capacity + 1 - next_unused); }
+
+    // register_node (:110-160): find the node or give it a slot; a new node
+    // takes one reference on each of its children.
+    uint32_t intern(const uint32_t *n, int lvl)
+    {
+        Key k;
+        std::memcpy(k.data(), n, 32);
+        k[8] = (uint32_t)lvl;
+        auto it = index.find(k);
+        if (it != index.end()) return it->second;
+        uint32_t s;
+        if (!free_slots.empty()) {
+            s = free_slots.back();
+            free_slots.pop_back();
+        } else {
+            s = next_unused++;
+        }
+        std::memcpy(slot(s), n, 32);
+        refs[s] = 0;
+        level[s] = (uint8_t)lvl;
+        index.emplace(k, s);
+        ++live;
+        mark(s);
+        if (lvl > 0)
+            for (int c = 0; c < 8; ++c)
+                if (n[c]) ++refs[n[c]];
+        return s;
+    }
+
+    // remove_node (:162-174), completed: a dead node is unindexed, zeroed and
+    // releases its children.
+    void release(uint32_t s)
+    {
+        if (--refs[s]) return;
+        Key k;
+        std::memcpy(k.data(), slot(s), 32);
+        k[8] = level[s];
+        index.erase(k);
+        const int lvl = level[s];
+        uint32_t n[8];
+        std::memcpy(n, slot(s), 32);
+        std::memset(slot(s), 0, 32);
+        free_slots.push_back(s);
+        --live;
+        mark(s);
+        if (lvl > 0)
+            for (int c = 0; c < 8; ++c)
+                if (n[c]) release(n[c]);
+    }
+
+    // Copy an input pool in, level by level; memo maps (input id, level) to slots.
+    int adopt(const uint32_t *in, uint32_t n_in, uint32_t id, int lvl,
+              std::unordered_map<uint64_t, uint32_t> &memo, uint32_t *out)
+    {
+        if (id == 0 || id > n_in) return OCH_E_INVALID;
+        auto it = memo.find((uint64_t)id << 8 | (uint64_t)lvl);
+        if (it != memo.end()) {
+            *out = it->second;
+            return OCH_OK;
+        }
+        uint32_t n[8];
+        std::memcpy(n, in + (size_t)(id - 1) * 8, 32);
+        if (lvl > 0)
+            for (int c = 0; c < 8; ++c)
+                if (n[c]) {
+                    const int st = adopt(in, n_in, n[c], lvl - 1, memo, &n[c]);
+                    if (st != OCH_OK) return st;
+                }
+        bool zero = true;
+        for (int c = 0; c < 8; ++c) zero &= n[c] == 0;
+        if (zero) return OCH_E_INVALID;   // an empty node is never registered (:226-229)
+        if (headroom() == 0) return OCH_E_CAPACITY;
+        *out = intern(n, lvl);
+        memo.emplace((uint64_t)id << 8 | (uint64_t)lvl, *out);
+        return OCH_OK;
+    }
+};
+
+extern "C" {
+
+OCH_API int och_editor_create(const uint32_t *nodes, uint32_t n_nodes, uint32_t root, int depth, uint32_t capacity,
+                              och_editor **out)
+{
+    if (!out || (n_nodes && !nodes) || depth < 1 || depth > 16 || capacity == 0 || capacity > (1u << 28))
+        return OCH_E_INVALID;
+    *out = nullptr;
+    och_editor *e = new (std::nothrow) och_editor;
+    if (!e) return OCH_E_NOMEM;
+    try {
+        e->depth = depth;
+        e->capacity = capacity;
+        e->nodes.assign((size_t)capacity * 8, 0u);
+        e->refs.assign((size_t)capacity + 1, 0u);
+        e->level.assign((size_t)capacity + 1, 0);
+        e->index.reserve(capacity);
+    } catch (const std::bad_alloc &) {
+        delete e;
+        return OCH_E_NOMEM;
+    }
+    if (root) {
+        std::unordered_map<uint64_t, uint32_t> memo;
+        const int st = e->adopt(nodes, n_nodes, root, depth - 1, memo, &e->root);
+        if (st != OCH_OK) {
+            delete e;
+            return st;
+        }
+        ++e->refs[e->root];
+    }
+    e->root_dirty = true;
+    *out = e;
+    return OCH_OK;
+}
+
+OCH_API int och_editor_destroy(och_editor *e)
+{
+    delete e;
+    return OCH_OK;
+}
+
+OCH_API int och_editor_set(och_editor *e, int xi, int yi, int zi, uint32_t v)
+{
+    if (!e) return OCH_E_INVALID;
+    const int dim = 1 << e->depth;
+    if (xi < 0 || yi < 0 || zi < 0 || xi >= dim || yi >= dim || zi >= dim) return OCH_OK;   // :180 ignores
+    if (e->headroom() < (uint32_t)e->depth) return OCH_E_CAPACITY;
+    uint32_t path[32];
+    uint32_t cur = e->root;
+    for (int l = e->depth - 1; l >= 0; --l) {
+        path[l] = cur;
+        cur = cur ? e->slot(cur)[child_of(xi, yi, zi, l)] : 0;
+    }
+    if (cur == v) return OCH_OK;   // unchanged voxel: the path re-registers to itself
+    uint32_t child = v;
+    for (int l = 0; l < e->depth; ++l) {
+        uint32_t n[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        if (path[l]) std::memcpy(n, e->slot(path[l]), 32);
+        n[child_of(xi, yi, zi, l)] = child;
+        bool zero = true;
+        for (int c = 0; c < 8; ++c) zero &= n[c] == 0;
+        child = zero ? 0 : e->intern(n, l);
+    }
+    if (child) ++e->refs[child];
+    if (e->root) e->release(e->root);
+    e->root = child;
+    e->root_dirty = true;
+    return OCH_OK;
+}
+
+OCH_API uint32_t och_editor_at(const och_editor *e, int x, int y, int z)
+{
+    if (!e || !e->root) return 0;
+    uint32_t cur = e->root;
+    for (int l = e->depth - 1; l >= 0; --l) {
+        const uint32_t nx = e->slot(cur)[child_of(x, y, z, l)];
+        if (l == 0 || !nx) return nx;
+        cur = nx;
+    }
+    return 0;
+}
+
+OCH_API int och_editor_info(const och_editor *e, och_editor_stats *info)
+{
+    if (!e || !info) return OCH_E_INVALID;
+    info->capacity = e->capacity;
+    info->live_nodes = e->live;
+    info->high_water = e->next_unused - 1;
+    info->root = e->root;
+    info->depth = e->depth;
+    info->dirty_first = e->dirty_hi ? e->dirty_lo : 0;
+    info->dirty_count = e->dirty_hi ? e->dirty_hi - e->dirty_lo + 1 : 0;
+    return OCH_OK;
+}
+
+OCH_API int och_editor_nodes(const och_editor *e, const uint32_t **nodes, uint32_t *n_slots, uint32_t *root)
+{
+    if (!e || !nodes || !n_slots || !root) return OCH_E_INVALID;
+    *nodes = e->nodes.data();
+    *n_slots = e->capacity;
+    *root = e->root;
+    return OCH_OK;
+}
+
+OCH_API int och_editor_flush(och_editor *e, och_gpu_pool *pool)
+{
+    if (!e || !pool) return OCH_E_INVALID;
+    och_pool_info pi;
+    int st = och_gpu_pool_info(pool, &pi);
+    if (st != OCH_OK) return st;
+    if (pi.index_base != 1 || pi.depth != e->depth || pi.n_nodes != e->capacity + 1) return OCH_E_INVALID;
+    if (!e->dirty_hi && !e->root_dirty) return OCH_OK;
+    const uint32_t first = e->dirty_hi ? e->dirty_lo : 1;
+    const uint32_t count = e->dirty_hi ? e->dirty_hi - e->dirty_lo + 1 : 0;
+    st = och_gpu_pool_update(pool, first, count, count ? e->slot(first) : nullptr, e->root);
+    if (st != OCH_OK) return st;
+    e->dirty_lo = UINT32_MAX;
+    e->dirty_hi = 0;
+    e->root_dirty = false;
+    return OCH_OK;
+}
+
+}  // extern "C"
