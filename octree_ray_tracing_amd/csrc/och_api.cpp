@@ -145,6 +145,7 @@ struct och_gpu_pool {
     uint32_t *d_packed = nullptr;
     uint32_t packed_root = 0;
     uint32_t packed_nodes = 0;
+    bool packed_by_slot = false;    // d_packed numbered like d_nodes (editor flushes)
     int opt_layout = 1;
     int opt_tile_order = 0;
     int opt_bounce_compact = 1;
@@ -313,6 +314,7 @@ int upload_packed(och_gpu_pool *p, const uint32_t *nodes, uint32_t n_nodes)
     if (p->d_packed) OCH_HIP(hipFree(p->d_packed));
     p->d_packed = nullptr;
     p->packed_nodes = 0;
+    p->packed_by_slot = false;
     if (!pack_pool(nodes, n_nodes, p->root, p->depth, p->index_base, packed, proot)) return OCH_OK;   // raw only
     OCH_HIP(hipMalloc(&p->d_packed, packed.size() * 4));
     OCH_HIP(hipMemcpy(p->d_packed, packed.data(), packed.size() * 4, hipMemcpyHostToDevice));
@@ -484,6 +486,50 @@ OCH_API int och_gpu_pool_update(och_gpu_pool *p, uint32_t first, uint32_t count,
     p->root = root;
     return upload_packed(p, p->mirror.data(), n_user);
 }
+
+}  // extern "C"
+
+int och::pool_write_slots(och_gpu_pool *p, uint32_t first, uint32_t count, const uint32_t *raw,
+                          const uint32_t *packed, uint32_t root, uint32_t packed_root, bool full)
+{
+    if (!p || p->index_base != 1 || (count && !raw)) return fail(OCH_E_INVALID, "bad editor flush");
+    if ((uint64_t)first + count > p->n_nodes || (full && (first != 0 || count != p->n_nodes)))
+        return fail(OCH_E_INVALID, "editor window [%u, +%u) outside the pool", first, count);
+    if (packed && p->n_nodes > kIdLimit) return fail(OCH_E_INVALID, "packed ids exceed 24 bits");
+    DeviceGuard g(p->device);
+    OCH_HIP(hipStreamSynchronize(p->stream()));
+    // mirror and raw device slots: slot 0 is the padding node, never written
+    const uint32_t lo = first ? first : 1;
+    const uint32_t skip = lo - first;
+    if (count > skip) {
+        const size_t n = (size_t)(count - skip) * 8;
+        std::memcpy(p->mirror.data() + (size_t)(lo - 1) * 8, raw + (size_t)skip * 8, n * 4);
+        OCH_HIP(hipMemcpy(p->d_nodes + (size_t)lo * 8, raw + (size_t)skip * 8, n * 4, hipMemcpyHostToDevice));
+    }
+    p->root = root;
+    if (!packed) {
+        if (p->d_packed) OCH_HIP(hipFree(p->d_packed));
+        p->d_packed = nullptr;
+        p->packed_nodes = 0;
+        p->packed_by_slot = false;
+        return OCH_OK;
+    }
+    if (full || !p->d_packed || !p->packed_by_slot) {
+        if (!full) return fail(OCH_E_INVALID, "packed buffer is not in editor numbering");
+        if (p->d_packed) OCH_HIP(hipFree(p->d_packed));
+        p->d_packed = nullptr;
+        p->packed_nodes = 0;
+        OCH_HIP(hipMalloc(&p->d_packed, (size_t)p->n_nodes * 32));
+        p->packed_nodes = p->n_nodes;
+        p->packed_by_slot = true;
+    }
+    if (count)
+        OCH_HIP(hipMemcpy(p->d_packed + (size_t)first * 8, packed, (size_t)count * 32, hipMemcpyHostToDevice));
+    p->packed_root = packed_root;
+    return OCH_OK;
+}
+
+extern "C" {
 
 OCH_API int och_gpu_set_rcp_lut(och_gpu_pool *p, const uint32_t *lut, int log2_entries)
 {

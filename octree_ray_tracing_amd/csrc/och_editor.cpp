@@ -54,6 +54,12 @@ struct och_editor {
     uint32_t next_unused = 1;             // slots >= next_unused were never handed out
     uint32_t live = 0;
     std::vector<uint32_t> nodes;          // capacity x 8, slot s at (s-1)*8
+    // The kernels' packed layout numbered like the slots ((capacity+1) x 8, slot
+    // s at s*8, 0 = padding): interior words child | child_mask << 24.  A node
+    // is immutable while it lives, so its word is written once, at intern.
+    std::vector<uint32_t> packed;
+    bool packed_ok = false;               // capacity < 2^24
+    const och_gpu_pool *synced = nullptr; // pool the last flush wrote
     std::vector<uint32_t> refs;           // parent count (+1 for the root)
     std::vector<uint8_t> level;
     std::vector<uint32_t> free_slots;
@@ -68,6 +74,13 @@ struct och_editor {
         if (s < dirty_lo) dirty_lo = s;
         if (s > dirty_hi) dirty_hi = s;
     }
+    uint32_t mask_of(uint32_t s) const
+    {
+        uint32_t m = 0;
+        for (int c = 0; c < 8; ++c) m |= (uint32_t)(slot(s)[c] != 0) << c;
+        return m;
+    }
+    uint32_t packed_root() const { return root ? root | mask_of(root) << 24 : 0; }
     uint32_t headroom() const { return (uint32_t)free_slots.size() + (capacity + 1 - next_unused); }
 
     // register_node (:110-160): find the node or give it a slot; a new node
@@ -87,6 +100,9 @@ struct och_editor {
             s = next_unused++;
         }
         std::memcpy(slot(s), n, 32);
+        if (packed_ok)
+            for (int c = 0; c < 8; ++c)
+                packed[(size_t)s * 8 + c] = lvl > 0 && n[c] ? n[c] | mask_of(n[c]) << 24 : n[c];
         refs[s] = 0;
         level[s] = (uint8_t)lvl;
         index.emplace(k, s);
@@ -111,6 +127,7 @@ struct och_editor {
         uint32_t n[8];
         std::memcpy(n, slot(s), 32);
         std::memset(slot(s), 0, 32);
+        if (packed_ok) std::memset(packed.data() + (size_t)s * 8, 0, 32);
         free_slots.push_back(s);
         --live;
         mark(s);
@@ -161,6 +178,8 @@ OCH_API int och_editor_create(const uint32_t *nodes, uint32_t n_nodes, uint32_t 
         e->depth = depth;
         e->capacity = capacity;
         e->nodes.assign((size_t)capacity * 8, 0u);
+        e->packed_ok = capacity < (1u << 24);
+        if (e->packed_ok) e->packed.assign((size_t)(capacity + 1) * 8, 0u);
         e->refs.assign((size_t)capacity + 1, 0u);
         e->level.assign((size_t)capacity + 1, 0);
         e->index.reserve(capacity);
@@ -258,11 +277,23 @@ OCH_API int och_editor_flush(och_editor *e, och_gpu_pool *pool)
     int st = och_gpu_pool_info(pool, &pi);
     if (st != OCH_OK) return st;
     if (pi.index_base != 1 || pi.depth != e->depth || pi.n_nodes != e->capacity + 1) return OCH_E_INVALID;
-    if (!e->dirty_hi && !e->root_dirty) return OCH_OK;
-    const uint32_t first = e->dirty_hi ? e->dirty_lo : 1;
-    const uint32_t count = e->dirty_hi ? e->dirty_hi - e->dirty_lo + 1 : 0;
-    st = och_gpu_pool_update(pool, first, count, count ? e->slot(first) : nullptr, e->root);
-    if (st != OCH_OK) return st;
+    const uint32_t *pk = e->packed_ok ? e->packed.data() : nullptr;
+    if (e->synced != pool) {
+        // first flush to this pool: both layouts whole, packed in slot numbering
+        std::vector<uint32_t> raw((size_t)(e->capacity + 1) * 8, 0u);
+        std::memcpy(raw.data() + 8, e->nodes.data(), e->nodes.size() * 4);
+        st = och::pool_write_slots(pool, 0, e->capacity + 1, raw.data(), pk, e->root, e->packed_root(), true);
+    } else if (e->dirty_hi || e->root_dirty) {
+        const uint32_t first = e->dirty_hi ? e->dirty_lo : 1;
+        const uint32_t count = e->dirty_hi ? e->dirty_hi - e->dirty_lo + 1 : 0;
+        st = och::pool_write_slots(pool, first, count, count ? e->slot(first) : nullptr,
+                                   pk ? pk + (size_t)first * 8 : nullptr, e->root, e->packed_root(), false);
+    }
+    if (st != OCH_OK) {
+        e->synced = nullptr;   // the next flush rewrites the pool whole
+        return st;
+    }
+    e->synced = pool;
     e->dirty_lo = UINT32_MAX;
     e->dirty_hi = 0;
     e->root_dirty = false;

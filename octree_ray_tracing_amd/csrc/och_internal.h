@@ -29,6 +29,15 @@ struct DevPool {
     float half_voxel;       // voxel_dim / 2 = 2^-(depth+1) (ORT/och_h_octree.h:28), bounce origins
 };
 
+// The editor's flush (och_editor.cpp): write slots [first, first + count) of a
+// 1-based pool's raw layout and, when `packed` is given, of a packed layout
+// numbered like the raw one (id = slot; the editor keeps one level per slot
+// and ids below 2^24), plus both roots.  `full` replaces the packed buffer
+// (count must then cover slots 0..n_nodes-1 and raw/packed start at slot 0).
+// No re-validation: the editor only writes ids it handed out.
+int pool_write_slots(och_gpu_pool *pool, uint32_t first, uint32_t count, const uint32_t *raw,
+                     const uint32_t *packed, uint32_t root, uint32_t packed_root, bool full);
+
 struct DevFrame {
     och_camera cams[OCH_MAX_VIEWS];   // equal width / height
     int32_t n_views;

@@ -145,3 +145,34 @@ def test_gpu_mirror_after_flushes(ort, O, gpu_device):
             assert_same(gpu_trace_dev(pool, ORIGIN, rays), ref)
     pool.close()
     ed.close()
+
+
+@pytest.mark.gpu
+def test_gpu_mirror_cleared_and_regrown(ort, O, gpu_device):
+    """Root -> 0 (every voxel removed) and back, flushed each time."""
+    from test_gpu_parity import gpu_trace_dev
+    depth = 4
+    T = O.HRef(depth, 12)
+    T.fill_terrain()
+    ed = ort.Editor(T.nodes(), T.root, depth, capacity=1024)
+    pool = ed.make_pool(device=0)
+    rays = O.raygen(0.3, -0.6, 1.25, 64, 36)
+    for x, y, z in _all_voxels(depth):
+        ed.set(x, y, z, 0)
+    ed.flush(pool)
+    assert pool.get_root() == 0
+    for layout in (1, 0):
+        pool.set_option("layout", layout)
+        assert (gpu_trace_dev(pool, ORIGIN, rays)["dir"] == 6).all()
+    R = O.HRef(depth, 12)
+    for x, y, z, v in _edits(5, 200, 0, 16):
+        ed.set(x, y, z, v)
+        R.set(x, y, z, v)
+    ed.flush(pool)
+    ref = O.trace_batch(R.pool(), O.Rcp(None), ORIGIN, rays, want_push=True)
+    for layout in (1, 0):
+        pool.set_option("layout", layout)
+        got = gpu_trace_dev(pool, ORIGIN, rays)
+        assert np.array_equal(got["dir"], ref["dir"]) and np.array_equal(got["voxel"], ref["voxel"])
+        assert np.array_equal(got["t"], ref["t"].view(np.uint32)) and np.array_equal(got["push"], ref["push"])
+    pool.close()
