@@ -289,8 +289,8 @@ OCH_API uint32_t och_pool_at(const uint32_t *nodes, uint32_t root, int depth, in
  * 301-435): h_octree::set / at (ORT/och_h_octree.h:176-258) over a host pool of
  * `capacity` slots (1-based, slot s at nodes[(s-1)*8]) that a device pool of
  * the same size mirrors.  An edit path-copies at most `depth` new nodes into
- * the lowest free slots and frees dead ones; och_editor_flush uploads the
- * window of slots written since the last flush through och_gpu_pool_update.
+ * freed or never-used slots and frees dead ones; och_editor_flush uploads the
+ * runs of slots written since the last flush, raw and packed layouts alike.
  * Traced records equal the reference's after the same edits (slot numbering
  * differs: the reference places nodes by hash, :110-160). */
 typedef struct och_editor och_editor;
@@ -301,8 +301,8 @@ typedef struct och_editor_stats {
     uint32_t high_water;    /* highest slot ever handed out */
     uint32_t root;
     int32_t depth;
-    uint32_t dirty_first;   /* window written since the last flush (count 0 = none) */
-    uint32_t dirty_count;
+    uint32_t dirty_first;   /* lowest slot written since the last flush */
+    uint32_t dirty_count;   /* distinct slots written since the last flush (0 = none) */
 } och_editor_stats;
 
 /* Adopt a 1-based pool (e.g. och_build_terrain's; root 0 = empty tree).
@@ -320,7 +320,9 @@ OCH_API int och_editor_info(const och_editor *editor, och_editor_stats *info);
 /* The slot array (capacity x 8, valid until the next edit) and root: pass
  * them to och_gpu_pool_create to make the mirroring device pool. */
 OCH_API int och_editor_nodes(const och_editor *editor, const uint32_t **nodes, uint32_t *n_slots, uint32_t *root);
-/* Upload the dirty window and the root to a pool made from this editor
+/* Upload the dirty slots and the root to a pool made from this editor (the first
+ * flush to a pool writes it whole, replacing its packed layout with one
+ * numbered like the slots)
  * (index_base 1, same depth, capacity slots). */
 OCH_API int och_editor_flush(och_editor *editor, och_gpu_pool *pool);
 

@@ -20,6 +20,7 @@
 //    tree is left unchanged; the reference exit(0)s mid-edit (:112-116).
 #include "och_internal.h"
 
+#include <algorithm>
 #include <array>
 #include <cstring>
 #include <new>
@@ -64,15 +65,25 @@ struct och_editor {
     std::vector<uint8_t> level;
     std::vector<uint32_t> free_slots;
     std::unordered_map<Key, uint32_t, KeyHash> index;
-    uint32_t dirty_lo = UINT32_MAX, dirty_hi = 0;
+    std::vector<uint32_t> dirty;          // slots written since the last flush (repeats allowed)
     bool root_dirty = false;
 
     uint32_t *slot(uint32_t s) { return nodes.data() + (size_t)(s - 1) * 8; }
     const uint32_t *slot(uint32_t s) const { return nodes.data() + (size_t)(s - 1) * 8; }
-    void mark(uint32_t s)
+    void mark(uint32_t s) { dirty.push_back(s); }
+    // Sorted distinct dirty slots, coalesced into runs [first, last] that skip
+    // gaps of at most kGap clean slots (one copy then beats two).
+    std::vector<std::pair<uint32_t, uint32_t>> dirty_runs()
     {
-        if (s < dirty_lo) dirty_lo = s;
-        if (s > dirty_hi) dirty_hi = s;
+        constexpr uint32_t kGap = 32;
+        std::sort(dirty.begin(), dirty.end());
+        dirty.erase(std::unique(dirty.begin(), dirty.end()), dirty.end());
+        std::vector<std::pair<uint32_t, uint32_t>> runs;
+        for (uint32_t s : dirty) {
+            if (!runs.empty() && s - runs.back().second <= kGap + 1) runs.back().second = s;
+            else runs.emplace_back(s, s);
+        }
+        return runs;
     }
     uint32_t mask_of(uint32_t s) const
     {
@@ -136,6 +147,61 @@ struct och_editor {
                 if (n[c]) release(n[c]);
     }
 
+    // Renumber the live slots breadth-first from the root (levels contiguous,
+    // siblings adjacent): the builder's order, which the traversal's cache
+    // locality depends on.  Adoption hands out slots in post-order.
+    void renumber_breadth_first()
+    {
+        if (!root) return;
+        std::vector<uint32_t> order{root};
+        std::vector<uint32_t> to(capacity + 1, 0);
+        to[root] = 1;
+        for (size_t q = 0; q < order.size(); ++q) {
+            const uint32_t s = order[q];
+            if (level[s] == 0) continue;
+            for (int c = 0; c < 8; ++c) {
+                const uint32_t ch = slot(s)[c];
+                if (ch && !to[ch]) {
+                    to[ch] = (uint32_t)order.size() + 1;
+                    order.push_back(ch);
+                }
+            }
+        }
+        std::vector<uint32_t> nn((size_t)capacity * 8, 0u), nr(capacity + 1, 0u);
+        std::vector<uint8_t> nl(capacity + 1, 0);
+        for (size_t q = 0; q < order.size(); ++q) {
+            const uint32_t s = order[q], d = (uint32_t)q + 1;
+            uint32_t *o = nn.data() + (size_t)q * 8;
+            for (int c = 0; c < 8; ++c) {
+                const uint32_t ch = slot(s)[c];
+                o[c] = level[s] > 0 && ch ? to[ch] : ch;
+            }
+            nr[d] = refs[s];
+            nl[d] = level[s];
+        }
+        nodes.swap(nn);
+        refs.swap(nr);
+        level.swap(nl);
+        index.clear();
+        free_slots.clear();
+        next_unused = (uint32_t)order.size() + 1;
+        live = (uint32_t)order.size();
+        root = 1;
+        if (packed_ok) std::fill(packed.begin(), packed.end(), 0u);
+        for (uint32_t d = 1; d < next_unused; ++d) {
+            Key k;
+            std::memcpy(k.data(), slot(d), 32);
+            k[8] = level[d];
+            index.emplace(k, d);
+            if (packed_ok)
+                for (int c = 0; c < 8; ++c) {
+                    const uint32_t ch = slot(d)[c];
+                    packed[(size_t)d * 8 + c] = level[d] > 0 && ch ? ch | mask_of(ch) << 24 : ch;
+                }
+        }
+        dirty.clear();
+    }
+
     // Copy an input pool in, level by level; memo maps (input id, level) to slots.
     int adopt(const uint32_t *in, uint32_t n_in, uint32_t id, int lvl,
               std::unordered_map<uint64_t, uint32_t> &memo, uint32_t *out)
@@ -195,6 +261,7 @@ OCH_API int och_editor_create(const uint32_t *nodes, uint32_t n_nodes, uint32_t 
             return st;
         }
         ++e->refs[e->root];
+        e->renumber_breadth_first();
     }
     e->root_dirty = true;
     *out = e;
@@ -256,8 +323,11 @@ OCH_API int och_editor_info(const och_editor *e, och_editor_stats *info)
     info->high_water = e->next_unused - 1;
     info->root = e->root;
     info->depth = e->depth;
-    info->dirty_first = e->dirty_hi ? e->dirty_lo : 0;
-    info->dirty_count = e->dirty_hi ? e->dirty_hi - e->dirty_lo + 1 : 0;
+    std::vector<uint32_t> d(e->dirty);
+    std::sort(d.begin(), d.end());
+    d.erase(std::unique(d.begin(), d.end()), d.end());
+    info->dirty_first = d.empty() ? 0 : d.front();
+    info->dirty_count = (uint32_t)d.size();
     return OCH_OK;
 }
 
@@ -283,19 +353,23 @@ OCH_API int och_editor_flush(och_editor *e, och_gpu_pool *pool)
         std::vector<uint32_t> raw((size_t)(e->capacity + 1) * 8, 0u);
         std::memcpy(raw.data() + 8, e->nodes.data(), e->nodes.size() * 4);
         st = och::pool_write_slots(pool, 0, e->capacity + 1, raw.data(), pk, e->root, e->packed_root(), true);
-    } else if (e->dirty_hi || e->root_dirty) {
-        const uint32_t first = e->dirty_hi ? e->dirty_lo : 1;
-        const uint32_t count = e->dirty_hi ? e->dirty_hi - e->dirty_lo + 1 : 0;
-        st = och::pool_write_slots(pool, first, count, count ? e->slot(first) : nullptr,
-                                   pk ? pk + (size_t)first * 8 : nullptr, e->root, e->packed_root(), false);
+    } else if (!e->dirty.empty() || e->root_dirty) {
+        const auto runs = e->dirty_runs();
+        if (runs.empty())
+            st = och::pool_write_slots(pool, 1, 0, nullptr, pk ? pk + 8 : nullptr, e->root, e->packed_root(), false);
+        // synchronous copies on the pool's stream: no launch sees a partial flush
+        for (size_t r = 0; r < runs.size() && st == OCH_OK; ++r) {
+            const uint32_t first = runs[r].first, count = runs[r].second - runs[r].first + 1;
+            st = och::pool_write_slots(pool, first, count, e->slot(first), pk ? pk + (size_t)first * 8 : nullptr,
+                                       e->root, e->packed_root(), false);
+        }
     }
     if (st != OCH_OK) {
         e->synced = nullptr;   // the next flush rewrites the pool whole
         return st;
     }
     e->synced = pool;
-    e->dirty_lo = UINT32_MAX;
-    e->dirty_hi = 0;
+    e->dirty.clear();
     e->root_dirty = false;
     return OCH_OK;
 }

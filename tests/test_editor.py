@@ -116,7 +116,9 @@ def test_adopts_builder_pool(ort, O):
     rng = np.random.default_rng(3)
     for x, y, z in rng.integers(0, 64, (2000, 3)).tolist():
         assert ed.at(x, y, z) == ref.at(x, y, z)
-    assert ed.stats()["live_nodes"] <= tree.nodes.shape[0]
+    # adoption renumbers breadth-first: the builder's canonical pool comes back as is
+    assert ed.root == tree.root and ed.stats()["live_nodes"] == tree.nodes.shape[0]
+    assert np.array_equal(ed.nodes()[:tree.nodes.shape[0]], tree.nodes)
 
 
 @pytest.mark.gpu
