@@ -91,6 +91,50 @@ private:
     och_gpu_pool *pool_ = nullptr;
 };
 
+// h_octree::set / at (ORT/och_h_octree.h:176-258) with a device mirror that is
+// refreshed by uploading only the slots the edits wrote.
+class editor {
+public:
+    editor(const uint32_t *nodes, uint32_t n_nodes, uint32_t root, int depth, uint32_t capacity)
+        : depth_(depth)
+    {
+        const int st = och_editor_create(nodes, n_nodes, root, depth, capacity, &ed_);
+        if (st != OCH_OK) throw error(st, "och_editor_create");
+    }
+    editor(const editor &) = delete;
+    editor &operator=(const editor &) = delete;
+    ~editor() { och_editor_destroy(ed_); }
+
+    void set(int x, int y, int z, uint32_t v)
+    {
+        const int st = och_editor_set(ed_, x, y, z, v);
+        if (st != OCH_OK) throw error(st, "och_editor_set");
+    }
+    uint32_t at(int x, int y, int z) const { return och_editor_at(ed_, x, y, z); }
+    uint32_t get_root() const
+    {
+        och_editor_stats st;
+        och_editor_info(ed_, &st);
+        return st.root;
+    }
+
+    // The device pool that mirrors this editor; refresh it with flush().
+    tree make_tree(int device = -1) const
+    {
+        const uint32_t *words = nullptr;
+        uint32_t slots = 0, root = 0;
+        check(och_editor_nodes(ed_, &words, &slots, &root), "och_editor_nodes");
+        return tree(words, slots, root, depth_, 1, __builtin_inff(), device);
+    }
+    void flush(tree &t) { check(och_editor_flush(ed_, t.handle()), "och_editor_flush"); }
+
+    och_editor *handle() const { return ed_; }
+
+private:
+    och_editor *ed_ = nullptr;
+    int depth_;
+};
+
 // tree_camera's per-frame state (pos :55, dir :53, fov :95).
 struct camera {
     float3 pos{1.5F, 1.5F, 1.5F};

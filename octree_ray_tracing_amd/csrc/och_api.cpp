@@ -489,6 +489,8 @@ OCH_API int och_gpu_pool_update(och_gpu_pool *p, uint32_t first, uint32_t count,
 
 }  // extern "C"
 
+int och::report(int status, const char *msg) { return fail(status, "%s", msg); }
+
 int och::pool_write_slots(och_gpu_pool *p, uint32_t first, uint32_t count, const uint32_t *raw,
                           const uint32_t *packed, uint32_t root, uint32_t packed_root, bool full)
 {

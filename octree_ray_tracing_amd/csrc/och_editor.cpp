@@ -236,10 +236,10 @@ OCH_API int och_editor_create(const uint32_t *nodes, uint32_t n_nodes, uint32_t 
                               och_editor **out)
 {
     if (!out || (n_nodes && !nodes) || depth < 1 || depth > 16 || capacity == 0 || capacity > (1u << 28))
-        return OCH_E_INVALID;
+        return och::report(OCH_E_INVALID, "och_editor_create: bad argument (depth 1..16, capacity 1..2^28)");
     *out = nullptr;
     och_editor *e = new (std::nothrow) och_editor;
-    if (!e) return OCH_E_NOMEM;
+    if (!e) return och::report(OCH_E_NOMEM, "och_editor_create: out of host memory");
     try {
         e->depth = depth;
         e->capacity = capacity;
@@ -251,14 +251,16 @@ OCH_API int och_editor_create(const uint32_t *nodes, uint32_t n_nodes, uint32_t 
         e->index.reserve(capacity);
     } catch (const std::bad_alloc &) {
         delete e;
-        return OCH_E_NOMEM;
+        return och::report(OCH_E_NOMEM, "och_editor_create: out of host memory");
     }
     if (root) {
         std::unordered_map<uint64_t, uint32_t> memo;
         const int st = e->adopt(nodes, n_nodes, root, depth - 1, memo, &e->root);
         if (st != OCH_OK) {
             delete e;
-            return st;
+            return och::report(st, st == OCH_E_CAPACITY ? "och_editor_create: the pool does not fit in capacity slots"
+                                                        : "och_editor_create: a child names a slot outside the pool "
+                                                          "or an empty node");
         }
         ++e->refs[e->root];
         e->renumber_breadth_first();
@@ -279,7 +281,8 @@ OCH_API int och_editor_set(och_editor *e, int xi, int yi, int zi, uint32_t v)
     if (!e) return OCH_E_INVALID;
     const int dim = 1 << e->depth;
     if (xi < 0 || yi < 0 || zi < 0 || xi >= dim || yi >= dim || zi >= dim) return OCH_OK;   // :180 ignores
-    if (e->headroom() < (uint32_t)e->depth) return OCH_E_CAPACITY;
+    if (e->headroom() < (uint32_t)e->depth)
+        return och::report(OCH_E_CAPACITY, "och_editor_set: fewer free slots than depth (tree unchanged)");
     uint32_t path[32];
     uint32_t cur = e->root;
     for (int l = e->depth - 1; l >= 0; --l) {
@@ -346,7 +349,8 @@ OCH_API int och_editor_flush(och_editor *e, och_gpu_pool *pool)
     och_pool_info pi;
     int st = och_gpu_pool_info(pool, &pi);
     if (st != OCH_OK) return st;
-    if (pi.index_base != 1 || pi.depth != e->depth || pi.n_nodes != e->capacity + 1) return OCH_E_INVALID;
+    if (pi.index_base != 1 || pi.depth != e->depth || pi.n_nodes != e->capacity + 1)
+        return och::report(OCH_E_INVALID, "och_editor_flush: the pool was not made from this editor's slots");
     const uint32_t *pk = e->packed_ok ? e->packed.data() : nullptr;
     if (e->synced != pool) {
         // first flush to this pool: both layouts whole, packed in slot numbering

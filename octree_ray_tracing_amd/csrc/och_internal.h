@@ -35,6 +35,9 @@ struct DevPool {
 // and ids below 2^24), plus both roots.  `full` replaces the packed buffer
 // (count must then cover slots 0..n_nodes-1 and raw/packed start at slot 0).
 // No re-validation: the editor only writes ids it handed out.
+// Record `msg` as och_last_error's text and return status.
+int report(int status, const char *msg);
+
 int pool_write_slots(och_gpu_pool *pool, uint32_t first, uint32_t count, const uint32_t *raw,
                      const uint32_t *packed, uint32_t root, uint32_t packed_root, bool full);
 
