@@ -8,7 +8,10 @@ h_octree layout (1-based, root 1) or och::octree layout (0-based, root 0).
 from __future__ import annotations
 
 import ctypes as C
+import struct
+import zlib
 from dataclasses import dataclass, field
+from pathlib import Path
 
 import numpy as np
 
@@ -33,6 +36,49 @@ class NodePool:
     def at(self, x: int, y: int, z: int) -> int:
         """h_octree::at (ORT/och_h_octree.h:239-258)."""
         return call("och_pool_at", self.nodes.ctypes.data, self.root, self.depth, self.index_base, x, y, z)
+
+    # -- linearised node-pool file (SURVEY §8f row 1): a 64-byte header, then the
+    # n x 8 little-endian uint32 slots exactly as och_gpu_pool_create takes them.
+    # The reference rebuilds its world on every start (ORT/test_och_h_octree.cpp:822);
+    # a depth-12 build takes ~30 s even in parallel, a load is one read.
+    _MAGIC = b"OCHPOOL\0"
+    _HEADER = struct.Struct("<8sIiiIQI")   # magic, version, depth, index_base, root, n_nodes, crc32
+    _VERSION = 1
+
+    def save(self, path) -> None:
+        nodes = np.ascontiguousarray(self.nodes, dtype="<u4").reshape(-1, 8)
+        crc = zlib.crc32(memoryview(nodes).cast("B"))
+        head = self._HEADER.pack(self._MAGIC, self._VERSION, self.depth, self.index_base, self.root,
+                                 nodes.shape[0], crc)
+        with open(path, "wb") as f:
+            f.write(head.ljust(64, b"\0"))
+            f.write(memoryview(nodes).cast("B"))
+
+    @classmethod
+    def load(cls, path, mmap: bool = False, verify: bool = True) -> "NodePool":
+        """Read a pool file.  Raises ValueError on a bad magic/version, a size
+        that does not match the header, or (verify=True) a checksum mismatch.
+        mmap=True maps the slots read-only instead of reading them."""
+        path = Path(path)
+        size = path.stat().st_size
+        with open(path, "rb") as f:
+            raw = f.read(64)
+        if len(raw) < 64:
+            raise ValueError(f"{path}: truncated header")
+        magic, ver, depth, base, root, n, crc = cls._HEADER.unpack(raw[:cls._HEADER.size])
+        if magic != cls._MAGIC or ver != cls._VERSION:
+            raise ValueError(f"{path}: not a version-{cls._VERSION} node-pool file")
+        if size != 64 + n * 32:
+            raise ValueError(f"{path}: {size} bytes, header says {n} nodes ({64 + n * 32} bytes)")
+        if not 1 <= depth <= 22 or base not in (0, 1):
+            raise ValueError(f"{path}: depth {depth} / index base {base} out of range")
+        if mmap:
+            nodes = np.memmap(path, dtype="<u4", mode="r", offset=64, shape=(n, 8))
+        else:
+            nodes = np.fromfile(path, dtype="<u4", offset=64, count=n * 8).reshape(n, 8)
+        if verify and zlib.crc32(memoryview(np.ascontiguousarray(nodes)).cast("B")) != crc:
+            raise ValueError(f"{path}: checksum mismatch")
+        return cls(np.asarray(nodes, dtype=np.uint32), root, depth, base)
 
 
 def build_terrain(depth: int, tunnels: bool = True, dedup: bool = True, rand_kind: str = "glibc",

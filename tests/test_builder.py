@@ -101,3 +101,35 @@ def test_bad_params(ort):
         ort.build_terrain(13)
     with pytest.raises(ort.OchError):
         ort.build_terrain(11, dedup=False)
+
+
+def test_pool_file_round_trip_and_corruption(ort, tmp_path):
+    """Linearised node-pool file (NodePool.save / load)."""
+    tree = ort.build_terrain(6)
+    p = tmp_path / "d6.ochpool"
+    tree.save(p)
+    assert p.stat().st_size == 64 + tree.nodes.nbytes
+    for mm in (False, True):
+        back = ort.NodePool.load(p, mmap=mm)
+        assert (back.root, back.depth, back.index_base) == (tree.root, tree.depth, tree.index_base)
+        assert np.array_equal(back.nodes, tree.nodes)
+        assert back.at(10, 20, 5) == tree.at(10, 20, 5)
+    octree = ort.build_terrain(4, dedup=False)
+    octree.save(p)
+    back = ort.NodePool.load(p)
+    assert back.index_base == 0 and np.array_equal(back.nodes, octree.nodes)
+    raw = bytearray(p.read_bytes())
+    raw[70] ^= 1                                  # flip one bit of a slot
+    p.write_bytes(bytes(raw))
+    with pytest.raises(ValueError, match="checksum"):
+        ort.NodePool.load(p)
+    ort.NodePool.load(p, verify=False)
+    p.write_bytes(bytes(raw[:-4]))
+    with pytest.raises(ValueError, match="bytes"):
+        ort.NodePool.load(p)
+    p.write_bytes(b"NOTAPOOL" + bytes(raw[8:]))
+    with pytest.raises(ValueError, match="node-pool"):
+        ort.NodePool.load(p)
+    p.write_bytes(bytes(raw[:10]))
+    with pytest.raises(ValueError, match="truncated"):
+        ort.NodePool.load(p)
