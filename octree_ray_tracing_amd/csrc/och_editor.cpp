@@ -21,25 +21,12 @@
 #include "och_internal.h"
 
 #include <algorithm>
-#include <array>
 #include <cstring>
 #include <new>
 #include <unordered_map>
 #include <vector>
 
 namespace {
-
-using Key = std::array<uint32_t, 9>;   // 8 children + level
-
-struct KeyHash {
-    size_t operator()(const Key &k) const noexcept
-    {
-        uint64_t h = 0xCBF29CE484222325ull;   // FNV-1a over the 36 bytes
-        for (uint32_t w : k)
-            for (int b = 0; b < 4; ++b) h = (h ^ ((w >> (8 * b)) & 0xFF)) * 0x100000001B3ull;
-        return (size_t)h;
-    }
-};
 
 inline int child_of(int x, int y, int z, int level)   // z_encode_16 digit, ORT/och_z_order.cpp
 {
@@ -64,7 +51,13 @@ struct och_editor {
     std::vector<uint32_t> refs;           // parent count (+1 for the root)
     std::vector<uint8_t> level;
     std::vector<uint32_t> free_slots;
-    std::unordered_map<Key, uint32_t, KeyHash> index;
+    // Hash-cons index (the reference's node_hashtable role, :70-83, :110-160):
+    // open addressing over slot ids (0 = empty, kTomb = removed), keyed by the
+    // slot's 8 words + level and compared in place in `nodes`.
+    static constexpr uint32_t kTomb = UINT32_MAX;
+    std::vector<uint32_t> table;
+    size_t table_mask = 0;
+    size_t table_used = 0;                // entries + tombstones
     std::vector<uint32_t> dirty;          // slots written since the last flush (repeats allowed)
     bool root_dirty = false;
 
@@ -92,17 +85,59 @@ struct och_editor {
         return m;
     }
     uint32_t packed_root() const { return root ? root | mask_of(root) << 24 : 0; }
+    static size_t hash_of(const uint32_t *n, int lvl)
+    {
+        uint64_t h = 0x9E3779B97F4A7C15ull * (uint64_t)(lvl + 1);
+        for (int c = 0; c < 8; ++c) {
+            h = (h ^ n[c]) * 0xFF51AFD7ED558CCDull;
+            h ^= h >> 29;
+        }
+        return (size_t)h;
+    }
+    // The slot holding (n, lvl), or 0 with *ins = where to insert it.
+    uint32_t lookup(const uint32_t *n, int lvl, size_t *ins) const
+    {
+        size_t i = hash_of(n, lvl) & table_mask, tomb = SIZE_MAX;
+        for (;; i = (i + 1) & table_mask) {
+            const uint32_t e = table[i];
+            if (e == 0) {
+                *ins = tomb != SIZE_MAX ? tomb : i;
+                return 0;
+            }
+            if (e == kTomb) {
+                if (tomb == SIZE_MAX) tomb = i;
+            } else if (level[e] == lvl && !std::memcmp(slot(e), n, 32)) {
+                return e;
+            }
+        }
+    }
+    void unindex(uint32_t s)              // while the slot still holds its node
+    {
+        size_t i = hash_of(slot(s), level[s]) & table_mask;
+        while (table[i] != s) i = (i + 1) & table_mask;
+        table[i] = kTomb;
+    }
+    // Rebuild without tombstones from the live slots (refs > 0 between edits).
+    void reindex()
+    {
+        std::fill(table.begin(), table.end(), 0u);
+        table_used = 0;
+        for (uint32_t s = 1; s < next_unused; ++s) {
+            if (!refs[s]) continue;
+            size_t ins;
+            lookup(slot(s), level[s], &ins);
+            table[ins] = s;
+            ++table_used;
+        }
+    }
     uint32_t headroom() const { return (uint32_t)free_slots.size() + (capacity + 1 - next_unused); }
 
     // register_node (:110-160): find the node or give it a slot; a new node
     // takes one reference on each of its children.
     uint32_t intern(const uint32_t *n, int lvl)
     {
-        Key k;
-        std::memcpy(k.data(), n, 32);
-        k[8] = (uint32_t)lvl;
-        auto it = index.find(k);
-        if (it != index.end()) return it->second;
+        size_t ins;
+        if (const uint32_t found = lookup(n, lvl, &ins)) return found;
         uint32_t s;
         if (!free_slots.empty()) {
             s = free_slots.back();
@@ -116,7 +151,8 @@ struct och_editor {
                 packed[(size_t)s * 8 + c] = lvl > 0 && n[c] ? n[c] | mask_of(n[c]) << 24 : n[c];
         refs[s] = 0;
         level[s] = (uint8_t)lvl;
-        index.emplace(k, s);
+        if (table[ins] == 0) ++table_used;
+        table[ins] = s;
         ++live;
         mark(s);
         if (lvl > 0)
@@ -130,10 +166,7 @@ struct och_editor {
     void release(uint32_t s)
     {
         if (--refs[s]) return;
-        Key k;
-        std::memcpy(k.data(), slot(s), 32);
-        k[8] = level[s];
-        index.erase(k);
+        unindex(s);
         const int lvl = level[s];
         uint32_t n[8];
         std::memcpy(n, slot(s), 32);
@@ -182,17 +215,13 @@ struct och_editor {
         nodes.swap(nn);
         refs.swap(nr);
         level.swap(nl);
-        index.clear();
         free_slots.clear();
         next_unused = (uint32_t)order.size() + 1;
         live = (uint32_t)order.size();
         root = 1;
+        reindex();
         if (packed_ok) std::fill(packed.begin(), packed.end(), 0u);
         for (uint32_t d = 1; d < next_unused; ++d) {
-            Key k;
-            std::memcpy(k.data(), slot(d), 32);
-            k[8] = level[d];
-            index.emplace(k, d);
             if (packed_ok)
                 for (int c = 0; c < 8; ++c) {
                     const uint32_t ch = slot(d)[c];
@@ -248,7 +277,10 @@ OCH_API int och_editor_create(const uint32_t *nodes, uint32_t n_nodes, uint32_t 
         if (e->packed_ok) e->packed.assign((size_t)(capacity + 1) * 8, 0u);
         e->refs.assign((size_t)capacity + 1, 0u);
         e->level.assign((size_t)capacity + 1, 0);
-        e->index.reserve(capacity);
+        size_t tsize = 64;
+        while (tsize < 2 * (size_t)capacity) tsize <<= 1;
+        e->table.assign(tsize, 0u);
+        e->table_mask = tsize - 1;
     } catch (const std::bad_alloc &) {
         delete e;
         return och::report(OCH_E_NOMEM, "och_editor_create: out of host memory");
@@ -283,6 +315,7 @@ OCH_API int och_editor_set(och_editor *e, int xi, int yi, int zi, uint32_t v)
     if (xi < 0 || yi < 0 || zi < 0 || xi >= dim || yi >= dim || zi >= dim) return OCH_OK;   // :180 ignores
     if (e->headroom() < (uint32_t)e->depth)
         return och::report(OCH_E_CAPACITY, "och_editor_set: fewer free slots than depth (tree unchanged)");
+    if (e->table_used + (size_t)e->depth > (e->table_mask + 1) / 4 * 3) e->reindex();   // tombstones
     uint32_t path[32];
     uint32_t cur = e->root;
     for (int l = e->depth - 1; l >= 0; --l) {

@@ -178,3 +178,21 @@ def test_gpu_mirror_cleared_and_regrown(ort, O, gpu_device):
         assert np.array_equal(got["dir"], ref["dir"]) and np.array_equal(got["voxel"], ref["voxel"])
         assert np.array_equal(got["t"], ref["t"].view(np.uint32)) and np.array_equal(got["push"], ref["push"])
     pool.close()
+
+
+def test_churn_reuses_slots_and_tombstones(ort):
+    """Thousands of place/remove cycles in a small pool: freed slots are
+    reused and the hash index's tombstones are swept (no capacity error)."""
+    depth = 4
+    ed = ort.Editor(np.zeros((0, 8), np.uint32), 0, depth, capacity=3 * depth)
+    ed.set(0, 0, 0, 1)
+    for i in range(3000):
+        x, y, z = i % 16, (i * 7) % 16, (i * 3) % 16
+        if (x, y, z) == (0, 0, 0):
+            continue
+        ed.set(x, y, z, 2)
+        assert ed.at(x, y, z) == 2 and ed.at(0, 0, 0) == 1
+        ed.set(x, y, z, 0)
+        assert ed.at(x, y, z) == 0
+    st = ed.stats()
+    assert st["live_nodes"] == depth and st["high_water"] <= 3 * depth
