@@ -1,36 +1,45 @@
 """bench.py -- primary-ray throughput of the MI355X SVO-DAG ray caster.
 
-Workload (BASELINE.json configs[2] at N=1): the reference's terrain at depth 12
-(4096^3, built in parallel by och_build_terrain), camera at (1.5,1.5,1.5),
-yaw 0.3, fov 1.25.  One step = two frames, pitch 0 and pitch -0.6 (the two
-views every BASELINE config is quoted at), each frame being the reference's
-update_position + update_image (raygen, SVO-DAG traversal, palette shading)
-as one fused gfx950 kernel writing the RGBA8 framebuffer.
-
-N > 1 (weak scaling, configs[3]'s frame at N=4): the frame grows to
-round(1920*sqrt(N)) x round(1080*sqrt(N)) so each rank keeps ~1920x1080 rays;
-rows are dealt in 8-row chunks round-robin over ranks, and every frame ends
-with an RCCL all-gather of the framebuffer slices plus an on-device unshard.
-The node pool is built once on rank 0 and broadcast over RCCL.
+Workloads (BASELINE.json):
+  N = 1  configs[2]: the reference's terrain at depth 12 (4096^3, built in
+         parallel by och_build_terrain), 1920x1080, camera at (1.5,1.5,1.5),
+         yaw 0.3, fov 1.25.
+  N > 1  configs[3]: the same tree, one fixed 3840x2160 frame split over the
+         N ranks (strong scaling; --scaling weak grows the frame with N
+         instead).  Rows are dealt in 8-row chunks round-robin over ranks, and
+         every frame ends with an RCCL all-gather of the slices (1-byte colour
+         codes) plus an on-device shade + unshard.  Rank 0 builds the pool and
+         broadcasts it over RCCL.
+One step = two frames, pitch 0 and pitch -0.6 (the two views every BASELINE
+config is quoted at), each being the reference's update_position +
+update_image (raygen, SVO-DAG traversal, palette shading) as one fused gfx950
+launch for both views, then the exchange.
 
 Steps alternate over --inflight (default 3) HIP streams with their own frame
 buffers, so one step's slowest rays (a few grazing tiles)
 overlap the next step's bulk; every step is rendered in full.  The serial
-frame latency is reported beside it (roofline.kernel_ms_idle_gpu).
+frame latency is reported beside it (roofline.kernel_ms_serial).
 
 value = rays of all frames of all ranks / (max over ranks of the timed wall
-time), timed between barrier + synchronize on both sides.
+time), timed between barrier + synchronize on both sides.  `sustained`
+repeats the measurement over >= --sustain seconds, three times (median).
 
 The same line carries config 5 (BASELINE configs[4]) under "bounce": the same
 frames with one mirrored secondary ray per hit pixel, in-block wavefront
 compaction on, rays = primary + secondary.
+
+The cpu leg (rank 0): the CPU oracle (test infrastructure) is timed on this
+host's cores at N = 1 (`cpu_baseline`), and at every N it checks the frames
+of the last timed step -- primary and config 5 -- pixel for pixel (`parity`).
 """
 from __future__ import annotations
 
 import argparse
+import hashlib
 import json
 import math
 import os
+import statistics
 import sys
 import time
 from pathlib import Path
@@ -41,18 +50,34 @@ ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT))
 
 HBM_PEAK_GBS = 8000.0      # MI355X HBM3E, /opt/skills/guides/MI355X_MICROARCH.md
+# gfx950 VALU issue: a wave64 VALU instruction takes 2 cycles of its SIMD-32
+# (MI355X_MICROARCH.md), 4 SIMDs per CU, 256 CUs, 2.4 GHz peak engine clock.
+VALU_PEAK_GINST_S = 256 * 4 * 2.4 / 2
 PITCHES = (0.0, -0.6)
 YAW, FOV = 0.3, 1.25
 ORIGIN = (1.5, 1.5, 1.5)
+PMC_PATH = ROOT / "profiles" / "pmc_summary.json"
 
 
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def frame_size(n_gpus: int, width: int | None, height: int | None):
+def kernel_source_digest() -> str:
+    """Identity of the kernel code a PMC profile was taken of."""
+    h = hashlib.sha256()
+    for f in ("och_kernels.hip", "och_internal.h", "Makefile"):
+        h.update((ROOT / "octree_ray_tracing_amd" / "csrc" / f).read_bytes())
+    return h.hexdigest()[:16]
+
+
+def frame_size(n_gpus: int, width: int | None, height: int | None, scaling: str):
     if width and height:
         return width, height
+    if n_gpus == 1:
+        return 1920, 1080                                  # configs[2]
+    if scaling == "strong":
+        return 3840, 2160                                  # configs[3]
     s = math.sqrt(n_gpus)
     return int(round(1920 * s)), int(round(1080 * s))
 
@@ -108,13 +133,17 @@ def build_pool_nodes(depth: int, rank: int, world: int, dev):
     return nodes, root, tree_nodes, build_s
 
 
-def cpu_baseline(nodes, root, depth, width, height, budget_s: float = 8.0):
-    """The CPU oracle (a C port of the reference tracer, native RCPPS) on this
-    host, rank 0 only.  `value`: traversal of the two views' camera rays
+def cpu_leg(nodes, root, depth, width, height, frames, bounce_frames, time_it: bool, budget_s: float):
+    """The cpu leg, rank 0: the CPU oracle (a C port of the reference tracer
+    with the host's native RCPPS; test infrastructure, used only here as the
+    baseline and the checker).
+
+    time_it (N = 1): `value` = traversal of the two views' camera rays
     (generated once, outside the timed region) on every allowed thread for
-    about budget_s; `value_1core`: the same two views once on one thread;
-    `value_frame_path`: raygen + trace + numpy shading of two frames, the
-    whole per-frame job as this harness runs it."""
+    about budget_s; `value_1core` = the same two views once on one thread;
+    `value_frame_path` = raygen + trace + numpy shading of both frames.
+    Always: the GPU frames of the last timed step (primary and config 5)
+    against the oracle's, pixel for pixel."""
     from oracle import oracle as O
     import octree_ray_tracing_amd as ort
 
@@ -124,69 +153,75 @@ def cpu_baseline(nodes, root, depth, width, height, budget_s: float = 8.0):
     rcp = O.Rcp(None)
     pal = ort.VoxelData().get_colours()
     origin = np.array(ORIGIN, np.float32)
+    t_ray = time.perf_counter()
     views = [O.raygen(YAW, p, FOV, width, height) for p in PITCHES]
-    rays_done, t_total, frames = 0, 0.0, 0
+    t_ray = time.perf_counter() - t_ray
+    # parity of the bench's own frames (also the frame-path timing)
+    tf = time.perf_counter()
+    refs = [O.trace_batch(pool, rcp, origin, rays, nthreads=threads) for rays in views]
+    want = [O.shade_fast(r["dir"], r["voxel"], pal).reshape(height, width) for r in refs]
+    tf = time.perf_counter() - tf + t_ray
+    parity = {"frames": len(want), "pixels": 0, "mismatches": 0}
+    for v, w in enumerate(want):
+        g = frames[v].view(np.uint32)
+        parity["pixels"] += int(w.size)
+        parity["mismatches"] += int(np.count_nonzero(g != w))
+    if bounce_frames is not None:
+        for v, rays in enumerate(views):
+            r = O.trace_bounce_batch(pool, rcp, origin, rays, nthreads=threads)
+            w = O.shade_bounce(r["dir"], r["voxel"], r["dir2"], pal).reshape(height, width)
+            parity["frames"] += 1
+            parity["pixels"] += int(w.size)
+            parity["mismatches"] += int(np.count_nonzero(bounce_frames[v].view(np.uint32) != w))
+    parity["checked"] = ("last timed step: both views, primary" + (" and config 5" if bounce_frames is not None else "")
+                         + ", GPU RGBA8 frames vs oracle trace + trace_pixel shading, native RCPPS on both sides")
+    if not time_it:
+        return None, parity
+    rays_done, t_total, n = 0, 0.0, 0
     t_end = time.perf_counter() + budget_s
-    while time.perf_counter() < t_end or frames < 2:
-        rays = views[frames % 2]
+    while time.perf_counter() < t_end or n < 2:
+        rays = views[n % 2]
         t0 = time.perf_counter()
         O.trace_batch(pool, rcp, origin, rays, nthreads=threads)
         t_total += time.perf_counter() - t0
         rays_done += rays.shape[0]
-        frames += 1
+        n += 1
     # One core (SURVEY 8d asks for 1 thread and all threads).
     t1 = time.perf_counter()
     for rays in views:
         O.trace_batch(pool, rcp, origin, rays, nthreads=1)
     t1 = time.perf_counter() - t1
-    # The whole frame as this harness runs it (single-threaded raygen, numpy shading).
-    tf = time.perf_counter()
-    for p in PITCHES:
-        r = O.trace_batch(pool, rcp, origin, O.raygen(YAW, p, FOV, width, height), nthreads=threads)
-        O.shade_fast(r["dir"], r["voxel"], pal)
-    tf = time.perf_counter() - tf
     try:
         cpu = next(l.split(":", 1)[1].strip() for l in open("/proc/cpuinfo") if l.startswith("model name"))
     except Exception:
         cpu = "unknown"
     n2 = width * height * len(PITCHES)
-    return {"value": rays_done / t_total / 1e6, "unit": "Mrays/s", "cores": threads, "kind": "port",
-            "sample": f"{frames} traversals of full {width}x{height} camera frames (pitch 0 / -0.6 alternating, "
+    base = {"value": rays_done / t_total / 1e6, "unit": "Mrays/s", "cores": threads, "kind": "port",
+            "sample": f"{n} traversals of full {width}x{height} camera frames (pitch 0 / -0.6 alternating, "
                       f"rays generated untimed), depth {depth}, {threads} threads on {cpu}, {t_total:.1f}s",
             "value_1core": n2 / t1 / 1e6,
             "sample_1core": f"the two views' traversal once on 1 thread, {t1:.1f}s",
             "value_frame_path": n2 / tf / 1e6,
-            "sample_frame_path": f"raygen (1 thread) + traversal ({threads} threads) + numpy shading of the two views, {tf:.2f}s"}
-
-
-# gfx950 VALU issue: a wave64 VALU instruction takes 2 cycles of its SIMD
-# (MI355X_MICROARCH.md), 4 SIMDs per CU, 256 CUs, 2.4 GHz peak engine clock.
-VALU_PEAK_GINST_S = 256 * 4 * 2.4 / 2
-
-
-def valu_roofline(pmc, step_s: float):
-    """The render kernel's real limiter: VALU wave-instructions per launch
-    (rocprofv3 SQ_INSTS_VALU from profiles/pmc_summary.json, the same config)
-    issued per second of the pipelined step, against the chip's issue peak."""
-    if not pmc or "SQ_INSTS_VALU" not in pmc:
-        return None
-    insts = float(pmc["SQ_INSTS_VALU"])
-    ach = insts / step_s / 1e9
-    return {"bound": "valu-issue", "insts_per_launch": int(insts), "insts_per_wave": pmc.get("valu_insts_per_wave"),
-            "achieved": round(ach, 1), "peak": VALU_PEAK_GINST_S, "unit": "G wave-instructions/s",
-            "frac": round(ach / VALU_PEAK_GINST_S, 4),
-            "source": "rocprofv3 --pmc SQ_INSTS_VALU (profiles/pmc_summary.json) / bench ms_per_step"}
+            "sample_frame_path": f"raygen (1 thread) + traversal ({threads} threads) + numpy shading of the two views, "
+                                 f"{tf:.2f}s"}
+    return base, parity
 
 
 def load_pmc(kernel: str, config_key: str):
-    p = ROOT / "profiles" / "pmc_summary.json"
-    if not p.exists():
-        return None
+    """The committed rocprofv3 PMC summary of this configuration, if it was
+    taken of the kernel source in this tree (profiles/pmc_summary.json,
+    written by tools/pmc_summary.py)."""
+    if not PMC_PATH.exists():
+        return None, "no profiles/pmc_summary.json"
     try:
-        d = json.loads(p.read_text())
-        return d.get(config_key, {}).get(kernel)
-    except Exception:
-        return None
+        d = json.loads(PMC_PATH.read_text())
+    except Exception as e:
+        return None, f"unreadable PMC summary: {e}"
+    if d.get("config") != config_key:
+        return None, f"PMC summary is of {d.get('config')}, not {config_key}"
+    if d.get("kernel_source_sha") != kernel_source_digest():
+        return None, "PMC summary was taken of other kernel sources (stale profile)"
+    return d.get("kernels", {}).get(kernel), "profiles/pmc_summary.json"
 
 
 def main():
@@ -197,9 +232,14 @@ def main():
     ap.add_argument("--depth", type=int, default=12)
     ap.add_argument("--width", type=int, default=None)
     ap.add_argument("--height", type=int, default=None)
+    ap.add_argument("--scaling", choices=("strong", "weak"), default="strong",
+                    help="N > 1: strong = configs[3]'s fixed 3840x2160 frame; weak = ~1920x1080 rays per rank")
     ap.add_argument("--row-chunk", type=int, default=8)
-    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-cpu-baseline", action="store_true", help="skip the CPU timing (parity is still checked)")
+    ap.add_argument("--no-parity", action="store_true", help="skip the oracle check of the last step's frames")
     ap.add_argument("--cpu-budget", type=float, default=8.0)
+    ap.add_argument("--sustain", type=float, default=1.0,
+                    help="seconds per sustained-throughput run (three runs, median); 0 = off")
     ap.add_argument("--opt", action="append", default=[], metavar="NAME=VALUE",
                     help="pool launch option (och_gpu_set_option), e.g. tile_order=1")
     ap.add_argument("--no-bounce", action="store_true", help="skip the config-5 (secondary rays) measurement")
@@ -235,7 +275,7 @@ def main():
     import octree_ray_tracing_amd as ort
     from octree_ray_tracing_amd.frame import ShardedFrame, slice_row_map
 
-    W, H = frame_size(world, a.width, a.height)
+    W, H = frame_size(world, a.width, a.height, a.scaling)
     nodes, root, tree_nodes, build_s = build_pool_nodes(a.depth, rank, world, dev)
     pool = ort.HOctree(nodes, root, a.depth, device=local)
     pool.set_palette(ort.VoxelData().get_colours())
@@ -255,7 +295,6 @@ def main():
         with torch.cuda.stream(s_):
             sfs.append(ShardedFrame(pool, W, H, a.row_chunk, n_views=len(PITCHES), indexed=indexed))
     pool.set_stream(stream)
-    sf = sfs[0]
 
     # PUSH counts of this rank's rays (for the algorithmic byte count): trace
     # the rank's own rows once with counting on; not part of the timed region.
@@ -263,17 +302,16 @@ def main():
     push_total, hits_total, rays_rank = 0, 0, 0
     dirs = torch.empty(W * H * 3, dtype=torch.float32, device=dev)
     o_t = torch.tensor(ORIGIN, dtype=torch.float32, device=dev)
+    n_px = W * H
+    hd = torch.empty(n_px, dtype=torch.int32, device=dev)
+    hv = torch.empty(n_px, dtype=torch.int32, device=dev)
+    ht = torch.empty(n_px, dtype=torch.float32, device=dev)
+    hp = torch.empty(n_px, dtype=torch.int32, device=dev)
+    mine = rows[rows >= 0].to(dev).long()
     for cam in cams:
         pool.raygen_dev(cam, dirs)
-        n = W * H
-        hd = torch.empty(n, dtype=torch.int32, device=dev)
-        hv = torch.empty(n, dtype=torch.int32, device=dev)
-        ht = torch.empty(n, dtype=torch.float32, device=dev)
-        hp = torch.empty(n, dtype=torch.int32, device=dev)
         pool.trace_batch_dev(o_t, dirs, hd, hv, ht, hp)
-        mine = rows[rows >= 0].to(dev).long()
-        hp2 = hp.view(H, W)[mine]
-        push_total += int(hp2.sum().item())
+        push_total += int(hp.view(H, W)[mine].sum().item())
         hits_total += int((hd.view(H, W)[mine] < 6).sum().item())
         rays_rank += int(mine.numel()) * W
     # trace-only throughput over resident rays (the och_gpu_trace_batch_dev path), N=1 only
@@ -292,9 +330,9 @@ def main():
                 tms.append((s0, s1))
         torch.cuda.synchronize()
         ms = np.array([x.elapsed_time(y) for x, y in tms])
-        trace_only = {"mrays_s": W * H * len(cams) * 10 / ms.sum() / 1e3, "ms_per_frame": float(ms.mean()),
-                      "bytes_per_ray": 12 + 12 + 4 * push_total / (W * H * len(cams))}
-        del hd, hv, ht, hp
+        trace_only = {"mrays_s": n_px * len(cams) * 10 / ms.sum() / 1e3, "ms_per_frame": float(ms.mean()),
+                      "bytes_per_ray": 12 + 12 + 4 * push_total / (n_px * len(cams))}
+    del hd, hv, ht, hp, dirs
 
     def step(k, ev=None, bounce=False):
         """One step: render both views of this rank's rows, all-gather, unshard --
@@ -311,62 +349,69 @@ def main():
                 ev.append((e0, e1))
             f_.exchange()
 
+    def timed(n, bounce=False, ev=None):
+        """n steps between barrier + synchronize; max over ranks of the wall time."""
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for k in range(n):
+            step(k, ev, bounce)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
+        if world > 1:
+            coll(dist.all_reduce, el, op=dist.ReduceOp.MAX)
+        return float(el.item())
+
     # Frame latency: the render launch alone on an otherwise idle GPU.
     lat = []
     for k in range(max(a.warmup, 1) + 5):
         step(0, lat if k >= max(a.warmup, 1) else None)
         torch.cuda.synchronize()
     latency_ms = float(np.median([x.elapsed_time(y) for x, y in lat]))
-    # warmup
+    # warmup, then the timed steps
     for k in range(a.warmup):
         step(k)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
     ev = []
-    t0 = time.perf_counter()
-    for k in range(a.steps):
-        step(k, ev)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
+    elapsed = timed(a.steps, ev=ev)
+    last = (a.steps - 1) % len(sfs)
+    frames_host = sfs[last].frames.cpu().numpy() if rank == 0 else None
     pool.set_stream(stream)
     kms = np.array([x.elapsed_time(y) for x, y in ev])
-    t_max = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-    if world > 1:
-        coll(dist.all_reduce, t_max, op=dist.ReduceOp.MAX)
-    elapsed = float(t_max.item())
+    frames = a.steps * len(cams)
+    total_rays = W * H * frames
+    value = total_rays / elapsed / 1e6
+
+    # Sustained: >= a.sustain seconds of steps, three runs, median.
+    sustained = None
+    if a.sustain > 0:
+        n_s = max(a.steps, int(math.ceil(a.sustain / (elapsed / a.steps))))
+        runs = [timed(n_s) for _ in range(3)]
+        vals = [W * H * len(cams) * n_s / r / 1e6 for r in runs]
+        sustained = {"value": round(statistics.median(vals), 2), "unit": "Mrays/s", "steps_per_run": n_s,
+                     "runs_s": [round(r, 4) for r in runs], "values": [round(v, 2) for v in vals]}
 
     # Config 5 (BASELINE configs[4]): the same frames with one mirrored
     # secondary ray per hit pixel, in-block wavefront compaction on; same
     # pipelining and timing discipline.  Rays = primary + secondary.
     bounce = None
+    bounce_host = None
     if not a.no_bounce:
-        def timed_steps(n, bounce_on=True):
+        def bounce_run(n):
             for k in range(2):
-                step(k, None, bounce_on)
-            torch.cuda.synchronize()
-            if world > 1:
-                dist.barrier()
-            torch.cuda.synchronize()
+                step(k, None, True)
             bev = []
-            tb = time.perf_counter()
-            for k in range(n):
-                step(k, bev, bounce_on)
-            torch.cuda.synchronize()
-            if world > 1:
-                dist.barrier()
-            torch.cuda.synchronize()
-            el = torch.tensor([time.perf_counter() - tb], dtype=torch.float64, device=dev)
-            if world > 1:
-                coll(dist.all_reduce, el, op=dist.ReduceOp.MAX)
-            return float(el.item()), float(np.mean([x.elapsed_time(y) for x, y in bev]))
-        b_el, b_kms = timed_steps(a.steps)
+            el = timed(n, bounce=True, ev=bev)
+            return el, float(np.mean([x.elapsed_time(y) for x, y in bev]))
+        b_el, b_kms = bounce_run(a.steps)
+        if rank == 0:
+            bounce_host = sfs[(a.steps - 1) % len(sfs)].frames.cpu().numpy()
         pool.set_option("bounce_compact", 0)
-        nc_el, nc_kms = timed_steps(max(a.steps // 2, 3))
+        nc_el, nc_kms = bounce_run(max(a.steps // 2, 3))
         pool.set_option("bounce_compact", 1)
         pool.set_stream(stream)
         hits = torch.tensor([hits_total], dtype=torch.int64, device=dev)
@@ -375,7 +420,7 @@ def main():
         secondary = int(hits.item())
         primary = W * H * len(cams)
         bounce = {"workload": "configs[4]: depth-12, primary + 1-bounce secondary rays (divergent), "
-                              "wavefront compaction on" + ("" if world == 1 else f", {world} GPUs"),
+                              "wavefront compaction on" + ("" if world == 1 else f", {W}x{H} over {world} GPUs"),
                   "value": round((primary + secondary) * a.steps / b_el / 1e6, 2), "unit": "Mrays/s",
                   "primary_mrays_s": round(primary * a.steps / b_el / 1e6, 2),
                   "ms_per_step": round(b_el / a.steps * 1e3, 4), "secondary_rays_per_step": secondary,
@@ -383,25 +428,54 @@ def main():
                   "compaction_off_ms_per_step": round(nc_el / max(a.steps // 2, 3) * 1e3, 4),
                   "compaction_off_kernel_ms": round(nc_kms, 4)}
 
-    frames = a.steps * len(cams)
-    total_rays = W * H * frames
-    value = total_rays / elapsed / 1e6
-    # Algorithmic bytes of the dominant kernel (the render launch, both views)
-    # on this rank: the pixel store per ray (1 B code, or 4 B RGBA8 + a 4 B
-    # palette read per hit ray) + 4 B per child-slot read (PUSH).
-    if indexed:
-        bytes_per_launch = 1 * rays_rank + 4 * push_total
-    else:
-        bytes_per_launch = 4 * rays_rank + 4 * push_total + 4 * hits_total
+    # Roofline of the dominant kernel (the render launch, both views, this
+    # rank's rows).  Binding limit: VALU issue -- VALU
+    # wave-instructions per launch (rocprofv3 SQ_INSTS_VALU, the committed
+    # profile of this configuration and kernel source) per second of the
+    # pipelined step, against the chip's issue peak.  HBM: SURVEY §8(d)'s
+    # canonical algorithmic bytes, 24 B in + 12 B out + 4 B per PUSH per ray.
+    step_s = elapsed / a.steps
     k_avg_ms = float(kms.mean())
-    achieved = bytes_per_launch / (k_avg_ms * 1e-3) / 1e9
-    pmc = load_pmc("k_render", f"d{a.depth}_{W}x{H}_n{world}")
+    canon_bytes = 36 * rays_rank + 4 * push_total
+    hbm = {"bound": "hbm", "bytes_per_launch": int(canon_bytes),
+           "bytes_model": "SURVEY 8(d) canonical: 24 B ray in + 12 B hit record out + 4 B per PUSH, per ray",
+           "achieved": round(canon_bytes / (k_avg_ms * 1e-3) / 1e9, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+           "frac": round(canon_bytes / (k_avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 5),
+           "achieved_per_step": round(canon_bytes / step_s / 1e9, 2),
+           "frac_per_step": round(canon_bytes / step_s / 1e9 / HBM_PEAK_GBS, 5)}
+    pmc, pmc_src = load_pmc("k_render", f"d{a.depth}_{W}x{H}_n{world}")
+    roof = {"kernel": f"k_trace_grid<CameraSource,{'CodeSink' if indexed else 'FrameSink'}> (2 views per launch)",
+            "kernel_ms": round(k_avg_ms, 4), "kernel_ms_serial": round(latency_ms, 4),
+            "ms_per_step": round(step_s * 1e3, 4), "frames_in_flight": len(streams),
+            "push_per_ray": round(push_total / rays_rank, 3), "rays_per_launch": rays_rank,
+            "traffic": None if pmc is None else pmc.get("hbm_bytes_per_launch"),
+            "traffic_note": "PMC 2*FETCH_SIZE + WRITE_SIZE per render launch (MI355X_MICROARCH.md HBM): bytes "
+                            "leaving L2, Infinity-Cache hits included", "pmc_source": pmc_src, "hbm": hbm}
+    if pmc and "SQ_INSTS_VALU" in pmc:
+        insts = float(pmc["SQ_INSTS_VALU"])
+        ach = insts / step_s / 1e9
+        roof.update({"bound": "valu-issue", "achieved": round(ach, 1), "peak": VALU_PEAK_GINST_S,
+                     "unit": "G VALU wave-instructions/s", "frac": round(ach / VALU_PEAK_GINST_S, 4),
+                     "valu_insts_per_launch": int(insts), "valu_insts_per_wave": pmc.get("valu_insts_per_wave"),
+                     "achieved_per_launch": round(insts / (k_avg_ms * 1e-3) / 1e9, 1),
+                     "note": "issue rate over the pipelined step (frames overlap, so per-launch durations overlap "
+                             "too); the DAG is L2/MALL-resident, so HBM is far from binding (see hbm)"})
+    else:
+        roof.update({k: hbm[k] for k in ("bound", "achieved", "peak", "unit", "frac")})
 
-    cpu = None
-    if rank == 0 and world == 1 and not a.no_cpu_baseline:
-        cpu = cpu_baseline(nodes, root, a.depth, W, H, a.cpu_budget)
+    cpu, parity = None, None
+    if rank == 0 and not a.no_parity:
+        cpu, parity = cpu_leg(nodes, root, a.depth, W, H, frames_host, bounce_host,
+                              time_it=world == 1 and not a.no_cpu_baseline, budget_s=a.cpu_budget)
 
     if rank == 0:
+        if world == 1:
+            workload = "configs[2]: 4096^3 depth-12 och_h_octree DAG, 1920x1080 primary rays, 1 MI355X"
+        elif a.scaling == "strong" and (W, H) == (3840, 2160):
+            workload = (f"configs[3]: 4096^3 depth-12, 3840x2160 primary rays tiled across {world} MI355X "
+                        "with RCCL framebuffer all-gather")
+        else:
+            workload = f"depth-12 DAG, {W}x{H} frame row-sharded over {world} MI355X + RCCL all-gather"
         line = {
             "metric": "Mrays/sec primary traversal (depth-12 SVO-DAG, raygen+trace+shade per frame)",
             "value": round(value, 2),
@@ -409,15 +483,13 @@ def main():
             "n_gpus": world,
             "steps": a.steps,
             "warmup": a.warmup,
-            "ms_per_step": round(elapsed / a.steps * 1e3, 4),
+            "ms_per_step": round(step_s * 1e3, 4),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "weak" if (world > 1 and a.scaling == "weak") else "strong",
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic: reference terrain fill (simplex heightmap + tunnels) at depth 12, built on the host",
-            "config": {"workload": "configs[2]: 4096^3 depth-12 och_h_octree DAG, 1920x1080 primary rays, 1 MI355X"
-                                   if world == 1 else
-                                   f"configs[3]-style: depth-12 DAG, {W}x{H} frame row-sharded over {world} MI355X + RCCL all-gather",
+            "config": {"workload": workload,
                        "depth": a.depth, "width": W, "height": H, "frames_per_step": len(cams),
                        "pitches": list(PITCHES), "yaw": YAW, "fov": FOV, "row_chunk": a.row_chunk,
                        "dag_nodes": int(nodes.shape[0]), "tree_nodes": tree_nodes,
@@ -425,17 +497,10 @@ def main():
                        "parallelism": f"rows{world}",
                        "frames": "indexed-colour codes, shaded after the exchange" if indexed else "rgba8",
                        "options": {k: pool.get_option(k) for k in pool.OPTIONS}},
-            "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 5),
-                         "traffic": None if pmc is None else pmc.get("hbm_bytes_per_launch"),
-                         "kernel": f"k_trace_grid<CameraSource,{'CodeSink' if indexed else 'FrameSink'}> (2 views per launch)",
-                         "kernel_ms": round(k_avg_ms, 4),
-                         "kernel_ms_idle_gpu": round(latency_ms, 4), "frames_in_flight": len(streams),
-                         "bytes_per_launch": int(bytes_per_launch),
-                         "push_per_ray": round(push_total / rays_rank, 3),
-                         "valu": valu_roofline(pmc, elapsed / a.steps),
-                         "note": "pointer-chase over an L2/MALL-resident DAG: latency/VALU-bound, not HBM-bound"},
+            "roofline": roof,
             "cpu_baseline": cpu,
+            "parity": parity,
+            "sustained": sustained,
             "trace_batch": trace_only,
             "bounce": bounce,
         }

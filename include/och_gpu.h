@@ -139,17 +139,21 @@ OCH_API int och_gpu_set_stream(och_gpu_pool *pool, void *hip_stream);
 OCH_API int och_gpu_synchronize(och_gpu_pool *pool);
 /* Launch schedule of trace/render kernels. */
 typedef enum och_option {
-    OCH_OPT_SCHEDULE = 0,      /* 0 = grid (one ray per thread), 1 = persistent waves with lane refill */
+    OCH_OPT_SCHEDULE = 0,      /* 0 = grid (one ray per thread), 1 = persistent waves with lane refill,
+                                  2 = grid with lane refill: each wave walks a chunk of OCH_OPT_CHUNK_TILES
+                                  64-ray tiles and refills its idle lanes (ballot + popcount) whenever at
+                                  least OCH_OPT_REFILL of them have finished */
     OCH_OPT_BLOCK = 1,         /* threads per workgroup: 64..1024, multiple of 64 (default 256) */
     OCH_OPT_WAVES_PER_CU = 2,  /* persistent: resident waves per compute unit (default 32) */
-    OCH_OPT_REFILL = 3,        /* persistent: refill a wave once this many of its lanes are idle (1..64) */
+    OCH_OPT_REFILL = 3,        /* schedules 1, 2: refill a wave once this many of its lanes are idle (1..64) */
     OCH_OPT_LAYOUT = 4,        /* 0 = the caller's node layout; 1 = packed (default when the DAG has < 2^24
                                   (node, level) pairs): per-level breadth-first ids, interior slots carry the
                                   child's occupancy mask so only descents and hits touch memory */
     OCH_OPT_TILE_ORDER = 5,    /* camera rays (render): 0 = 8x8-pixel tiles row-major; 1 = 64x64-pixel supertiles,
                                   each handed to one XCD so neighbouring rays share that XCD's L2 */
-    OCH_OPT_BOUNCE_COMPACT = 6 /* config 5: 1 (default) = compact each block's secondary rays into its first lanes
+    OCH_OPT_BOUNCE_COMPACT = 6,/* config 5: 1 (default) = compact each block's secondary rays into its first lanes
                                   (wave ballot/popcount + LDS queue) before tracing them; 0 = trace in place */
+    OCH_OPT_CHUNK_TILES = 7    /* schedule 2: 64-ray tiles per wave, a power of two in 1..64 (default 4) */
 } och_option;
 OCH_API int och_gpu_set_option(och_gpu_pool *pool, int option, int value);
 OCH_API int och_gpu_get_option(const och_gpu_pool *pool, int option, int *value);
@@ -320,10 +324,15 @@ OCH_API int och_editor_info(const och_editor *editor, och_editor_stats *info);
 /* The slot array (capacity x 8, valid until the next edit) and root: pass
  * them to och_gpu_pool_create to make the mirroring device pool. */
 OCH_API int och_editor_nodes(const och_editor *editor, const uint32_t **nodes, uint32_t *n_slots, uint32_t *root);
-/* Upload the dirty slots and the root to a pool made from this editor (the first
- * flush to a pool writes it whole, replacing its packed layout with one
- * numbered like the slots)
- * (index_base 1, same depth, capacity slots). */
+/* Upload the dirty slots, then the root, to a pool made from this editor
+ * (index_base 1, same depth, capacity slots).  Slots are rewritten in place,
+ * so the flush first waits for ALL work on the pool's device (every stream).
+ * Only a pool this editor's last flush wrote, untouched since, gets the
+ * windowed upload; any other pool (a new one, one another editor or
+ * och_gpu_pool_update wrote, or one a failed flush left behind) is written
+ * whole, its packed layout replaced by one numbered like the slots.  The root
+ * is published after every slot it reaches, so a failed flush leaves the pool
+ * tracing its previous tree. */
 OCH_API int och_editor_flush(och_editor *editor, och_gpu_pool *pool);
 
 #ifdef __cplusplus

@@ -41,15 +41,24 @@ class NodePool:
     # n x 8 little-endian uint32 slots exactly as och_gpu_pool_create takes them.
     # The reference rebuilds its world on every start (ORT/test_och_h_octree.cpp:822);
     # a depth-12 build takes ~30 s even in parallel, a load is one read.
+    # Version 2: the CRC-32 covers the header fields (depth, index base, root,
+    # node count) and then the slots; version-1 files (slots only) still load.
     _MAGIC = b"OCHPOOL\0"
     _HEADER = struct.Struct("<8sIiiIQI")   # magic, version, depth, index_base, root, n_nodes, crc32
-    _VERSION = 1
+    _VERSION = 2
+
+    @classmethod
+    def _crc(cls, version, depth, base, root, n, slots) -> int:
+        crc = 0
+        if version >= 2:
+            crc = zlib.crc32(struct.pack("<IiiIQ", version, depth, base, root, n))
+        return zlib.crc32(slots, crc)
 
     def save(self, path) -> None:
         nodes = np.ascontiguousarray(self.nodes, dtype="<u4").reshape(-1, 8)
-        crc = zlib.crc32(memoryview(nodes).cast("B"))
-        head = self._HEADER.pack(self._MAGIC, self._VERSION, self.depth, self.index_base, self.root,
-                                 nodes.shape[0], crc)
+        n = nodes.shape[0]
+        crc = self._crc(self._VERSION, self.depth, self.index_base, self.root, n, memoryview(nodes).cast("B"))
+        head = self._HEADER.pack(self._MAGIC, self._VERSION, self.depth, self.index_base, self.root, n, crc)
         with open(path, "wb") as f:
             f.write(head.ljust(64, b"\0"))
             f.write(memoryview(nodes).cast("B"))
@@ -57,8 +66,9 @@ class NodePool:
     @classmethod
     def load(cls, path, mmap: bool = False, verify: bool = True) -> "NodePool":
         """Read a pool file.  Raises ValueError on a bad magic/version, a size
-        that does not match the header, or (verify=True) a checksum mismatch.
-        mmap=True maps the slots read-only instead of reading them."""
+        that does not match the header, a depth / index base / root outside
+        their ranges, or (verify=True) a checksum mismatch.  mmap=True maps the
+        slots read-only instead of reading them."""
         path = Path(path)
         size = path.stat().st_size
         with open(path, "rb") as f:
@@ -66,17 +76,20 @@ class NodePool:
         if len(raw) < 64:
             raise ValueError(f"{path}: truncated header")
         magic, ver, depth, base, root, n, crc = cls._HEADER.unpack(raw[:cls._HEADER.size])
-        if magic != cls._MAGIC or ver != cls._VERSION:
-            raise ValueError(f"{path}: not a version-{cls._VERSION} node-pool file")
+        if magic != cls._MAGIC or ver not in (1, 2):
+            raise ValueError(f"{path}: not a version-1/2 node-pool file")
         if size != 64 + n * 32:
             raise ValueError(f"{path}: {size} bytes, header says {n} nodes ({64 + n * 32} bytes)")
         if not 1 <= depth <= 22 or base not in (0, 1):
             raise ValueError(f"{path}: depth {depth} / index base {base} out of range")
+        # h_octree: root 0 = empty tree, else 1..n; och::octree: root 0 of n >= 1 nodes
+        if (base == 1 and root > n) or (base == 0 and (root != 0 or n == 0)):
+            raise ValueError(f"{path}: root {root} outside a {n}-node pool (index base {base})")
         if mmap:
             nodes = np.memmap(path, dtype="<u4", mode="r", offset=64, shape=(n, 8))
         else:
             nodes = np.fromfile(path, dtype="<u4", offset=64, count=n * 8).reshape(n, 8)
-        if verify and zlib.crc32(memoryview(np.ascontiguousarray(nodes)).cast("B")) != crc:
+        if verify and cls._crc(ver, depth, base, root, n, memoryview(np.ascontiguousarray(nodes)).cast("B")) != crc:
             raise ValueError(f"{path}: checksum mismatch")
         return cls(np.asarray(nodes, dtype=np.uint32), root, depth, base)
 

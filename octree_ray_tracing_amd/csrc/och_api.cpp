@@ -134,7 +134,7 @@ struct och_gpu_pool {
     hipEvent_t ev_start = nullptr, ev_stop = nullptr;
     bool timed = false;
     // schedule (och_gpu_set_option)
-    int opt_schedule = 0, opt_block = 64, opt_waves_per_cu = 32, opt_refill = 16;
+    int opt_schedule = 0, opt_block = 64, opt_waves_per_cu = 32, opt_refill = 16, opt_chunk_tiles = 4;
     int cus = 256;
     uint32_t *d_counter = nullptr;
     uint64_t *stamps = nullptr;
@@ -146,6 +146,8 @@ struct och_gpu_pool {
     uint32_t packed_root = 0;
     uint32_t packed_nodes = 0;
     bool packed_by_slot = false;    // d_packed numbered like d_nodes (editor flushes)
+    uint64_t serial = 0;            // process-unique, never reused (och::pool_serial)
+    uint64_t last_writer = 0;       // editor id of the last och::pool_commit, 0 otherwise
     int opt_layout = 1;
     int opt_tile_order = 0;
     int opt_bounce_compact = 1;
@@ -158,7 +160,8 @@ struct och_gpu_pool {
     och::Schedule schedule() const
     {
         och::Schedule sc;
-        sc.persistent = opt_schedule == 1;
+        sc.kind = opt_schedule;
+        sc.chunk_tiles = opt_chunk_tiles;
         sc.block = opt_block;
         sc.waves_per_cu = opt_waves_per_cu;
         sc.refill_min = opt_refill;
@@ -393,6 +396,8 @@ OCH_API int och_gpu_pool_create(const uint32_t *nodes, uint32_t n_nodes, uint32_
     if (!g.ok) return fail(OCH_E_HIP, "hipSetDevice(%d) failed", device);
 
     och_gpu_pool *p = new och_gpu_pool;
+    static std::atomic<uint64_t> next_serial{1};
+    p->serial = next_serial.fetch_add(1);
     p->device = device;
     p->depth = depth;
     p->index_base = index_base;
@@ -484,6 +489,7 @@ OCH_API int och_gpu_pool_update(och_gpu_pool *p, uint32_t first, uint32_t count,
                                (size_t)count * 32, hipMemcpyHostToDevice, p->stream()));
     OCH_HIP(hipStreamSynchronize(p->stream()));
     p->root = root;
+    p->last_writer = 0;
     return upload_packed(p, p->mirror.data(), n_user);
 }
 
@@ -491,15 +497,31 @@ OCH_API int och_gpu_pool_update(och_gpu_pool *p, uint32_t first, uint32_t count,
 
 int och::report(int status, const char *msg) { return fail(status, "%s", msg); }
 
+uint64_t och::pool_serial(const och_gpu_pool *p) { return p ? p->serial : 0; }
+uint64_t och::pool_last_writer(const och_gpu_pool *p) { return p ? p->last_writer : 0; }
+
+int och::pool_drain(och_gpu_pool *p)
+{
+    if (!p) return fail(OCH_E_INVALID, "pool is NULL");
+    DeviceGuard g(p->device);
+    // Every stream, not just the pool's: bench and frame code rotate the pool
+    // over several streams with frames in flight, and a kernel still walking a
+    // slot that is rewritten in place could read a torn DAG.
+    OCH_HIP(hipDeviceSynchronize());
+    return OCH_OK;
+}
+
 int och::pool_write_slots(och_gpu_pool *p, uint32_t first, uint32_t count, const uint32_t *raw,
-                          const uint32_t *packed, uint32_t root, uint32_t packed_root, bool full)
+                          const uint32_t *packed, bool full)
 {
     if (!p || p->index_base != 1 || (count && !raw)) return fail(OCH_E_INVALID, "bad editor flush");
     if ((uint64_t)first + count > p->n_nodes || (full && (first != 0 || count != p->n_nodes)))
         return fail(OCH_E_INVALID, "editor window [%u, +%u) outside the pool", first, count);
     if (packed && p->n_nodes > kIdLimit) return fail(OCH_E_INVALID, "packed ids exceed 24 bits");
+    if (packed && !full && (!p->d_packed || !p->packed_by_slot))
+        return fail(OCH_E_INVALID, "packed buffer is not in editor numbering");
     DeviceGuard g(p->device);
-    OCH_HIP(hipStreamSynchronize(p->stream()));
+    p->last_writer = 0;                 // until pool_commit: a failed flush forces a full rewrite
     // mirror and raw device slots: slot 0 is the padding node, never written
     const uint32_t lo = first ? first : 1;
     const uint32_t skip = lo - first;
@@ -508,26 +530,36 @@ int och::pool_write_slots(och_gpu_pool *p, uint32_t first, uint32_t count, const
         std::memcpy(p->mirror.data() + (size_t)(lo - 1) * 8, raw + (size_t)skip * 8, n * 4);
         OCH_HIP(hipMemcpy(p->d_nodes + (size_t)lo * 8, raw + (size_t)skip * 8, n * 4, hipMemcpyHostToDevice));
     }
-    p->root = root;
-    if (!packed) {
+    if (!packed) return OCH_OK;
+    if (full && (!p->d_packed || !p->packed_by_slot || p->packed_nodes != p->n_nodes)) {
         if (p->d_packed) OCH_HIP(hipFree(p->d_packed));
         p->d_packed = nullptr;
         p->packed_nodes = 0;
         p->packed_by_slot = false;
-        return OCH_OK;
-    }
-    if (full || !p->d_packed || !p->packed_by_slot) {
-        if (!full) return fail(OCH_E_INVALID, "packed buffer is not in editor numbering");
-        if (p->d_packed) OCH_HIP(hipFree(p->d_packed));
-        p->d_packed = nullptr;
-        p->packed_nodes = 0;
         OCH_HIP(hipMalloc(&p->d_packed, (size_t)p->n_nodes * 32));
         p->packed_nodes = p->n_nodes;
         p->packed_by_slot = true;
     }
     if (count)
         OCH_HIP(hipMemcpy(p->d_packed + (size_t)first * 8, packed, (size_t)count * 32, hipMemcpyHostToDevice));
-    p->packed_root = packed_root;
+    return OCH_OK;
+}
+
+int och::pool_commit(och_gpu_pool *p, uint32_t root, uint32_t packed_root, bool packed, uint64_t writer)
+{
+    if (!p || p->index_base != 1) return fail(OCH_E_INVALID, "bad editor flush");
+    if (packed && (!p->d_packed || !p->packed_by_slot))
+        return fail(OCH_E_INVALID, "packed buffer is not in editor numbering");
+    DeviceGuard g(p->device);
+    if (!packed && p->d_packed) {
+        OCH_HIP(hipFree(p->d_packed));
+        p->d_packed = nullptr;
+        p->packed_nodes = 0;
+        p->packed_by_slot = false;
+    }
+    p->root = root;
+    p->packed_root = packed ? packed_root : 0;
+    p->last_writer = writer;
     return OCH_OK;
 }
 
@@ -583,7 +615,7 @@ OCH_API int och_gpu_set_option(och_gpu_pool *p, int option, int value)
     if (!p) return fail(OCH_E_INVALID, "pool is NULL");
     switch (option) {
     case OCH_OPT_SCHEDULE:
-        if (value != 0 && value != 1) return fail(OCH_E_INVALID, "schedule must be 0 or 1");
+        if (value < 0 || value > 2) return fail(OCH_E_INVALID, "schedule must be 0, 1 or 2");
         p->opt_schedule = value;
         return OCH_OK;
     case OCH_OPT_BLOCK:
@@ -611,6 +643,11 @@ OCH_API int och_gpu_set_option(och_gpu_pool *p, int option, int value)
         if (value != 0 && value != 1) return fail(OCH_E_INVALID, "bounce compaction must be 0 or 1");
         p->opt_bounce_compact = value;
         return OCH_OK;
+    case OCH_OPT_CHUNK_TILES:
+        if (value < 1 || value > 64 || (value & (value - 1)))
+            return fail(OCH_E_INVALID, "chunk tiles %d: a power of two in 1..64", value);
+        p->opt_chunk_tiles = value;
+        return OCH_OK;
     default:
         return fail(OCH_E_INVALID, "unknown option %d", option);
     }
@@ -627,6 +664,7 @@ OCH_API int och_gpu_get_option(const och_gpu_pool *p, int option, int *value)
     case OCH_OPT_LAYOUT: *value = (p->opt_layout == 1 && p->d_packed) ? 1 : 0; return OCH_OK;
     case OCH_OPT_TILE_ORDER: *value = p->opt_tile_order; return OCH_OK;
     case OCH_OPT_BOUNCE_COMPACT: *value = p->opt_bounce_compact; return OCH_OK;
+    case OCH_OPT_CHUNK_TILES: *value = p->opt_chunk_tiles; return OCH_OK;
     default: return fail(OCH_E_INVALID, "unknown option %d", option);
     }
 }

@@ -7,8 +7,8 @@
 // placement follows the FNV hash, so an edit touches slots scattered over the
 // whole 2^L table.  Here a node keeps its slot until it dies, new nodes take
 // the lowest free slots, and every written slot is recorded, so
-// och_editor_flush re-uploads one [first, last] window of dirty slots through
-// och_gpu_pool_update instead of the pool.
+// och_editor_flush re-uploads only the runs of dirty slots (och::pool_write_slots)
+// instead of the pool.
 //
 // Differences from the reference that do not change any traced record (the
 // tracer reads children only, never slot positions or counts):
@@ -21,6 +21,7 @@
 #include "och_internal.h"
 
 #include <algorithm>
+#include <atomic>
 #include <cstring>
 #include <new>
 #include <unordered_map>
@@ -47,7 +48,8 @@ struct och_editor {
     // is immutable while it lives, so its word is written once, at intern.
     std::vector<uint32_t> packed;
     bool packed_ok = false;               // capacity < 2^24
-    const och_gpu_pool *synced = nullptr; // pool the last flush wrote
+    uint64_t id = 0;                      // process-unique editor id (the pools' last_writer)
+    uint64_t synced = 0;                  // och::pool_serial of the pool the last flush wrote
     std::vector<uint32_t> refs;           // parent count (+1 for the root)
     std::vector<uint8_t> level;
     std::vector<uint32_t> free_slots;
@@ -269,6 +271,8 @@ OCH_API int och_editor_create(const uint32_t *nodes, uint32_t n_nodes, uint32_t 
     *out = nullptr;
     och_editor *e = new (std::nothrow) och_editor;
     if (!e) return och::report(OCH_E_NOMEM, "och_editor_create: out of host memory");
+    static std::atomic<uint64_t> next_id{1};
+    e->id = next_id.fetch_add(1);
     try {
         e->depth = depth;
         e->capacity = capacity;
@@ -385,27 +389,32 @@ OCH_API int och_editor_flush(och_editor *e, och_gpu_pool *pool)
     if (pi.index_base != 1 || pi.depth != e->depth || pi.n_nodes != e->capacity + 1)
         return och::report(OCH_E_INVALID, "och_editor_flush: the pool was not made from this editor's slots");
     const uint32_t *pk = e->packed_ok ? e->packed.data() : nullptr;
-    if (e->synced != pool) {
-        // first flush to this pool: both layouts whole, packed in slot numbering
+    // Windowed only when this pool holds exactly what this editor's last flush
+    // wrote: same pool (by serial -- a new pool can reuse a freed address) and
+    // nobody (another editor, och_gpu_pool_update) wrote it since.
+    const bool windowed = e->synced == och::pool_serial(pool) && och::pool_last_writer(pool) == e->id;
+    if (windowed && e->dirty.empty() && !e->root_dirty) return OCH_OK;
+    st = och::pool_drain(pool);
+    if (st == OCH_OK && !windowed) {
+        // both layouts whole, packed in slot numbering
         std::vector<uint32_t> raw((size_t)(e->capacity + 1) * 8, 0u);
         std::memcpy(raw.data() + 8, e->nodes.data(), e->nodes.size() * 4);
-        st = och::pool_write_slots(pool, 0, e->capacity + 1, raw.data(), pk, e->root, e->packed_root(), true);
-    } else if (!e->dirty.empty() || e->root_dirty) {
+        st = och::pool_write_slots(pool, 0, e->capacity + 1, raw.data(), pk, true);
+    } else if (st == OCH_OK) {
         const auto runs = e->dirty_runs();
-        if (runs.empty())
-            st = och::pool_write_slots(pool, 1, 0, nullptr, pk ? pk + 8 : nullptr, e->root, e->packed_root(), false);
-        // synchronous copies on the pool's stream: no launch sees a partial flush
         for (size_t r = 0; r < runs.size() && st == OCH_OK; ++r) {
             const uint32_t first = runs[r].first, count = runs[r].second - runs[r].first + 1;
             st = och::pool_write_slots(pool, first, count, e->slot(first), pk ? pk + (size_t)first * 8 : nullptr,
-                                       e->root, e->packed_root(), false);
+                                       false);
         }
     }
+    // The roots go out last, once every slot they reach is on the device.
+    if (st == OCH_OK) st = och::pool_commit(pool, e->root, e->packed_root(), pk != nullptr, e->id);
     if (st != OCH_OK) {
-        e->synced = nullptr;   // the next flush rewrites the pool whole
+        e->synced = 0;   // the next flush rewrites the pool whole
         return st;
     }
-    e->synced = pool;
+    e->synced = och::pool_serial(pool);
     e->dirty.clear();
     e->root_dirty = false;
     return OCH_OK;

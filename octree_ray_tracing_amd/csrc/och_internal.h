@@ -29,17 +29,32 @@ struct DevPool {
     float half_voxel;       // voxel_dim / 2 = 2^-(depth+1) (ORT/och_h_octree.h:28), bounce origins
 };
 
-// The editor's flush (och_editor.cpp): write slots [first, first + count) of a
-// 1-based pool's raw layout and, when `packed` is given, of a packed layout
-// numbered like the raw one (id = slot; the editor keeps one level per slot
-// and ids below 2^24), plus both roots.  `full` replaces the packed buffer
-// (count must then cover slots 0..n_nodes-1 and raw/packed start at slot 0).
+// The editor's flush (och_editor.cpp) writes a 1-based pool in three steps:
+//   pool_drain       -- waits for all work on the pool's device (kernels on any
+//                       stream may still be walking the slots about to change);
+//   pool_write_slots -- copies slots [first, first + count) of the raw layout
+//                       and, when `packed` is given, of a packed layout
+//                       numbered like the raw one (id = slot; the editor keeps
+//                       one level per slot and ids below 2^24).  `full`
+//                       replaces the packed buffer (count must then cover
+//                       slots 0..n_nodes-1 and raw/packed start at slot 0).
+//                       Roots are not touched, so a failed flush leaves the
+//                       pool tracing its old tree;
+//   pool_commit      -- publishes both roots (packed == false drops the packed
+//                       layout) and records `writer` as the pool's last writer.
 // No re-validation: the editor only writes ids it handed out.
-// Record `msg` as och_last_error's text and return status.
+// pool_serial: a process-unique id of the pool (never reused, unlike its
+// address); pool_last_writer: the editor id of the last commit, 0 after
+// och_gpu_pool_create / och_gpu_pool_update / a failed write.
+// report: record `msg` as och_last_error's text and return status.
 int report(int status, const char *msg);
 
+int pool_drain(och_gpu_pool *pool);
 int pool_write_slots(och_gpu_pool *pool, uint32_t first, uint32_t count, const uint32_t *raw,
-                     const uint32_t *packed, uint32_t root, uint32_t packed_root, bool full);
+                     const uint32_t *packed, bool full);
+int pool_commit(och_gpu_pool *pool, uint32_t root, uint32_t packed_root, bool packed, uint64_t writer);
+uint64_t pool_serial(const och_gpu_pool *pool);
+uint64_t pool_last_writer(const och_gpu_pool *pool);
 
 struct DevFrame {
     och_camera cams[OCH_MAX_VIEWS];   // equal width / height
@@ -53,10 +68,12 @@ struct DevFrame {
 
 // How trace/render launches are scheduled (och_gpu_set_option).
 struct Schedule {
-    bool persistent;        // resident waves pulling rays from *counter, lane refill
+    int kind;               // 0 grid, 1 persistent (resident waves pulling rays from *counter),
+                            // 2 grid with lane refill (each wave walks a chunk of chunk_tiles tiles)
+    int chunk_tiles;        // refill: 8x8 tiles (64 rays each) per wave
     int block;              // threads per workgroup (multiple of 64)
     int waves_per_cu;       // persistent grid size per CU
-    int refill_min;         // refill once this many lanes of a wave are idle
+    int refill_min;         // persistent / refill: refill once this many lanes of a wave are idle
     int tile_order;         // camera rays: 0 row-major 8x8 tiles, 1 supertiles grouped per XCD
     int bounce_compact;     // config 5: compact the block's secondary rays into its first lanes
     int cus;                // compute units of the device

@@ -9,8 +9,10 @@
 // before the unsigned t compare, denormal masks compared as integers.
 // Build with -ffp-contract=off and without denormal flushing.
 //
-// Two schedules share the traversal:
+// Three schedules share the traversal:
 //   grid       -- one ray per thread, the hardware dispatcher balances waves;
+//   refill     -- one wave per chunk of a few tiles; finished lanes take the
+//                 chunk's next rays whenever enough of them are idle;
 //   persistent -- a resident grid of waves pulls rays from a device counter;
 //                 when enough lanes of a wave have finished (ballot +
 //                 popcount), one atomic refills them, so no lane idles while
@@ -307,6 +309,11 @@ struct ArraySource {
     {
         return get(wave_base + lane, o, d, out);
     }
+    // Refill: ray base + k, base wave-uniform, k < 64.
+    __device__ __forceinline__ bool get_refill(uint32_t base, uint32_t k, float *o, float *d, uint32_t &out) const
+    {
+        return get(base + k, o, d, out);
+    }
 };
 
 // tree_camera::update_position per pixel (ORT/test_och_h_octree.cpp:119-136):
@@ -396,6 +403,41 @@ struct CameraSource {
         int row;
         if (row_chunk % (int)kTileH == 0) {                // the tile lies inside one row chunk
             const int chunk = __builtin_amdgcn_readfirstlane(srow0 / row_chunk);
+            row = (chunk * n_shards + shard) * row_chunk + (srow - chunk * row_chunk);
+        } else {
+            const int chunk = srow / row_chunk;
+            row = (chunk * n_shards + shard) * row_chunk + (srow - chunk * row_chunk);
+        }
+        return finish(view, col, srow, row, o, d, out);
+    }
+    // Refill (k_trace_refill): ray base + k, base wave-uniform, k < 64.  The
+    // rays span at most two tiles, A = base / 64 and A + 1, whose coordinates
+    // are wave-uniform (scalar unit); each lane selects its tile.  A chunk of
+    // the refill schedule never crosses a view (per_view is a multiple of the
+    // chunk), so both tiles share the view.
+    __device__ __forceinline__ bool get_refill(uint32_t base, uint32_t k, float *o, float *d, uint32_t &out) const
+    {
+        base = __builtin_amdgcn_readfirstlane(base);
+        uint32_t view, txa, tya, vb, txb, tyb;
+        tile_of(base, view, txa, tya);
+        tile_of(base + 64u, vb, txb, tyb);
+        view = __builtin_amdgcn_readfirstlane(view);
+        txa = __builtin_amdgcn_readfirstlane(txa);
+        tya = __builtin_amdgcn_readfirstlane(tya);
+        txb = __builtin_amdgcn_readfirstlane(txb);
+        tyb = __builtin_amdgcn_readfirstlane(tyb);
+        const uint32_t j = (base & 63u) + k;                  // < 128
+        const bool in_a = j < 64u;
+        const uint32_t pix = j & 63u;
+        const uint32_t tx = in_a ? txa : txb, ty = in_a ? tya : tyb;
+        const int col = (int)(tx * kTileW + pix % kTileW);
+        const int srow = (int)(ty * kTileH + pix / kTileW);
+        if (col >= width || srow >= slice_rows) return false;
+        int row;
+        if (row_chunk % (int)kTileH == 0) {                    // each tile lies inside one row chunk
+            const int ca = __builtin_amdgcn_readfirstlane((int)(tya * kTileH) / row_chunk);
+            const int cb = __builtin_amdgcn_readfirstlane((int)(tyb * kTileH) / row_chunk);
+            const int chunk = in_a ? ca : cb;
             row = (chunk * n_shards + shard) * row_chunk + (srow - chunk * row_chunk);
         } else {
             const int chunk = srow / row_chunk;
@@ -665,6 +707,66 @@ __global__ void k_trace_bounce(DevPool P, Src S, Sink K, int compact, uint64_t *
     if (stamps) stamp(stamps, stamp_cap, t0, total);
 }
 
+// Grid schedule with lane refill (north_star's wavefront compaction of
+// active rays): each wave owns a chunk of `chunk_rays` consecutive rays (a
+// few 8x8 tiles) and walks them with its 64 lanes.  Whenever at least
+// `refill_min` lanes have finished (ballot + popcount, wave-uniform), the
+// finished lanes write their records and the idle lanes take the chunk's
+// next rays in lane order (prefix popcount), so a wave's lanes stay busy
+// until its chunk runs dry instead of idling beside its slowest ray.  Ray
+// setup (raygen + ray_init) runs once per refill on the idle lanes only; the
+// tile arithmetic of a refill is wave-uniform (get_refill).
+constexpr uint32_t kNoRay = 0xFFFFFFFFu;
+
+template <class Src, class Sink, bool kPacked, bool kCount>
+__global__ void k_trace_refill(DevPool P, Src S, Sink K, uint32_t chunk_rays, int refill_min, uint64_t *stamps,
+                               uint32_t stamp_cap)
+{
+    extern __shared__ uint32_t lds_stack[];
+    const uint64_t t0 = stamps ? realtime() : 0;
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wave = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    uint32_t *stack = lds_stack + threadIdx.x;
+    const uint32_t n = S.count();
+    uint32_t cursor = wave * chunk_rays;                            // wave-uniform
+    const uint32_t end = min(cursor + chunk_rays, n);
+    Ray r;
+    r.level = 0;                                                    // no ray: not active
+    uint32_t out = kNoRay;
+    uint64_t finished = 0;
+    const uint64_t below = (1ull << lane) - 1ull;
+    for (;;) {
+        // Retire: finished lanes write their record.
+        if (out != kNoRay && !ray_active(r, P)) {
+            K.put(out, ray_result(r, P));
+            out = kNoRay;
+            ++finished;
+        }
+        // Refill the idle lanes from the chunk.
+        uint64_t idle = __ballot(out == kNoRay);
+        if (cursor < end) {
+            const uint32_t n_idle = (uint32_t)__popcll(idle);
+            const uint32_t take = min(n_idle, end - cursor);
+            if (out == kNoRay) {
+                const uint32_t k = (uint32_t)__popcll(idle & below);
+                float o[3], d[3];
+                if (k < take && S.get_refill(cursor, k, o, d, out))
+                    ray_init<kPacked, kCount>(r, P, o, d, stack, blockDim.x);
+                else
+                    out = kNoRay;
+            }
+            cursor += take;
+        }
+        if (cursor >= end && __ballot(out != kNoRay) == 0) break;
+        // Walk until refill_min lanes are idle (all of them once the chunk is dry).
+        const uint32_t keep = cursor < end ? 64u - (uint32_t)refill_min : 0u;
+        do {
+            if (ray_active(r, P)) ray_iterate<kPacked, kCount>(r, P, blockDim.x);
+        } while ((uint32_t)__popcll(__ballot(ray_active(r, P))) > keep);
+    }
+    if (stamps) stamp(stamps, stamp_cap, t0, finished);
+}
+
 template <class Src, class Sink, bool kPacked, bool kCount>
 __global__ void k_trace_persistent(DevPool P, Src S, Sink K, uint32_t *counter, int refill_min, uint64_t *stamps,
                                    uint32_t stamp_cap)
@@ -794,7 +896,12 @@ hipError_t launch_as(const DevPool &p, const Src &s, const Sink &k, uint32_t n, 
 #define OCH_LDS_MIN 0     // occupancy experiments: pad each block's LDS to this many bytes
 #endif
     const size_t lds = stack_bytes(p.depth, block) > OCH_LDS_MIN ? stack_bytes(p.depth, block) : OCH_LDS_MIN;
-    if (sc.persistent) {
+    if (sc.kind == 2) {
+        const uint32_t chunk = 64u * (uint32_t)sc.chunk_tiles;
+        const uint32_t waves = (n + chunk - 1) / chunk, wpb = (uint32_t)block / 64u;
+        hipLaunchKernelGGL((k_trace_refill<Src, Sink, kPacked, kCount>), dim3((waves + wpb - 1) / wpb), dim3(block),
+                           lds, stream, p, s, k, chunk, sc.refill_min, sc.stamps, sc.stamp_cap);
+    } else if (sc.kind == 1) {
         hipError_t e = hipMemsetAsync(sc.counter, 0, sizeof(uint32_t), stream);
         if (e != hipSuccess) return e;
         const uint32_t blocks_per_cu = (uint32_t)((sc.waves_per_cu * 64 + block - 1) / block);
@@ -854,6 +961,10 @@ CameraSource camera_source(const DevFrame &f, const Schedule &sc)
     const uint32_t tiles_y = (uint32_t)(f.slice_rows + kTileH - 1) / kTileH;
     src.supertiles_x = (src.tiles_x + 7) / 8;
     src.per_view = sc.tile_order == 1 ? src.supertiles_x * ((tiles_y + 7) / 8) * 64u * 64u : src.tiles_x * tiles_y * 64u;
+    if (sc.kind == 2) {   // refill chunks never cross a view: pad each view to whole chunks (padding rays are invalid)
+        const uint32_t chunk = 64u * (uint32_t)sc.chunk_tiles;
+        src.per_view = (src.per_view + chunk - 1) / chunk * chunk;
+    }
     src.slice_pixels = (uint32_t)f.slice_rows * (uint32_t)src.width;
     return src;
 }

@@ -143,10 +143,11 @@ class GpuPool:
         call("och_gpu_pool_update", self._h, int(first), nodes.shape[0], _np_ptr(nodes), int(root))
 
     OPTIONS = {"schedule": 0, "block": 1, "waves_per_cu": 2, "refill": 3, "layout": 4, "tile_order": 5,
-               "bounce_compact": 6}
+               "bounce_compact": 6, "chunk_tiles": 7}
 
     def set_option(self, name: str, value: int):
-        """Launch schedule: schedule (0 grid / 1 persistent), block, waves_per_cu, refill."""
+        """Launch options (och_gpu_set_option): schedule (0 grid / 1 persistent / 2 grid with lane
+        refill), block, waves_per_cu, refill, layout, tile_order, bounce_compact, chunk_tiles."""
         call("och_gpu_set_option", self._h, self.OPTIONS[name], int(value))
 
     def get_option(self, name: str) -> int:

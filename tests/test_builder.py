@@ -133,3 +133,35 @@ def test_pool_file_round_trip_and_corruption(ort, tmp_path):
     p.write_bytes(bytes(raw[:10]))
     with pytest.raises(ValueError, match="truncated"):
         ort.NodePool.load(p)
+
+
+def test_pool_file_header_corruption(ort, tmp_path):
+    """the checksum covers depth / index base / root / count, and a
+    root outside the pool is refused even when the checksum is skipped."""
+    import struct
+    tree = ort.build_terrain(5)
+    p = tmp_path / "d5.ochpool"
+    tree.save(p)
+    good = p.read_bytes()
+    # field offsets in the header: magic 0, version 8, depth 12, index_base 16, root 20, n 24, crc 32
+    for off, val in ((12, 6), (20, 2), (16, 1)):
+        raw = bytearray(good)
+        raw[off:off + 4] = struct.pack("<i", val)
+        if off == 16:                                   # index base 1 -> 0 makes root 1 invalid too
+            raw[off:off + 4] = struct.pack("<i", 0)
+        p.write_bytes(bytes(raw))
+        with pytest.raises(ValueError):
+            ort.NodePool.load(p)
+    raw = bytearray(good)
+    raw[20:24] = struct.pack("<I", tree.n_nodes + 1)    # root past the end
+    p.write_bytes(bytes(raw))
+    with pytest.raises(ValueError, match="root"):
+        ort.NodePool.load(p, verify=False)
+    # a version-1 file (checksum of the slots only) still loads
+    v1 = bytearray(good)
+    v1[8:12] = struct.pack("<I", 1)
+    import zlib
+    v1[32:36] = struct.pack("<I", zlib.crc32(good[64:]))
+    p.write_bytes(bytes(v1))
+    back = ort.NodePool.load(p)
+    assert np.array_equal(back.nodes, tree.nodes) and back.root == tree.root

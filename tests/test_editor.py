@@ -196,3 +196,66 @@ def test_churn_reuses_slots_and_tombstones(ort):
         assert ed.at(x, y, z) == 0
     st = ed.stats()
     assert st["live_nodes"] == depth and st["high_water"] <= 3 * depth
+
+
+@pytest.mark.gpu
+def test_gpu_flush_pool_identity(ort, O, gpu_device):
+    """pools are told apart by serial, not address.  A pool closed
+    and replaced by a new one (likely at the same address), one editor flushed
+    to two pools in turn, a pool rewritten by och_gpu_pool_update in between,
+    and a second editor flushing the same pool: every flush leaves the device
+    tracing exactly the reference table after the same edits."""
+    from test_gpu_parity import assert_same, gpu_trace_dev
+    depth = 6
+    T = O.HRef(depth, 14)
+    T.fill_terrain()
+    ed = ort.Editor(T.nodes(), T.root, depth)
+    rays = O.raygen(0.3, -0.6, 1.25, 160, 90)
+
+    def check(pool):
+        ref = O.trace_batch(T.pool(), O.Rcp(None), ORIGIN, rays, want_push=True)
+        for layout in (1, 0):
+            pool.set_option("layout", layout)
+            assert_same(gpu_trace_dev(pool, ORIGIN, rays), ref)
+        pool.set_option("layout", 1)
+
+    def edit(seed):
+        for x, y, z, v in _edits(seed, 60, 10, 50):
+            T.set(x, y, z, v)
+            ed.set(x, y, z, v)
+
+    a = ed.make_pool(device=0)
+    edit(1)
+    ed.flush(a)
+    check(a)
+    a.close()                                   # its address is free for the next pool
+    for k in range(3):
+        b = ed.make_pool(device=0)
+        edit(2 + k)
+        ed.flush(b)
+        check(b)
+        b.close()
+    p, q = ed.make_pool(device=0), ed.make_pool(device=0)
+    for k in range(3):                          # alternate flushes: each pool misses the other's window
+        edit(10 + k)
+        ed.flush(p)
+        check(p)
+        edit(20 + k)
+        ed.flush(q)
+        check(q)
+    # och_gpu_pool_update rewrites p (same content, caller-managed) -> next flush is whole
+    nodes = ed.nodes()
+    p.update(1, nodes, ed.root)
+    edit(30)
+    ed.flush(p)
+    check(p)
+    # a second editor with the same slot count writes q; the first editor's next flush is whole
+    ed2 = ort.Editor(T.nodes(), T.root, depth, capacity=ed.stats()["capacity"])
+    ed2.flush(q)
+    edit(40)
+    ed.flush(q)
+    check(q)
+    for x in (p, q):
+        x.close()
+    ed2.close()
+    ed.close()

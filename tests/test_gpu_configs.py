@@ -1,0 +1,160 @@
+"""GPU parity at the BASELINE configs' own workloads (depth-12 terrain).
+
+configs[2]: depth 12, 1920x1080 -- checked through the exact instance the
+            bench times: ShardedFrame (row chunks of 8, indexed-colour codes,
+            two views per launch, packed layout, grid schedule) followed by
+            k_shade_unshard, against the oracle's trace + trace_pixel shading
+            (ORT/test_och_h_octree.cpp:437-457, :64-85).
+configs[3]: depth 12, 3840x2160 as 8 row-chunk shards (one GPU renders each
+            rank's slice in turn), gathered and shaded.
+configs[4]: depth 12, 1920x1080 primary + one mirrored secondary ray per hit
+            (build-defined from get_directional_hit_offset, :487-502), with
+            the in-block compaction on and off: hit records and frames.
+
+Every comparison is bit for bit (RGBA8 words, direction, voxel id, t bits,
+PUSH counts).  The oracle runs this host's native RCPPS, the pool the table
+captured from the same host."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ORIGIN = np.array([1.5, 1.5, 1.5], np.float32)
+PITCHES = (0.0, -0.6)
+YAW, FOV = 0.3, 1.25
+
+
+@pytest.fixture(scope="module")
+def d12(ort):
+    return ort.build_terrain(12)
+
+
+@pytest.fixture(scope="module")
+def d12_ref(O, d12):
+    return O.OraclePool(d12.nodes, d12.root, 12, 1)
+
+
+@pytest.fixture(scope="module")
+def pal(ort):
+    return ort.VoxelData().get_colours()
+
+
+def oracle_frames(O, ref_pool, pal, W, H, bounce=False):
+    out = []
+    for p in PITCHES:
+        rays = O.raygen(YAW, p, FOV, W, H)
+        if bounce:
+            r = O.trace_bounce_batch(ref_pool, O.Rcp(None), ORIGIN, rays, nthreads=16)
+            out.append(O.shade_bounce(r["dir"], r["voxel"], r["dir2"], pal).reshape(H, W))
+        else:
+            r = O.trace_batch(ref_pool, O.Rcp(None), ORIGIN, rays, nthreads=16)
+            out.append(O.shade_fast(r["dir"], r["voxel"], pal).reshape(H, W))
+    return out
+
+
+def assert_frames(got, want):
+    for v, w in enumerate(want):
+        g = got[v].cpu().numpy().view(np.uint32)
+        bad = np.argwhere(g != w)
+        assert bad.size == 0, f"view {v}: {len(bad)} pixels differ, first {bad[:4].tolist()}"
+
+
+def test_bench_instance_d12_1080p(ort, O, gpu_device, d12, d12_ref, pal):
+    """configs[2]: k_trace_grid<CameraSource,CodeSink> + k_shade_unshard4, as bench.py runs them."""
+    import torch
+    from octree_ray_tracing_amd.frame import ShardedFrame
+    W, H = 1920, 1080
+    pool = ort.HOctree(d12.nodes, d12.root, 12, device=0)
+    pool.set_palette(pal)
+    assert pool.get_option("layout") == 1 and pool.get_option("schedule") == 0
+    want = oracle_frames(O, d12_ref, pal, W, H)
+    cams = [ort.camera(tuple(ORIGIN), YAW, p, FOV, W, H) for p in PITCHES]
+    # three frames in flight on three streams, as the bench pipelines them
+    streams = [torch.cuda.current_stream()] + [torch.cuda.Stream() for _ in range(2)]
+    sfs = []
+    for s in streams:
+        with torch.cuda.stream(s):
+            sfs.append(ShardedFrame(pool, W, H, 8, n_views=2, indexed=True))
+    for k in range(6):
+        s, sf = streams[k % 3], sfs[k % 3]
+        pool.set_stream(s)
+        with torch.cuda.stream(s):
+            sf.render(cams)
+    torch.cuda.synchronize()
+    for sf in sfs:
+        assert_frames(sf.frames, want)
+    pool.set_stream(torch.cuda.current_stream())
+    # the RGBA8 render path of the same frames
+    sf = ShardedFrame(pool, W, H, 8, n_views=2, indexed=False)
+    sf.render(cams)
+    torch.cuda.synchronize()
+    assert_frames(sf.frames, want)
+    pool.close()
+
+
+def test_config4_2160p_as_8_shards(ort, O, gpu_device, d12, d12_ref, pal):
+    """configs[3]: 3840x2160, rows dealt in 8-row chunks over 8 shards, gathered, shaded."""
+    import torch
+    W, H, n, chunk = 3840, 2160, 8, 8
+    pool = ort.HOctree(d12.nodes, d12.root, 12, device=0)
+    pool.set_palette(pal)
+    pool.set_stream(torch.cuda.current_stream())
+    cams = [ort.camera(tuple(ORIGIN), YAW, p, FOV, W, H) for p in PITCHES]
+    rows = ort.shard_rows(H, chunk, n)
+    gathered = torch.full((n, 2, rows, W), 255, dtype=torch.uint8, device="cuda")
+    for s in range(n):
+        pool.render_codes_views_dev(cams, gathered[s], chunk, s, n)
+    frames = torch.empty((2, H, W), dtype=torch.int32, device="cuda")
+    pool.shade_unshard_dev(gathered, frames, W, H, chunk, n, 2)
+    torch.cuda.synchronize()
+    want = oracle_frames(O, d12_ref, pal, W, H)
+    assert_frames(frames, want)
+    pool.close()
+
+
+@pytest.mark.parametrize("compact", [1, 0])
+def test_config5_d12_records(ort, O, gpu_device, d12, d12_ref, compact):
+    """configs[4]: primary + secondary hit records at depth 12, camera frame and random rays."""
+    from test_gpu_parity import assert_same_bounce, gpu_trace_bounce_dev
+    pool = ort.HOctree(d12.nodes, d12.root, 12, device=0)
+    pool.set_option("bounce_compact", compact)
+    rng = np.random.default_rng(12)
+    ro = rng.uniform(1.01, 1.99, (200000, 3)).astype(np.float32)
+    rd = rng.uniform(-1, 1, (200000, 3)).astype(np.float32)
+    rd /= np.linalg.norm(rd, axis=1, keepdims=True)
+    sets = [(ORIGIN, O.raygen(YAW, p, FOV, 1920, 1080)) for p in PITCHES] + [(ro, rd)]
+    for origins, dirs in sets:
+        ref = O.trace_bounce_batch(d12_ref, O.Rcp(None), origins, dirs, nthreads=16, want_push=True)
+        assert_same_bounce(gpu_trace_bounce_dev(pool, origins, dirs), ref)
+    pool.close()
+
+
+@pytest.mark.parametrize("compact", [1, 0])
+def test_config5_d12_frames(ort, O, gpu_device, d12, d12_ref, pal, compact):
+    """configs[4] frames through the bench's path (indexed codes, bounce=1), compaction on / off."""
+    import torch
+    from octree_ray_tracing_amd.frame import ShardedFrame
+    W, H = 1920, 1080
+    pool = ort.HOctree(d12.nodes, d12.root, 12, device=0)
+    pool.set_palette(pal)
+    pool.set_option("bounce_compact", compact)
+    cams = [ort.camera(tuple(ORIGIN), YAW, p, FOV, W, H) for p in PITCHES]
+    sf = ShardedFrame(pool, W, H, 8, n_views=2, indexed=True)
+    sf.render(cams, bounce=True)
+    torch.cuda.synchronize()
+    assert_frames(sf.frames, oracle_frames(O, d12_ref, pal, W, H, bounce=True))
+    pool.close()
+
+
+def test_d12_trace_records_all_schedules(ort, O, gpu_device, d12, d12_ref):
+    """configs[2] hit records and PUSH counts at depth 12 for both schedules and layouts."""
+    from test_gpu_parity import assert_same, gpu_trace_dev
+    pool = ort.HOctree(d12.nodes, d12.root, 12, device=0)
+    rays = O.raygen(YAW, -0.6, FOV, 1920, 1080)
+    ref = O.trace_batch(d12_ref, O.Rcp(None), ORIGIN, rays, nthreads=16, want_push=True)
+    for sched in (0, 1):
+        for layout in (1, 0):
+            pool.set_option("schedule", sched)
+            pool.set_option("layout", layout)
+            assert_same(gpu_trace_dev(pool, ORIGIN, rays), ref)
+    pool.close()

@@ -98,11 +98,14 @@ def main():
     s = summarise(Path(a.root))
     print(json.dumps(s, indent=1, sort_keys=True))
     if a.update and a.key:
+        # One configuration per file, tied to the kernel sources it was taken
+        # of: bench.py uses it only when both match (bench.load_pmc).
+        sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+        from bench import kernel_source_digest
         p = Path(a.update)
-        d = json.loads(p.read_text()) if p.exists() else {}
-        d[a.key] = s
-        p.write_text(json.dumps(d, indent=1, sort_keys=True))
-        print(f"updated {p} [{a.key}]", file=sys.stderr)
+        p.write_text(json.dumps({"config": a.key, "kernel_source_sha": kernel_source_digest(), "kernels": s},
+                                indent=1, sort_keys=True))
+        print(f"wrote {p} [{a.key}]", file=sys.stderr)
 
 
 if __name__ == "__main__":
