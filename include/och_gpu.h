@@ -249,6 +249,38 @@ OCH_API int och_gpu_render_codes_views_dev(och_gpu_pool *pool, const och_camera 
 OCH_API int och_gpu_shade_unshard_views_dev(och_gpu_pool *pool, const uint8_t *gathered, uint32_t *frames,
                                             int width, int height, int row_chunk, int n_shards, int n_views);
 
+/* ------------------------------------------------------------ multi-GPU frames, one process */
+/* SURVEY §8(e) for a C++ host: one process, one thread, every GPU of the node.
+ * Each device holds a replica of the pool; rows are dealt in chunks of
+ * row_chunk rows round-robin over the devices (och_shard_rows); every device
+ * renders its slice, one RCCL all-gather (ncclCommInitAll over the devices,
+ * xGMI) hands every device all slices, and each device shades + unshards them
+ * into [n_views][H][W] RGBA8 frames -- the frames och_gpu_render_views_dev
+ * would write, bit for bit.  Slices travel as 1-byte colour codes when the
+ * palette has at most OCH_CODE_MAX_VOXELS ids, as RGBA8 otherwise.  RCCL is
+ * loaded on first use (dlopen; an RCCL already in the process is reused);
+ * OCH_E_NODEV when it cannot be.  devices = NULL means 0..n_devices-1.
+ * Replaces the per-pixel loop of ORT/test_och_h_octree.cpp:437-457 across GPUs. */
+typedef struct och_frame_group och_frame_group;
+OCH_API int och_frame_group_create(const int *devices, int n_devices, const uint32_t *nodes, uint32_t n_nodes,
+                                   uint32_t root, int depth, int index_base, float miss_t, och_frame_group **out);
+OCH_API int och_frame_group_destroy(och_frame_group *group);
+OCH_API int och_frame_group_size(const och_frame_group *group, int *n_devices);
+/* The pool replica on device `rank` (RCPPS table, stamps; owned by the group). */
+OCH_API int och_frame_group_pool(och_frame_group *group, int rank, och_gpu_pool **pool);
+OCH_API int och_frame_group_set_palette(och_frame_group *group, const uint32_t *rgba, uint32_t n_voxels);
+OCH_API int och_frame_group_set_option(och_frame_group *group, int option, int value);
+/* Enqueue one frame of n_views equal-size cameras on every device (bounce = 1:
+ * config 5's secondary rays).  Asynchronous; frames are valid once the
+ * group is synchronised (or downloaded). */
+OCH_API int och_frame_group_render(och_frame_group *group, const och_camera *cams, int n_views, int row_chunk,
+                                   int bounce);
+/* Device pointer of device `rank`'s [n_views][H][W] RGBA8 frames (valid until the next render). */
+OCH_API int och_frame_group_frames_dev(och_frame_group *group, int rank, uint32_t **frames);
+/* Copy device `rank`'s frames to a host buffer of n_views*H*W words (synchronous). */
+OCH_API int och_frame_group_download(och_frame_group *group, int rank, uint32_t *rgba);
+OCH_API int och_frame_group_synchronize(och_frame_group *group);
+
 /* ------------------------------------------------------------ builder */
 /* The demo terrain (ORT/test_och_h_octree.cpp:561-787) built in parallel
  * bottom-up, hash-consed to the same canonical DAG h_octree produces.

@@ -98,18 +98,13 @@ public:
     editor(const uint32_t *nodes, uint32_t n_nodes, uint32_t root, int depth, uint32_t capacity)
         : depth_(depth)
     {
-        const int st = och_editor_create(nodes, n_nodes, root, depth, capacity, &ed_);
-        if (st != OCH_OK) throw error(st, "och_editor_create");
+        check(och_editor_create(nodes, n_nodes, root, depth, capacity, &ed_), "och_editor_create");
     }
     editor(const editor &) = delete;
     editor &operator=(const editor &) = delete;
     ~editor() { och_editor_destroy(ed_); }
 
-    void set(int x, int y, int z, uint32_t v)
-    {
-        const int st = och_editor_set(ed_, x, y, z, v);
-        if (st != OCH_OK) throw error(st, "och_editor_set");
-    }
+    void set(int x, int y, int z, uint32_t v) { check(och_editor_set(ed_, x, y, z, v), "och_editor_set"); }
     uint32_t at(int x, int y, int z) const { return och_editor_at(ed_, x, y, z); }
     uint32_t get_root() const
     {
@@ -133,6 +128,56 @@ public:
 private:
     och_editor *ed_ = nullptr;
     int depth_;
+};
+
+// Every GPU of the node from one host thread: a pool replica
+// per device, row chunks dealt round-robin, one RCCL all-gather, shading on
+// every device.  frames(rank) is device rank's [views][H][W] RGBA8 copy.
+class frame_group {
+public:
+    frame_group(const std::vector<int> &devices, const uint32_t *nodes, uint32_t n_nodes, uint32_t root, int depth,
+                int index_base = 1, float miss_t = __builtin_inff())
+    {
+        check(och_frame_group_create(devices.data(), static_cast<int>(devices.size()), nodes, n_nodes, root, depth,
+                                     index_base, miss_t, &g_),
+              "och_frame_group_create");
+    }
+    frame_group(const frame_group &) = delete;
+    frame_group &operator=(const frame_group &) = delete;
+    ~frame_group() { och_frame_group_destroy(g_); }
+
+    int size() const
+    {
+        int n = 0;
+        check(och_frame_group_size(g_, &n), "och_frame_group_size");
+        return n;
+    }
+    void set_palette(const std::vector<uint32_t> &rgba)
+    {
+        check(och_frame_group_set_palette(g_, rgba.data(), static_cast<uint32_t>(rgba.size() / 6)),
+              "och_frame_group_set_palette");
+    }
+    void set_option(och_option option, int value)
+    {
+        check(och_frame_group_set_option(g_, option, value), "och_frame_group_set_option");
+    }
+    // One frame of every view, asynchronous on all devices.
+    void render(const std::vector<och_camera> &cams, int row_chunk = 8, bool bounce = false)
+    {
+        check(och_frame_group_render(g_, cams.data(), static_cast<int>(cams.size()), row_chunk, bounce ? 1 : 0),
+              "och_frame_group_render");
+    }
+    uint32_t *frames(int rank) const
+    {
+        uint32_t *p = nullptr;
+        check(och_frame_group_frames_dev(g_, rank, &p), "och_frame_group_frames_dev");
+        return p;
+    }
+    void download(int rank, uint32_t *rgba) const { check(och_frame_group_download(g_, rank, rgba), "och_frame_group_download"); }
+    void synchronize() const { check(och_frame_group_synchronize(g_), "och_frame_group_synchronize"); }
+
+private:
+    och_frame_group *g_ = nullptr;
 };
 
 // tree_camera's per-frame state (pos :55, dir :53, fov :95).

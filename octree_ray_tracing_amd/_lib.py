@@ -103,6 +103,16 @@ PROTOTYPES = {
     "och_editor_info": (C.c_int, [_P, C.POINTER(EditorStats)]),
     "och_editor_nodes": (C.c_int, [_P, C.POINTER(C.POINTER(_u32)), C.POINTER(_u32), C.POINTER(_u32)]),
     "och_editor_flush": (C.c_int, [_P, _P]),
+    "och_frame_group_create": (C.c_int, [_P, C.c_int, _P, _u32, _u32, C.c_int, C.c_int, _f32, C.POINTER(_P)]),
+    "och_frame_group_destroy": (C.c_int, [_P]),
+    "och_frame_group_size": (C.c_int, [_P, C.POINTER(C.c_int)]),
+    "och_frame_group_pool": (C.c_int, [_P, C.c_int, C.POINTER(_P)]),
+    "och_frame_group_set_palette": (C.c_int, [_P, _P, _u32]),
+    "och_frame_group_set_option": (C.c_int, [_P, C.c_int, C.c_int]),
+    "och_frame_group_render": (C.c_int, [_P, _P, C.c_int, C.c_int, C.c_int]),
+    "och_frame_group_frames_dev": (C.c_int, [_P, C.c_int, C.POINTER(_P)]),
+    "och_frame_group_download": (C.c_int, [_P, C.c_int, _P]),
+    "och_frame_group_synchronize": (C.c_int, [_P]),
 }
 
 # Functions whose int return value is data, not a status.

@@ -498,6 +498,13 @@ OCH_API int och_gpu_pool_update(och_gpu_pool *p, uint32_t first, uint32_t count,
 int och::report(int status, const char *msg) { return fail(status, "%s", msg); }
 
 uint64_t och::pool_serial(const och_gpu_pool *p) { return p ? p->serial : 0; }
+void *och::pool_stream(const och_gpu_pool *p) { return p ? static_cast<void *>(p->stream()) : nullptr; }
+int och::pool_palette_size(const och_gpu_pool *p, int *n)
+{
+    if (!p || !n) return fail(OCH_E_INVALID, "NULL argument");
+    *n = (int)p->n_voxels;
+    return OCH_OK;
+}
 uint64_t och::pool_last_writer(const och_gpu_pool *p) { return p ? p->last_writer : 0; }
 
 int och::pool_drain(och_gpu_pool *p)

@@ -54,6 +54,10 @@ int pool_write_slots(och_gpu_pool *pool, uint32_t first, uint32_t count, const u
                      const uint32_t *packed, bool full);
 int pool_commit(och_gpu_pool *pool, uint32_t root, uint32_t packed_root, bool packed, uint64_t writer);
 uint64_t pool_serial(const och_gpu_pool *pool);
+// The stream the pool enqueues on (hipStream_t) and its palette size
+// (och_group.cpp drives several pools from one thread).
+void *pool_stream(const och_gpu_pool *pool);
+int pool_palette_size(const och_gpu_pool *pool, int *n_voxels);
 uint64_t pool_last_writer(const och_gpu_pool *pool);
 
 struct DevFrame {

@@ -10,8 +10,12 @@ collective is the framebuffer exchange.
 """
 from __future__ import annotations
 
+import ctypes as C
+import math
+
 import numpy as np
 
+from ._lib import Camera, call
 from .tracer import GpuPool, shard_rows
 
 
@@ -102,3 +106,58 @@ class ShardedFrame:
     def render(self, cams, bounce: bool = False):
         self.render_local(cams, bounce)
         return self.exchange()
+
+
+class FrameGroup:
+    """One process driving several GPUs (och_frame_group_*, the C++ host's
+    form of SURVEY §8(e)): a pool replica per device, each renders its row
+    chunks, one RCCL all-gather (ncclCommInitAll over the devices) and a
+    shade + unshard per device.  `frames(rank)` is device `rank`'s copy of
+    the [views][H][W] RGBA8 frames."""
+
+    def __init__(self, nodes: np.ndarray, root: int, depth: int, devices=None, index_base: int = 1,
+                 miss_t: float | None = None):
+        nodes = np.ascontiguousarray(nodes, np.uint32).reshape(-1, 8)
+        if devices is None:
+            from .tracer import device_count
+            devices = list(range(device_count()))
+        devs = (C.c_int * len(devices))(*devices)
+        if miss_t is None:
+            miss_t = math.inf if index_base == 1 else 0.0
+        self._h = C.c_void_p()
+        self.n = len(devices)
+        call("och_frame_group_create", C.cast(devs, C.c_void_p), len(devices), nodes.ctypes.data, nodes.shape[0],
+             int(root), int(depth), int(index_base), float(miss_t), C.byref(self._h))
+        self._shape = None
+
+    def close(self):
+        if getattr(self, "_h", None) and self._h.value:
+            call("och_frame_group_destroy", self._h)
+            self._h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_palette(self, rgba: np.ndarray):
+        rgba = np.ascontiguousarray(rgba, np.uint32).reshape(-1)
+        call("och_frame_group_set_palette", self._h, rgba.ctypes.data, rgba.size // 6)
+
+    def set_option(self, name: str, value: int):
+        call("och_frame_group_set_option", self._h, GpuPool.OPTIONS[name], int(value))
+
+    def render(self, cams, row_chunk: int = 8, bounce: bool = False):
+        cams = list(cams) if isinstance(cams, (list, tuple)) else [cams]
+        arr = (Camera * len(cams))(*cams)
+        call("och_frame_group_render", self._h, C.cast(arr, C.c_void_p), len(cams), int(row_chunk), int(bool(bounce)))
+        self._shape = (len(cams), cams[0].height, cams[0].width)
+
+    def synchronize(self):
+        call("och_frame_group_synchronize", self._h)
+
+    def download(self, rank: int = 0) -> np.ndarray:
+        out = np.empty(self._shape, np.uint32)
+        call("och_frame_group_download", self._h, int(rank), out.ctypes.data)
+        return out

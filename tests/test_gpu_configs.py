@@ -152,7 +152,7 @@ def test_d12_trace_records_all_schedules(ort, O, gpu_device, d12, d12_ref):
     pool = ort.HOctree(d12.nodes, d12.root, 12, device=0)
     rays = O.raygen(YAW, -0.6, FOV, 1920, 1080)
     ref = O.trace_batch(d12_ref, O.Rcp(None), ORIGIN, rays, nthreads=16, want_push=True)
-    for sched in (0, 1):
+    for sched in (0, 1, 2):
         for layout in (1, 0):
             pool.set_option("schedule", sched)
             pool.set_option("layout", layout)

@@ -93,7 +93,7 @@ def test_camera_frames_host_rcpps(ort, O, gpu_device, depth):
     for pitch in (0.0, -0.6):
         rays = O.raygen(0.3, pitch, 1.25, 1920, 1080)
         ref = O.trace_batch(ref_pool, O.Rcp(None), ORIGIN, rays, nthreads=16, want_push=True)
-        for sched in (0, 1):
+        for sched in (0, 1, 2):
             for layout in (0, 1):
                 pool.set_option("schedule", sched)
                 pool.set_option("layout", layout)
@@ -218,7 +218,7 @@ def test_multi_view_render_and_unshard(ort, O, gpu_device):
     W, H = 320, 200
     cams = [ort.camera((1.5, 1.5, 1.5), y, p, 1.25, W, H) for y, p in ((0.3, 0.0), (0.3, -0.6), (1.9, -0.2))]
     single = [torch.from_numpy(pool.render(c).view(np.int32)) for c in cams]
-    for sched in (0, 1):
+    for sched in (0, 1, 2):
         pool.set_option("schedule", sched)
         out = torch.zeros((3, H, W), dtype=torch.int32, device="cuda")
         pool.render_views_dev(cams, out)
@@ -421,4 +421,51 @@ def test_indexed_colour_frames(ort, O, gpu_device, bounce, W):
     pool.set_palette(big)
     with pytest.raises(ort.OchError):
         pool.render_codes_views_dev(cams, gathered[0], chunk, 0, n, bounce)
+    pool.close()
+
+
+@pytest.mark.parametrize("chunk,refill", [(1, 1), (2, 64), (4, 16), (16, 8), (64, 32)])
+def test_refill_schedule_variants(ort, O, gpu_device, chunk, refill):
+    """Schedule 2 (grid with lane refill) at its extremes: one tile per wave
+    and refill after every finished lane, whole-wave refills, long chunks;
+    camera frames (odd sizes: partial tiles, padded chunks), sharded codes and
+    random rays, all bit-identical to the oracle."""
+    import torch
+    tree = ort.build_terrain(9)
+    pal = ort.VoxelData().get_colours()
+    pool = ort.HOctree(tree.nodes, tree.root, 9, device=0)
+    pool.set_palette(pal)
+    pool.set_stream(torch.cuda.current_stream())
+    pool.set_option("schedule", 2)
+    pool.set_option("chunk_tiles", chunk)
+    pool.set_option("refill", refill)
+    ref_pool = O.OraclePool(tree.nodes, tree.root, 9, 1)
+    rng = np.random.default_rng(chunk * 100 + refill)
+    o = rng.uniform(1.01, 1.99, (30001, 3)).astype(np.float32)
+    d = rng.uniform(-1, 1, (30001, 3)).astype(np.float32)
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    assert_same(gpu_trace_dev(pool, o, d), O.trace_batch(ref_pool, O.Rcp(None), o, d, nthreads=16, want_push=True))
+    W, H = 803, 451
+    cams = [ort.camera((1.5, 1.5, 1.5), 0.3, p, 1.25, W, H) for p in (0.0, -0.6)]
+    want = []
+    for p in (0.0, -0.6):
+        r = O.trace_batch(ref_pool, O.Rcp(None), ORIGIN, O.raygen(0.3, p, 1.25, W, H), nthreads=16)
+        want.append(O.shade(r["dir"], r["voxel"], pal).reshape(H, W))
+    for n, rc in ((1, H), (3, 8), (2, 5)):
+        rows = ort.shard_rows(H, rc, n)
+        gathered = torch.full((n, 2, rows, W), 255, dtype=torch.uint8, device="cuda")
+        for s_ in range(n):
+            pool.render_codes_views_dev(cams, gathered[s_], rc, s_, n)
+        full = torch.empty((2, H, W), dtype=torch.int32, device="cuda")
+        pool.shade_unshard_dev(gathered, full, W, H, rc, n, 2)
+        torch.cuda.synchronize()
+        for v in range(2):
+            assert np.array_equal(full[v].cpu().numpy().view(np.uint32), want[v]), (n, rc, v)
+    for order in (0, 1):
+        pool.set_option("tile_order", order)
+        frames = torch.zeros((2, H, W), dtype=torch.int32, device="cuda")
+        pool.render_views_dev(cams, frames)
+        torch.cuda.synchronize()
+        for v in range(2):
+            assert np.array_equal(frames[v].cpu().numpy().view(np.uint32), want[v]), (order, v)
     pool.close()

@@ -26,6 +26,9 @@ def main():
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--cache", default="/tmp/och_terrain_cache.npz")
     ap.add_argument("--out", default="gpurun_out/ab.json")
+    ap.add_argument("--pipelined", type=int, default=0,
+                    help="also time this many bench-style steps per arm and round (codes render + shade over 3 "
+                         "streams in flight, as bench.py), reporting wall-clock Mrays/s")
     a = ap.parse_args()
     arms = [json.loads(x) for x in (a.arm or ["{}"])]
 
@@ -67,12 +70,41 @@ def main():
                 torch.cuda.synchronize()
                 if r:
                     times[i].append(e0.elapsed_time(e1))
+    import time
+    from octree_ray_tracing_amd.frame import ShardedFrame
+    walls = [[] for _ in arms]
+    if a.pipelined:
+        streams = [stream] + [torch.cuda.Stream() for _ in range(2)]
+        sfs = []
+        for s_ in streams:
+            with torch.cuda.stream(s_):
+                sfs.append(ShardedFrame(pool, W, H, 8, n_views=2, indexed=True))
+        shaded = [None] * len(arms)
+        for r in range(a.rounds + 1):
+            for i, arm in enumerate(arms):
+                apply(arm)
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                for k in range(a.pipelined):
+                    pool.set_stream(streams[k % 3])
+                    with torch.cuda.stream(streams[k % 3]):
+                        sfs[k % 3].render(cams)
+                torch.cuda.synchronize()
+                if r:
+                    walls[i].append(time.perf_counter() - t0)
+                shaded[i] = sfs[(a.pipelined - 1) % 3].frames.clone()
+        pool.set_stream(stream)
     res = []
     for i, arm in enumerate(arms):
         t = np.array(times[i])
         row = {"arm": arm, "median_us": round(float(np.median(t)) * 1e3, 1), "min_us": round(float(t.min()) * 1e3, 1),
                "mrays_s": round(2 * W * H / float(np.median(t)) / 1e3, 1),
                "bit_exact_vs_arm0": bool(torch.equal(frames[i], frames[0]))}
+        if a.pipelined:
+            w = np.array(walls[i])
+            row["pipelined_mrays_s"] = round(2 * W * H * a.pipelined / float(np.median(w)) / 1e6, 1)
+            row["pipelined_ms_per_step"] = round(float(np.median(w)) / a.pipelined * 1e3, 4)
+            row["pipelined_bit_exact_vs_arm0"] = bool(torch.equal(shaded[i], shaded[0]))
         res.append(row)
         print(json.dumps(row), flush=True)
     Path(a.out).parent.mkdir(parents=True, exist_ok=True)
