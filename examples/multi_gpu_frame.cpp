@@ -28,7 +28,7 @@ int main(int argc, char **argv)
         std::fprintf(stderr, "no gfx950 device\n");
         return 1;
     }
-    och_terrain_params tp = {depth, 1, 1, 0, 0, 0};
+    och_terrain_params tp = {depth, 1, 1, 0, 0, 1};   // voxelised on the GPU
     och_host_pool hp;
     och::gpu::check(och_build_terrain(&tp, &hp), "och_build_terrain");
     int rc = 0;

@@ -22,7 +22,7 @@ int main(int argc, char **argv)
     cam.height = argc > 4 ? std::atoi(argv[4]) : 720;
     cam.yaw = argc > 6 ? std::strtof(argv[5], nullptr) : 0.3F;
     cam.pitch = argc > 6 ? std::strtof(argv[6], nullptr) : -0.6F;
-    och_terrain_params tp = {depth, 1, 1, 0, 0, 0};
+    och_terrain_params tp = {depth, 1, 1, 0, 0, 1};   // voxelised on the GPU
     och_host_pool hp;
     och::gpu::check(och_build_terrain(&tp, &hp), "och_build_terrain");
     std::printf("terrain depth %d: %u nodes (%.2f s)\n", depth, hp.n_nodes, hp.build_seconds);

@@ -293,7 +293,10 @@ typedef struct och_terrain_params {
     int32_t dedup;          /* 1 = h_octree DAG, 0 = pointer octree */
     int32_t rand_kind;      /* 0 = glibc rand() default seed, 1 = MSVC rand() */
     int32_t threads;        /* 0 = all hardware threads */
-    int32_t use_gpu;        /* evaluate voxels on the GPU when one is present */
+    int32_t use_gpu;        /* 1: voxelise 32^3 bricks on the current GPU (depth >= 5; smaller trees
+                               are built on the host), host threads hash-cons the leaf codes;
+                               OCH_E_NODEV if no GPU can run the kernel.  0: host threads only.
+                               Both give the same pool, slot for slot. */
 } och_terrain_params;
 
 typedef struct och_host_pool {

@@ -95,9 +95,12 @@ class NodePool:
 
 
 def build_terrain(depth: int, tunnels: bool = True, dedup: bool = True, rand_kind: str = "glibc",
-                  threads: int = 0, use_gpu: bool = True) -> NodePool:
+                  threads: int = 0, use_gpu: bool = False) -> NodePool:
+    """The demo world as a node pool.  use_gpu=True voxelises on the current
+    GPU (och_terrain_params.use_gpu; raises OchError OCH_E_NODEV without
+    one); the pool is the same either way."""
     params = TerrainParams(int(depth), int(tunnels), int(dedup), 1 if rand_kind == "msvc" else 0,
-                           int(threads), int(use_gpu))
+                           int(threads), int(bool(use_gpu)))
     hp = HostPool()
     call("och_build_terrain", C.byref(params), C.byref(hp))
     try:

@@ -188,6 +188,8 @@ struct och_gpu_pool {
         std::memcpy(&mb, &miss_t, 4);
         p.miss_bits = mb;
         p.half_voxel = std::ldexp(1.0F, -(depth + 1));
+        p.dim_lo = 1u << (23 - depth);
+        p.dim_span = (1u << 22) - p.dim_lo;
         return p;
     }
 };

@@ -14,6 +14,16 @@
 // (the level is part of the key): the reference may share one slot between a
 // leaf-level node and an interior node whose child indices happen to spell
 // the same 8 words -- harmless for tracing, impossible to renumber.
+//
+// use_gpu: the voxel function -- simplex noise for every voxel below the
+// surface, 2 * 10^10 evaluations at depth 12 -- runs on the GPU instead
+// (k_brick_codes): one workgroup per 32^3 brick writes the brick's 4096
+// leaf-level nodes as 24-bit codes (3 bits per child voxel), its voxel
+// histogram and whether all its leaves are equal.  Host threads hash-cons the
+// codes bottom-up exactly as they do their own voxels, batch after batch,
+// while the GPU computes the next batch; bricks of one repeated leaf (solid
+// stone away from the tunnels) reuse one reduction.  Same DAG, same numbering.
+#include <hip/hip_runtime.h>
 #include <sched.h>
 #include <sys/mman.h>
 
@@ -23,7 +33,9 @@
 #include <cstdlib>
 #include <cstring>
 #include <functional>
+#include <mutex>
 #include <thread>
+#include <unordered_map>
 #include <vector>
 
 #include "och_internal.h"
@@ -124,6 +136,21 @@ struct NodeStore {
         return id;
     }
 
+    // A leaf-level node given as its code (3 bits per child, child k at bits 3k).
+    uint32_t intern_code(uint32_t code)
+    {
+        uint32_t c[8];
+        for (int k = 0; k < 8; ++k) c[k] = (code >> (3 * k)) & 7u;
+        if (!dedup) return alloc(c, 0);
+        std::atomic<uint32_t> &slot = leaf_ids[code];
+        uint32_t id = slot.load(std::memory_order_acquire);
+        if (id) return id;
+        const uint32_t mine = alloc(c, 0);
+        if (!mine) return 0;
+        if (slot.compare_exchange_strong(id, mine, std::memory_order_acq_rel)) return mine;
+        return id;
+    }
+
     uint32_t intern(const uint32_t *c, int h)
     {
         if (!dedup) return alloc(c, h);
@@ -195,44 +222,11 @@ struct BrickStats {
     uint64_t tree_nodes = 0;
 };
 
-// Voxelise one brick of side S at (bx, by, bz) (brick units) and reduce it to
-// its subtree root.  vox: S^3 scratch, ids: (S/2)^3 scratch.
-uint32_t build_brick(const Terrain &tr, NodeStore &ns, int s_log2, int bx, int by, int bz, std::vector<uint8_t> &vox,
-                     std::vector<uint32_t> &ids, BrickStats &st)
+// Reduce a brick's leaf-level ids (n^3, n = S/2, (z*n+y)*n+x) to its subtree
+// root: levels h = 1 .. s_log2 - 1, in place.
+uint32_t reduce_brick(NodeStore &ns, int s_log2, std::vector<uint32_t> &ids, BrickStats &st)
 {
-    const int S = 1 << s_log2;
-    const int x0 = bx * S, y0 = by * S, z0 = bz * S;
-    for (int y = 0; y < S; ++y)
-        for (int x = 0; x < S; ++x) {
-            const size_t col = (size_t)(y0 + y) * tr.dim + (x0 + x);
-            const int h = tr.heights[col], top = tr.tops[col];
-            uint8_t *v = &vox[((size_t)y * S + x) * S];   // z fastest
-            for (int z = 0; z < S; ++z) {
-                const uint32_t val = och_terrain::voxel_value(kTables, x0 + x, y0 + y, z0 + z, h, top, tr.tunnels);
-                v[z] = (uint8_t)val;
-                st.hist[val & 7]++;
-            }
-        }
-    // h = 0: children are voxels, child index c = x | y << 1 | z << 2
-    int n = S / 2;
-    for (int z = 0; z < n; ++z)
-        for (int y = 0; y < n; ++y)
-            for (int x = 0; x < n; ++x) {
-                uint32_t c[8];
-                bool any = false;
-                for (int k = 0; k < 8; ++k) {
-                    const int vx = 2 * x + (k & 1), vy = 2 * y + ((k >> 1) & 1), vz = 2 * z + ((k >> 2) & 1);
-                    c[k] = vox[((size_t)vy * S + vx) * S + vz];
-                    any |= c[k] != 0;
-                }
-                uint32_t id = 0;
-                if (any) {
-                    id = ns.intern(c, 0);
-                    ++st.tree_nodes;
-                }
-                ids[((size_t)z * n + y) * n + x] = id;
-            }
-    // h >= 1: reduce in place ((z*n+y)*n+x indexing, n halves each level)
+    int n = (1 << s_log2) / 2;
     for (int h = 1; h < s_log2; ++h) {
         const int m = n / 2;
         for (int z = 0; z < m; ++z)
@@ -255,6 +249,237 @@ uint32_t build_brick(const Terrain &tr, NodeStore &ns, int s_log2, int bx, int b
         n = m;
     }
     return ids[0];
+}
+
+// Voxelise one brick of side S at (bx, by, bz) (brick units) and reduce it to
+// its subtree root.  vox: S^3 scratch, ids: (S/2)^3 scratch.
+uint32_t build_brick(const Terrain &tr, NodeStore &ns, int s_log2, int bx, int by, int bz, std::vector<uint8_t> &vox,
+                     std::vector<uint32_t> &ids, BrickStats &st)
+{
+    const int S = 1 << s_log2;
+    const int x0 = bx * S, y0 = by * S, z0 = bz * S;
+    for (int y = 0; y < S; ++y)
+        for (int x = 0; x < S; ++x) {
+            const size_t col = (size_t)(y0 + y) * tr.dim + (x0 + x);
+            const int h = tr.heights[col], top = tr.tops[col];
+            uint8_t *v = &vox[((size_t)y * S + x) * S];   // z fastest
+            for (int z = 0; z < S; ++z) {
+                const uint32_t val = och_terrain::voxel_value(kTables, x0 + x, y0 + y, z0 + z, h, top, tr.tunnels);
+                v[z] = (uint8_t)val;
+                st.hist[val & 7]++;
+            }
+        }
+    // h = 0: children are voxels, child index c = x | y << 1 | z << 2
+    const int n = S / 2;
+    for (int z = 0; z < n; ++z)
+        for (int y = 0; y < n; ++y)
+            for (int x = 0; x < n; ++x) {
+                uint32_t c[8];
+                bool any = false;
+                for (int k = 0; k < 8; ++k) {
+                    const int vx = 2 * x + (k & 1), vy = 2 * y + ((k >> 1) & 1), vz = 2 * z + ((k >> 2) & 1);
+                    c[k] = vox[((size_t)vy * S + vx) * S + vz];
+                    any |= c[k] != 0;
+                }
+                uint32_t id = 0;
+                if (any) {
+                    id = ns.intern(c, 0);
+                    ++st.tree_nodes;
+                }
+                ids[((size_t)z * n + y) * n + x] = id;
+            }
+    return reduce_brick(ns, s_log2, ids, st);
+}
+
+// ------------------------------------------------------------ GPU voxelisation
+
+constexpr int kBrickLog2 = 5, kBrick = 32, kLeaves = 4096;   // 32^3 voxels, 16^3 leaf-level nodes
+constexpr uint32_t kMixed = 0xFFFFFFFFu;
+
+__constant__ och_terrain::Tables c_tables = {OCH_PERM_TABLE, OCH_GRAD_TABLE};
+
+// One workgroup per brick (bricks[i] = bx | by << 10 | bz << 20): the 4096
+// leaf codes, (z * 16 + y) * 16 + x order; info[i] = {the common code when
+// every leaf is equal, else kMixed; voxel counts of ids 0..7}.
+__global__ __launch_bounds__(256) void k_brick_codes(const int32_t *__restrict__ heights, const uint8_t *__restrict__ tops,
+                                                     int dim, int tunnels, const uint32_t *__restrict__ bricks,
+                                                     uint32_t *__restrict__ codes, uint32_t *__restrict__ info)
+{
+    __shared__ och_terrain::Tables T;
+    __shared__ uint32_t hist[8], firsts[256];
+    __shared__ int mixed;
+    for (int i = threadIdx.x; i < (int)sizeof(T); i += blockDim.x)
+        reinterpret_cast<uint8_t *>(&T)[i] = reinterpret_cast<const uint8_t *>(&c_tables)[i];
+    if (threadIdx.x < 8) hist[threadIdx.x] = 0;
+    if (threadIdx.x == 0) mixed = 0;
+    __syncthreads();
+    const uint32_t b = bricks[blockIdx.x];
+    const int x0 = (int)(b & 1023u) * kBrick, y0 = (int)((b >> 10) & 1023u) * kBrick, z0 = (int)(b >> 20) * kBrick;
+    uint32_t cnt[5] = {0, 0, 0, 0, 0}, other = 0;
+    uint32_t first = 0;
+    bool same = true;
+    for (int leaf = threadIdx.x; leaf < kLeaves; leaf += blockDim.x) {
+        const int lx = leaf & 15, ly = (leaf >> 4) & 15, lz = leaf >> 8;
+        uint32_t code = 0;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const int x = x0 + 2 * lx + (k & 1), y = y0 + 2 * ly + ((k >> 1) & 1), z = z0 + 2 * lz + ((k >> 2) & 1);
+            const size_t col = (size_t)y * dim + x;
+            const uint32_t v = och_terrain::voxel_value(T, x, y, z, heights[col], tops[col], tunnels != 0);
+            code |= (v & 7u) << (3 * k);
+            if (v < 5) ++cnt[v];
+            else ++other;
+        }
+        codes[(size_t)blockIdx.x * kLeaves + leaf] = code;
+        if (leaf == (int)threadIdx.x) first = code;
+        same &= code == first;
+    }
+    for (int v = 0; v < 5; ++v)
+        if (cnt[v]) atomicAdd(&hist[v], cnt[v]);
+    if (other) atomicAdd(&hist[5], other);        // ids above 4 do not occur in this terrain
+    firsts[threadIdx.x] = first;
+    if (!same) mixed = 1;
+    __syncthreads();
+    if (firsts[threadIdx.x] != firsts[0]) mixed = 1;
+    __syncthreads();
+    if (threadIdx.x == 0) info[(size_t)blockIdx.x * 8] = mixed ? kMixed : firsts[0];
+    if (threadIdx.x < 6) info[(size_t)blockIdx.x * 8 + 1 + threadIdx.x] = hist[threadIdx.x];
+}
+
+#define BUILD_HIP(expr)                       \
+    do {                                      \
+        if ((expr) != hipSuccess) return false; \
+    } while (0)
+
+// Voxelise `work` on the current GPU in batches and hash-cons the codes on
+// `threads` host threads, overlapping batch k + 1 on the GPU with batch k on
+// the host.  Returns false when the GPU path is unavailable (the caller then
+// builds on the host); node ids written so far are dropped by the renumbering.
+bool build_bricks_gpu(const Terrain &tr, NodeStore &ns, int threads, const std::vector<uint32_t> &work, int G,
+                      std::vector<uint32_t> &brick_root, std::vector<BrickStats> &stats, double *gpu_seconds)
+{
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return false;
+    const size_t n_work = work.size();
+    const size_t B = 4096;                        // bricks per batch: 64 MiB of codes
+    int32_t *d_heights = nullptr;
+    uint8_t *d_tops = nullptr;
+    uint32_t *d_bricks[2] = {nullptr, nullptr}, *d_codes[2] = {nullptr, nullptr}, *d_info[2] = {nullptr, nullptr};
+    uint32_t *h_codes[2] = {nullptr, nullptr}, *h_info[2] = {nullptr, nullptr}, *h_bricks[2] = {nullptr, nullptr};
+    hipStream_t st[2] = {nullptr, nullptr};
+    hipEvent_t done[2] = {nullptr, nullptr};
+    auto cleanup = [&] {
+        for (int k = 0; k < 2; ++k) {
+            if (st[k]) (void)hipStreamSynchronize(st[k]);
+            if (d_bricks[k]) (void)hipFree(d_bricks[k]);
+            if (d_codes[k]) (void)hipFree(d_codes[k]);
+            if (d_info[k]) (void)hipFree(d_info[k]);
+            if (h_codes[k]) (void)hipHostFree(h_codes[k]);
+            if (h_info[k]) (void)hipHostFree(h_info[k]);
+            if (h_bricks[k]) (void)hipHostFree(h_bricks[k]);
+            if (done[k]) (void)hipEventDestroy(done[k]);
+            if (st[k]) (void)hipStreamDestroy(st[k]);
+        }
+        if (d_heights) (void)hipFree(d_heights);
+        if (d_tops) (void)hipFree(d_tops);
+    };
+    auto run = [&]() -> bool {
+        const size_t cols = (size_t)tr.dim * tr.dim;
+        BUILD_HIP(hipMalloc(&d_heights, cols * 4));
+        BUILD_HIP(hipMalloc(&d_tops, cols));
+        BUILD_HIP(hipMemcpy(d_heights, tr.heights.data(), cols * 4, hipMemcpyHostToDevice));
+        BUILD_HIP(hipMemcpy(d_tops, tr.tops.data(), cols, hipMemcpyHostToDevice));
+        for (int k = 0; k < 2; ++k) {
+            BUILD_HIP(hipStreamCreateWithFlags(&st[k], hipStreamNonBlocking));
+            BUILD_HIP(hipEventCreateWithFlags(&done[k], hipEventDisableTiming));
+            BUILD_HIP(hipMalloc(&d_bricks[k], B * 4));
+            BUILD_HIP(hipMalloc(&d_codes[k], B * kLeaves * 4));
+            BUILD_HIP(hipMalloc(&d_info[k], B * 8 * 4));
+            BUILD_HIP(hipHostMalloc(&h_codes[k], B * kLeaves * 4, hipHostMallocDefault));
+            BUILD_HIP(hipHostMalloc(&h_info[k], B * 8 * 4, hipHostMallocDefault));
+            BUILD_HIP(hipHostMalloc(&h_bricks[k], B * 4, hipHostMallocDefault));
+        }
+        const size_t n_batches = (n_work + B - 1) / B;
+        auto launch = [&](size_t batch) -> bool {
+            const int k = (int)(batch & 1);
+            const size_t lo = batch * B, n = std::min(B, n_work - lo);
+            for (size_t i = 0; i < n; ++i) {
+                const uint32_t w = work[lo + i];
+                const uint32_t bx = w % G, by = (w / G) % G, bz = w / (G * G);
+                h_bricks[k][i] = bx | by << 10 | bz << 20;
+            }
+            BUILD_HIP(hipMemcpyAsync(d_bricks[k], h_bricks[k], n * 4, hipMemcpyHostToDevice, st[k]));
+            hipLaunchKernelGGL(k_brick_codes, dim3((unsigned)n), dim3(256), 0, st[k], d_heights, d_tops, tr.dim,
+                               tr.tunnels ? 1 : 0, d_bricks[k], d_codes[k], d_info[k]);
+            BUILD_HIP(hipGetLastError());
+            BUILD_HIP(hipMemcpyAsync(h_codes[k], d_codes[k], n * kLeaves * 4, hipMemcpyDeviceToHost, st[k]));
+            BUILD_HIP(hipMemcpyAsync(h_info[k], d_info[k], n * 8 * 4, hipMemcpyDeviceToHost, st[k]));
+            BUILD_HIP(hipEventRecord(done[k], st[k]));
+            return true;
+        };
+        // Bricks whose 4096 leaves are one repeated code reduce to the same root.
+        std::mutex memo_mu;
+        std::unordered_map<uint32_t, std::pair<uint32_t, uint64_t>> memo;   // code -> (root, tree nodes)
+        std::vector<std::vector<uint32_t>> ids(threads, std::vector<uint32_t>(kLeaves));
+        const auto t0 = std::chrono::steady_clock::now();
+        if (n_batches && !launch(0)) return false;
+        for (size_t batch = 0; batch < n_batches; ++batch) {
+            const int k = (int)(batch & 1);
+            BUILD_HIP(hipEventSynchronize(done[k]));
+            // the other buffer is free: its batch was consumed in the previous round
+            if (batch + 1 < n_batches && !launch(batch + 1)) return false;
+            const size_t lo = batch * B, n = std::min(B, n_work - lo);
+            const uint32_t *codes = h_codes[k], *info = h_info[k];
+            parallel_for(threads, n, [&](uint64_t i, int t) {
+                BrickStats &bs = stats[t];
+                const uint32_t *inf = info + i * 8;
+                for (int v = 0; v < 6; ++v) bs.hist[v] += inf[1 + v];
+                // an expanded tree (dedup = 0) shares nothing: every brick reduced on its own
+                const uint32_t uni = ns.dedup ? inf[0] : kMixed;
+                uint32_t root = 0;
+                if (uni != kMixed) {
+                    {
+                        std::lock_guard<std::mutex> g(memo_mu);
+                        auto it = memo.find(uni);
+                        if (it != memo.end()) {
+                            bs.tree_nodes += it->second.second;
+                            brick_root[work[lo + i]] = it->second.first;
+                            return;
+                        }
+                    }
+                    BrickStats one;
+                    std::vector<uint32_t> &id = ids[t];
+                    const uint32_t leaf = uni ? ns.intern_code(uni) : 0;
+                    std::fill(id.begin(), id.end(), leaf);
+                    one.tree_nodes = uni ? (uint64_t)kLeaves : 0;
+                    root = reduce_brick(ns, kBrickLog2, id, one);
+                    bs.tree_nodes += one.tree_nodes;
+                    std::lock_guard<std::mutex> g(memo_mu);
+                    memo.emplace(uni, std::make_pair(root, one.tree_nodes));
+                } else {
+                    std::vector<uint32_t> &id = ids[t];
+                    const uint32_t *c = codes + i * kLeaves;
+                    uint32_t last_code = 0, last_id = 0;
+                    for (int l = 0; l < kLeaves; ++l) {
+                        const uint32_t code = c[l];
+                        if (code != last_code || !ns.dedup) {
+                            last_code = code;
+                            last_id = code ? ns.intern_code(code) : 0;
+                        }
+                        id[l] = last_id;
+                        bs.tree_nodes += code != 0;
+                    }
+                    root = reduce_brick(ns, kBrickLog2, id, bs);
+                }
+                brick_root[work[lo + i]] = root;
+            });
+        }
+        if (gpu_seconds) *gpu_seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        return true;
+    };
+    const bool ok = run();
+    cleanup();
+    return ok;
 }
 
 }  // namespace
@@ -327,7 +552,13 @@ OCH_API int och_build_terrain(const och_terrain_params *params, och_host_pool *o
                 if (bz * S <= tr.brick_hmax[(size_t)by * G + bx]) work.push_back(((uint32_t)bz * G + by) * G + bx);
     std::vector<uint32_t> brick_root((size_t)G * G * G, 0);
     std::vector<BrickStats> stats(threads);
-    {
+    double gpu_s = 0.0;
+    if (params->use_gpu && s_log2 == kBrickLog2) {
+        if (!build_bricks_gpu(tr, ns, threads, work, G, brick_root, stats, &gpu_s)) {
+            ns.release();
+            return OCH_E_NODEV;   // asked for the GPU and none could run the voxel kernel
+        }
+    } else {
         std::vector<std::vector<uint8_t>> vox(threads, std::vector<uint8_t>((size_t)S * S * S));
         std::vector<std::vector<uint32_t>> ids(threads, std::vector<uint32_t>((size_t)S * S * S / 8));
         parallel_for(threads, work.size(), [&](uint64_t i, int t) {

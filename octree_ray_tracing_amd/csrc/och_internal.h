@@ -27,6 +27,8 @@ struct DevPool {
     int32_t lut_shift;
     uint32_t miss_bits;     // hit_time bits of a miss (+INF or +0.0)
     float half_voxel;       // voxel_dim / 2 = 2^-(depth+1) (ORT/och_h_octree.h:28), bounce origins
+    uint32_t dim_lo;        // child-size bit at the leaf level, 1 << (23 - depth)
+    uint32_t dim_span;      // (1 << 22) - dim_lo: a walk is active while dim - dim_lo <= dim_span
 };
 
 // The editor's flush (och_editor.cpp) writes a 1-based pool in three steps:

@@ -110,6 +110,18 @@ __device__ __forceinline__ void ray_push(Ray &r, const DevPool &P)
 #endif
 }
 
+#ifndef OCH_MERGED_DESCEND
+#define OCH_MERGED_DESCEND 1
+#endif
+// OCH_DIM_LEVEL: no level counter; the level is implied by the child-size bit
+// (level L <-> dim = 1 << (23 - L)): a MISS shifts dim past 1 << 22, a HIT
+// below 1 << (23 - depth), so the walk is active while dim stays in range.
+#ifndef OCH_DIM_LEVEL
+#define OCH_DIM_LEVEL 0
+#endif
+template <bool kCount>
+__device__ __forceinline__ void ray_push_descend(Ray &r, const DevPool &P, uint32_t stride);
+
 // Setup, ORT/och_h_octree.h:294-338, then the first PUSH at the root.
 // stack: this lane's first LDS slot.
 // stack: this lane's LDS column, depth + 1 slots `stride` words apart.
@@ -145,12 +157,15 @@ __device__ __forceinline__ void ray_init(Ray &r, const DevPool &P, const float *
     r.cur = P.root;
     r.sp = stack + stride;                                                  // slot 0: the miss POP's dummy read
     r.t_min = 0;                                                            // +0.0F
-    r.level = 1;
+    if (!OCH_DIM_LEVEL) r.level = 1;
     r.min_axis = 8;
     set_mode(r, kAtPush);
     r.child = 0;
     r.push = 0;
-    ray_push<kPacked, true>(r, P);
+    if (kPacked && OCH_MERGED_DESCEND)
+        ray_push_descend<true>(r, P, stride);
+    else
+        ray_push<kPacked, true>(r, P);
 }
 
 // The PUSH / STEP / POP machine (ORT/och_h_octree.h:342-446,
@@ -194,15 +209,15 @@ __device__ __forceinline__ void ray_phase_step(Ray &r, uint32_t stride)
     // POP :421-446.  At the root this is the MISS (:423-431): level 0 ends
     // the ray, and the rest of the POP runs on dead state (its stack read
     // lands in the column's spare slot 0) rather than behind a branch.
-    --r.level;
+    if (!OCH_DIM_LEVEL) --r.level;
     r.sp -= stride;
     r.cur = *r.sp;                                                      // :434
 #pragma unroll
     for (int a = 0; a < 3; ++a) r.p[a] &= ~r.dim;                       // :436
     r.dim <<= 1;                                                        // :438
     const uint32_t k = __builtin_ctz(r.dim);                            // :440-444, bit k of each position
-    r.idx = __builtin_amdgcn_ubfe(r.p[0], k, 1) | (__builtin_amdgcn_ubfe(r.p[1], k, 1) << 1) |
-            (__builtin_amdgcn_ubfe(r.p[2], k, 1) << 2);
+    r.idx = (((__builtin_amdgcn_ubfe(r.p[2], k, 1) << 1) | __builtin_amdgcn_ubfe(r.p[1], k, 1)) << 1) |
+            __builtin_amdgcn_ubfe(r.p[0], k, 1);
 }
 
 template <bool kPacked>
@@ -219,7 +234,7 @@ __device__ __forceinline__ void ray_phase_descend(Ray &r, const DevPool &P, uint
     // stays in r.child (no later load overwrites a finished lane's), and the
     // rest of the descent runs on dead state (its stack write lands in the
     // column's spare top slot) rather than behind a branch.
-    ++r.level;
+    if (!OCH_DIM_LEVEL) ++r.level;
     *r.sp = r.cur;                                                          // :357
     r.sp += stride;
     r.cur = child;
@@ -239,12 +254,57 @@ __device__ __forceinline__ void ray_phase_descend(Ray &r, const DevPool &P, uint
 // Still walking: level in 1..depth (0 = missed, depth + 1 = hit).
 __device__ __forceinline__ bool ray_active(const Ray &r, const DevPool &P)
 {
+    if (OCH_DIM_LEVEL) return r.dim - P.dim_lo <= P.dim_span;
     return (uint32_t)(r.level - 1) < (uint32_t)P.depth;
+}
+
+// Packed layout, PUSH and descent in one phase (OCH_MERGED_DESCEND): the
+// child's presence is a bit of the held node word and the descent's
+// geometry (:357-373) does not depend on the child's own slot word, so a
+// PUSH that finds its child descends at once; only the child's word -- the
+// node of the next PUSH, or the voxel id of a HIT -- is loaded, and the next
+// PUSH takes it (mode kPending) after the other lanes' STEP phase has hidden
+// the load.  Two phases per iteration instead of three.
+template <bool kCount>
+__device__ __forceinline__ void ray_push_descend(Ray &r, const DevPool &P, uint32_t stride)
+{
+    r.cur = in_mode(r, kPending) ? r.child : r.cur;
+    if (kCount) ++r.push;
+    const uint32_t c24 = r.idx ^ r.inv;                                     // 24 + child index
+    const uint32_t present = __builtin_amdgcn_ubfe(r.cur, c24, 1u);
+    set_mode(r, kStepping + present);                                       // kStepping or kPending
+    asm volatile("" : "+v"(r.mode));
+    if (!present) return;
+    // 32-bit byte offset from the uniform base: one scaled add, SGPR base address
+    const uint32_t off = ((r.cur & kIdMask) << 5) + (c24 << 2);
+    r.child = *reinterpret_cast<const uint32_t *>(reinterpret_cast<const char *>(P.nodes) - 96 + off);
+    // descent (:357-373); at the leaf level this is the HIT (:346-355): level
+    // becomes depth + 1, the stack write lands in the spare top slot
+    if (!OCH_DIM_LEVEL) ++r.level;
+    *r.sp = r.cur;
+    r.sp += stride;
+    r.dim >>= 1;
+    const float tm = ffrom(r.t_min);
+    uint32_t nidx = 0;
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        const uint32_t mid = r.p[a] | r.dim;
+        const bool upper = __builtin_fmaf(ffrom(mid), r.c[a], r.b[a]) >= tm;
+        nidx |= (uint32_t)upper << a;
+        r.p[a] = upper ? mid : r.p[a];
+    }
+    r.idx = nidx;
 }
 
 template <bool kPacked, bool kCount>
 __device__ __forceinline__ void ray_iterate(Ray &r, const DevPool &P, uint32_t stride)
 {
+    if (kPacked && OCH_MERGED_DESCEND) {
+        if (in_mode(r, kStepping)) ray_phase_step<kPacked>(r, stride);
+        // no activity test: a miss leaves the lane kStepping, a HIT ends in this phase
+        if (!in_mode(r, kStepping)) ray_push_descend<kCount>(r, P, stride);
+        return;
+    }
     if (!kPacked && in_mode(r, kPending)) ray_phase_descend<kPacked>(r, P, stride);
     if (in_mode(r, kStepping)) ray_phase_step<kPacked>(r, stride);
     if (kPacked && in_mode(r, kPending)) ray_phase_descend<kPacked>(r, P, stride);
@@ -255,7 +315,7 @@ __device__ __forceinline__ void ray_iterate(Ray &r, const DevPool &P, uint32_t s
 __device__ __forceinline__ Hit ray_result(const Ray &r, const DevPool &P)
 {
     Hit h;
-    if (r.level == 0) {
+    if (OCH_DIM_LEVEL ? r.dim > (1u << 22) : r.level == 0) {
         h.dir = OCH_EXIT;
         h.voxel = 0;
         h.t = P.miss_bits;
@@ -732,6 +792,7 @@ __global__ void k_trace_refill(DevPool P, Src S, Sink K, uint32_t chunk_rays, in
     const uint32_t end = min(cursor + chunk_rays, n);
     Ray r;
     r.level = 0;                                                    // no ray: not active
+    r.dim = 0;
     uint32_t out = kNoRay;
     uint64_t finished = 0;
     const uint64_t below = (1ull << lane) - 1ull;

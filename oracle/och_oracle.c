@@ -492,6 +492,23 @@ ORA_API uint32_t ora_voxel(int x, int y, int z, int h, int top, int tunnels)
     return 1;
 }
 
+/* The whole height map, row-major h[y * dim + x]. */
+ORA_API void ora_height_map(int dim, int32_t *h)
+{
+    for (int y = 0; y < dim; ++y)
+        for (int x = 0; x < dim; ++x) h[(size_t)y * dim + x] = ora_height(x, y, dim);
+}
+
+/* ora_voxel at n points (x, y, z triples) of a dim^3 world; tops = the
+ * dim x dim column tops (ora_column_tops).  Test helper for large trees. */
+ORA_API void ora_voxel_batch(int dim, const int32_t *xyz, uint64_t n, const uint8_t *tops, int tunnels, uint32_t *out)
+{
+    for (uint64_t i = 0; i < n; ++i) {
+        const int x = xyz[3 * i], y = xyz[3 * i + 1], z = xyz[3 * i + 2];
+        out[i] = ora_voxel(x, y, z, ora_height(x, y, dim), tops[(size_t)y * dim + x], tunnels);
+    }
+}
+
 /* ---------------------------------------------------- small DAG builder */
 
 /* Hash-consed bottom-up build of the terrain for small depths (<= 9): the

@@ -83,6 +83,10 @@ def lib():
         L.ora_is_tunnel.argtypes = [C.c_int] * 3
         L.ora_voxel.restype = C.c_uint32
         L.ora_voxel.argtypes = [C.c_int] * 6
+        L.ora_height_map.restype = None
+        L.ora_height_map.argtypes = [C.c_int, C.c_void_p]
+        L.ora_voxel_batch.restype = None
+        L.ora_voxel_batch.argtypes = [C.c_int, C.c_void_p, C.c_uint64, C.c_void_p, C.c_int, C.c_void_p]
         L.ora_build_terrain.restype = C.c_uint32
         L.ora_build_terrain.argtypes = [C.c_int, C.c_int, C.c_int, C.POINTER(C.c_void_p), C.POINTER(C.c_uint32)]
         L.ora_free.restype = None
@@ -245,6 +249,22 @@ def is_tunnel(x: int, y: int, z: int) -> bool:
 
 def voxel(x, y, z, h, top, tunnels=True) -> int:
     return lib().ora_voxel(x, y, z, h, top, int(tunnels))
+
+
+def height_map(dim: int) -> np.ndarray:
+    """ora_height for every column: (dim, dim) int32 indexed [y, x]."""
+    h = np.empty(dim * dim, np.int32)
+    lib().ora_height_map(dim, _ptr(h))
+    return h.reshape(dim, dim)
+
+
+def voxels_at(dim: int, xyz: np.ndarray, tops: np.ndarray, tunnels: bool = True) -> np.ndarray:
+    """ora_voxel at many points (n x 3 int32), closed form (ORT/test_och_h_octree.cpp:767-787)."""
+    xyz = np.ascontiguousarray(xyz, np.int32).reshape(-1, 3)
+    tops = np.ascontiguousarray(tops, np.uint8)
+    out = np.empty(xyz.shape[0], np.uint32)
+    lib().ora_voxel_batch(dim, _ptr(xyz), xyz.shape[0], _ptr(tops), int(tunnels), _ptr(out))
+    return out
 
 
 def build_terrain(depth: int, tunnels: bool = True, dedup: bool = True) -> OraclePool:

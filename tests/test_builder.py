@@ -165,3 +165,89 @@ def test_pool_file_header_corruption(ort, tmp_path):
     p.write_bytes(bytes(v1))
     back = ort.NodePool.load(p)
     assert np.array_equal(back.nodes, tree.nodes) and back.root == tree.root
+
+
+def pool_at_many(nodes, root, depth, xyz):
+    """h_octree::at (ORT/och_h_octree.h:239-258) at many points, vectorised over a 1-based pool."""
+    xyz = np.asarray(xyz, np.int64)
+    cur = np.full(xyz.shape[0], root, np.int64)
+    out = np.zeros(xyz.shape[0], np.uint32)
+    live = np.ones(xyz.shape[0], bool)
+    for level in range(depth - 1, -1, -1):
+        c = ((xyz[:, 0] >> level) & 1) | (((xyz[:, 1] >> level) & 1) << 1) | (((xyz[:, 2] >> level) & 1) << 2)
+        nxt = np.where(live, nodes[np.maximum(cur - 1, 0), c], 0).astype(np.int64)
+        if level == 0:
+            out = nxt.astype(np.uint32)
+        live &= nxt != 0
+        cur = nxt
+    return np.where(live | (out != 0), out, 0).astype(np.uint32)
+
+
+@pytest.mark.slow
+def test_d12_tree_pinned(ort, O, known):
+    """The headline workload's tree (depth 12, 4096^3), built in parallel by
+    och_build_terrain, against the oracle's closed-form voxel function
+    (ORT/test_och_h_octree.cpp:561-787, ORT/och_noise.h:73-366): 10^6 random
+    voxels, every column's top voxel, and +-2 voxels around tunnel boundaries
+    found along 2 000 random columns.  Node counts and the pool checksum are
+    pinned (SURVEY §6.1 has no depth-12 figures: pinned by this build, and
+    every GPU depth-12 parity test runs on this exact pool)."""
+    import zlib
+    depth, dim = 12, 4096
+    tree = ort.build_terrain(depth)
+    k = known["terrain_d12"]
+    assert tree.n_nodes == k["unique_nodes"] and tree.tree_nodes == k["tree_nodes"]
+    assert tree.solid_voxels == k["solid_voxels"]
+    assert zlib.crc32(tree.nodes.astype("<u4").tobytes()) == k["pool_crc32"]
+    tops = O.column_tops(dim)
+    hmap = O.height_map(dim)
+    rng = np.random.default_rng(12)
+    # 10^6 random voxels, half of them in the band the surface and tunnels cross
+    pts = rng.integers(0, dim, (1_000_000, 3)).astype(np.int32)
+    pts[:500_000, 2] = rng.integers(0, int(hmap.max()) + 3, 500_000)
+    assert np.array_equal(pool_at_many(tree.nodes, tree.root, depth, pts), O.voxels_at(dim, pts, tops))
+    # every column's top voxel (x, y, h(x, y)) and the two under it
+    ys, xs = np.mgrid[0:dim, 0:dim]
+    for dz in (0, -1, -2):
+        xyz = np.stack([xs.ravel(), ys.ravel(), hmap.ravel() + dz], 1).astype(np.int32)
+        xyz = xyz[xyz[:, 2] >= 0]
+        for part in np.array_split(xyz, 8):
+            assert np.array_equal(pool_at_many(tree.nodes, tree.root, depth, part), O.voxels_at(dim, part, tops))
+    # 2 000 random columns in full (z = 0 .. h + 2): every tunnel boundary along
+    # them, with the voxels around it, and the column tops
+    n_bound = 0
+    for x, y in rng.integers(0, dim, (2000, 2)).tolist():
+        h = int(hmap[y, x])
+        z = np.arange(0, h + 3, dtype=np.int32)
+        xyz = np.stack([np.full_like(z, x), np.full_like(z, y), z], 1)
+        want = O.voxels_at(dim, xyz, tops)
+        n_bound += int(np.count_nonzero((want[1:] == 0) != (want[:-1] == 0)))
+        assert np.array_equal(pool_at_many(tree.nodes, tree.root, depth, xyz), want), (x, y)
+    assert n_bound > 1000          # the columns do cross tunnels
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("depth,dedup", [(5, True), (8, True), (8, False), (10, True), (12, True)])
+def test_gpu_voxelisation_same_pool(ort, gpu_device, depth, dedup):
+    """use_gpu=1 (k_brick_codes + host hash-consing) builds the host builder's
+    pool slot for slot, with the same statistics; depth 12 is the bench's tree."""
+    import time
+    t0 = time.perf_counter()
+    g = ort.build_terrain(depth, dedup=dedup, use_gpu=True)
+    t_gpu = time.perf_counter() - t0
+    h = ort.build_terrain(depth, dedup=dedup, use_gpu=False)
+    assert (g.root, g.depth, g.index_base) == (h.root, h.depth, h.index_base)
+    assert np.array_equal(g.nodes, h.nodes)
+    assert (g.tree_nodes, g.solid_voxels) == (h.tree_nodes, h.solid_voxels)
+    assert list(g.voxel_hist) == list(h.voxel_hist)
+    print(f"depth {depth}: GPU voxelisation {t_gpu:.2f} s ({g.build_seconds:.2f} s in och_build_terrain), "
+          f"host {h.build_seconds:.2f} s")
+
+
+def test_gpu_voxelisation_needs_a_gpu(ort):
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    with pytest.raises(ort.OchError, match="NODEV"):
+        ort.build_terrain(6, use_gpu=True)
+    assert ort.build_terrain(4, use_gpu=True).n_nodes > 0     # below depth 5: host, as documented

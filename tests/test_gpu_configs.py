@@ -26,7 +26,7 @@ YAW, FOV = 0.3, 1.25
 
 @pytest.fixture(scope="module")
 def d12(ort):
-    return ort.build_terrain(12)
+    return ort.build_terrain(12, use_gpu=True)
 
 
 @pytest.fixture(scope="module")

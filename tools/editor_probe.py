@@ -43,7 +43,7 @@ def main():
     torch.cuda.set_device(0)
     res = {"depth": a.depth}
     t = time.perf_counter()
-    tree = ort.build_terrain(a.depth)
+    tree = ort.build_terrain(a.depth, use_gpu=True)
     res["build_s"] = time.perf_counter() - t
     res["dag_nodes"] = int(tree.nodes.shape[0])
     print("built", res, flush=True)

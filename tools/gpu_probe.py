@@ -29,7 +29,7 @@ def main():
     from oracle import oracle as O
 
     t0 = time.time()
-    tree = ort.build_terrain(a.depth)
+    tree = ort.build_terrain(a.depth, use_gpu=True)
     print(f"build depth {a.depth}: {tree.n_nodes} nodes, {tree.build_seconds:.2f}s", flush=True)
     pool = ort.HOctree(tree.nodes, tree.root, tree.depth, device=0)
     stream = torch.cuda.current_stream()

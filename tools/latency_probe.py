@@ -39,7 +39,7 @@ def main():
         z = np.load(cache)
         nodes, root = z["nodes"], int(z["root"])
     else:
-        tree = ort.build_terrain(a.depth)
+        tree = ort.build_terrain(a.depth, use_gpu=True)
         nodes, root = tree.nodes, tree.root
         np.savez(cache, nodes=nodes, root=root, depth=a.depth)
     pool = ort.HOctree(nodes, root, a.depth, device=0)

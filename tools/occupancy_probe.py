@@ -35,7 +35,7 @@ def main():
     stamps = torch.zeros((1 << 17) * 4, dtype=torch.int64, device=dev)
     frame = torch.empty(1920 * 1080, dtype=torch.int32, device=dev)
     for depth in (4, 8, 12):
-        tree = ort.build_terrain(depth)
+        tree = ort.build_terrain(depth, use_gpu=True)
         pool = ort.HOctree(tree.nodes, tree.root, depth, device=0)
         pool.set_palette(ort.VoxelData().get_colours())
         pool.set_stream(torch.cuda.current_stream())

@@ -91,22 +91,30 @@ static int step_one(Ray *r)
 }
 
 static int SCHED = 0;
+static int THRESH = 0;   /* schedule 0: skip a phase needed by fewer than THRESH lanes (at most one iteration) */
 
 /* schedule 0: the current kernel (step, descend, push; each phase skipped when no lane needs it) */
 static void wave_sched0(Ray *R, int n, Stats *S)
 {
     for (int i = 0; i < n; ++i) push(&R[i]);
+    int skipped_step = 0, skipped_desc = 0;
     for (;;) {
         int any = 0;
         for (int i = 0; i < n; ++i) any |= active(&R[i]);
         if (!any) break;
         S->iters += 1;
         int ns = 0, nadv = 0, npopper = 0, npop = 0, nd = 0, ndesc = 0, np = 0, nload = 0;
+        int want_step = 0, want_desc = 0;
+        for (int i = 0; i < n; ++i) { want_step += active(&R[i]) && R[i].stepping; want_desc += R[i].pending; }
+        const int run_step = want_step >= THRESH || skipped_step;
+        const int run_desc = want_desc >= THRESH || skipped_desc;
+        skipped_step = want_step && !run_step;
+        skipped_desc = want_desc && !run_desc;
         for (int i = 0; i < n; ++i) {
             Ray *r = &R[i];
             if (!active(r)) continue;
             ++r->iters;
-            if (r->stepping) {
+            if (r->stepping && run_step) {
                 ++ns; ++r->step;
                 uint32_t t[3];
                 for (int a = 0; a < 3; ++a) t[a] = f2u(fmaf(u2f(r->p[a]), r->c[a], r->b[a]));
@@ -128,7 +136,7 @@ static void wave_sched0(Ray *R, int n, Stats *S)
         }
         for (int i = 0; i < n; ++i) {
             Ray *r = &R[i];
-            if (!r->pending) continue;
+            if (!r->pending || !run_desc) continue;
             r->pending = 0; ++nd;
             if (r->level == DEPTH) { r->level = DEPTH + 1; continue; }
             ++ndesc;
@@ -144,7 +152,7 @@ static void wave_sched0(Ray *R, int n, Stats *S)
         int fresh[64] = {0};
         for (int i = 0; i < n; ++i) {
             Ray *r = &R[i];
-            if (r->stepping || !active(r)) continue;
+            if (r->stepping || r->pending || !active(r)) continue;
             ++np; push(r); nload += r->pending;
             fresh[i] = r->stepping;
         }
@@ -205,6 +213,7 @@ int main(int argc, char **argv)
     const float pitch = (float)atof(argv[3]);
     const int stride = argc > 4 ? atoi(argv[4]) : 1;
     SCHED = argc > 5 ? atoi(argv[5]) : 0;
+    THRESH = argc > 6 ? atoi(argv[6]) : 0;
     const int W = 1920, H = 1080;
     const float o[3] = {1.5F, 1.5F, 1.5F};
     Stats S = {0};

@@ -37,7 +37,7 @@ def main():
         z = np.load(cache)
         nodes, root = z["nodes"], int(z["root"])
     else:
-        tree = ort.build_terrain(depth)
+        tree = ort.build_terrain(depth, use_gpu=True)
         nodes, root = tree.nodes, tree.root
         np.savez(cache, nodes=nodes, root=root, depth=depth)
     pool = ort.HOctree(nodes, root, depth, device=0)

@@ -52,7 +52,7 @@ def main():
 
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(0)
-    tree = ort.build_terrain(a.depth)
+    tree = ort.build_terrain(a.depth, use_gpu=True)
     print(f"depth {a.depth}: {tree.n_nodes} nodes, built in {tree.build_seconds:.1f}s", flush=True)
     pool = ort.HOctree(tree.nodes, tree.root, a.depth, device=0)
     pool.set_palette(ort.VoxelData().get_colours())
