@@ -145,6 +145,7 @@ struct och_gpu_pool {
     uint32_t *d_packed = nullptr;
     uint32_t packed_root = 0;
     uint32_t packed_nodes = 0;
+    uint32_t packed_top_ids[5] = {1, 1, 1, 1, 1};   // first id past levels 1..T
     bool packed_by_slot = false;    // d_packed numbered like d_nodes (editor flushes)
     uint64_t serial = 0;            // process-unique, never reused (och::pool_serial)
     uint64_t last_writer = 0;       // editor id of the last och::pool_commit, 0 otherwise
@@ -188,6 +189,7 @@ struct och_gpu_pool {
         std::memcpy(&mb, &miss_t, 4);
         p.miss_bits = mb;
         p.half_voxel = std::ldexp(1.0F, -(depth + 1));
+        for (int t = 0; t < 5; ++t) p.top_ids[t] = pk && !packed_by_slot ? packed_top_ids[t] : 1u;
         p.dim_lo = 1u << (23 - depth);
         p.dim_span = (1u << 22) - p.dim_lo;
         return p;
@@ -247,7 +249,7 @@ int validate_pool(const uint32_t *nodes, uint32_t n_nodes, uint32_t root, int de
 // alone) is simply emitted once per level.  Returns false when more than
 // 2^24 - 1 ids would be needed.
 bool pack_pool(const uint32_t *nodes, uint32_t n_nodes, uint32_t root, int depth, int base,
-               std::vector<uint32_t> &out, uint32_t &packed_root)
+               std::vector<uint32_t> &out, uint32_t &packed_root, uint32_t *top_ids = nullptr)
 {
     auto mask_of = [&](uint32_t v) {
         const uint32_t *c = nodes + (size_t)(v - base) * 8;
@@ -297,6 +299,12 @@ bool pack_pool(const uint32_t *nodes, uint32_t n_nodes, uint32_t root, int depth
             if (c[k]) id_of(c[k], level + 1, true);
         if (next > kIdLimit) return false;
     }
+    if (top_ids)
+        for (int t = 0; t < 5; ++t) {
+            uint32_t n_top = 0;
+            while (n_top < order_l.size() && order_l[n_top] <= t) ++n_top;
+            top_ids[t] = 1 + n_top;                       // ids are breadth-first, 1-based
+        }
     out.resize((size_t)next * 8, 0u);
     for (size_t q = 0; q < order_v.size(); ++q) {
         const uint32_t v = order_v[q];
@@ -320,7 +328,8 @@ int upload_packed(och_gpu_pool *p, const uint32_t *nodes, uint32_t n_nodes)
     p->d_packed = nullptr;
     p->packed_nodes = 0;
     p->packed_by_slot = false;
-    if (!pack_pool(nodes, n_nodes, p->root, p->depth, p->index_base, packed, proot)) return OCH_OK;   // raw only
+    if (!pack_pool(nodes, n_nodes, p->root, p->depth, p->index_base, packed, proot, p->packed_top_ids))
+        return OCH_OK;   // raw only
     OCH_HIP(hipMalloc(&p->d_packed, packed.size() * 4));
     OCH_HIP(hipMemcpy(p->d_packed, packed.data(), packed.size() * 4, hipMemcpyHostToDevice));
     p->packed_root = proot;

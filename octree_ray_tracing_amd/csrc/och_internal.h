@@ -27,6 +27,7 @@ struct DevPool {
     int32_t lut_shift;
     uint32_t miss_bits;     // hit_time bits of a miss (+INF or +0.0)
     float half_voxel;       // voxel_dim / 2 = 2^-(depth+1) (ORT/och_h_octree.h:28), bounce origins
+    uint32_t top_ids[5];    // packed layout: ids below top_ids[T] belong to levels 1..T (OCH_LDS_TOP)
     uint32_t dim_lo;        // child-size bit at the leaf level, 1 << (23 - depth)
     uint32_t dim_span;      // (1 << 22) - dim_lo: a walk is active while dim - dim_lo <= dim_span
 };

@@ -117,10 +117,16 @@ __device__ __forceinline__ void ray_push(Ray &r, const DevPool &P)
 // (level L <-> dim = 1 << (23 - L)): a MISS shifts dim past 1 << 22, a HIT
 // below 1 << (23 - depth), so the walk is active while dim stays in range.
 #ifndef OCH_DIM_LEVEL
-#define OCH_DIM_LEVEL 0
+#define OCH_DIM_LEVEL 1
+#endif
+// OCH_LDS_TOP = T: the grid kernel keeps the packed nodes of levels 1..T in
+// LDS and reads near-root PUSHes from there (experiment, SURVEY §7 kernel notes).
+#ifndef OCH_LDS_TOP
+#define OCH_LDS_TOP 0
 #endif
 template <bool kCount>
-__device__ __forceinline__ void ray_push_descend(Ray &r, const DevPool &P, uint32_t stride);
+__device__ __forceinline__ void ray_push_descend(Ray &r, const DevPool &P, uint32_t stride,
+                                                 const uint32_t *top = nullptr);
 
 // Setup, ORT/och_h_octree.h:294-338, then the first PUSH at the root.
 // stack: this lane's first LDS slot.
@@ -266,7 +272,7 @@ __device__ __forceinline__ bool ray_active(const Ray &r, const DevPool &P)
 // PUSH takes it (mode kPending) after the other lanes' STEP phase has hidden
 // the load.  Two phases per iteration instead of three.
 template <bool kCount>
-__device__ __forceinline__ void ray_push_descend(Ray &r, const DevPool &P, uint32_t stride)
+__device__ __forceinline__ void ray_push_descend(Ray &r, const DevPool &P, uint32_t stride, const uint32_t *top)
 {
     r.cur = in_mode(r, kPending) ? r.child : r.cur;
     if (kCount) ++r.push;
@@ -277,7 +283,10 @@ __device__ __forceinline__ void ray_push_descend(Ray &r, const DevPool &P, uint3
     if (!present) return;
     // 32-bit byte offset from the uniform base: one scaled add, SGPR base address
     const uint32_t off = ((r.cur & kIdMask) << 5) + (c24 << 2);
-    r.child = *reinterpret_cast<const uint32_t *>(reinterpret_cast<const char *>(P.nodes) - 96 + off);
+    if (OCH_LDS_TOP && top && (r.cur & kIdMask) < P.top_ids[OCH_LDS_TOP])
+        r.child = *reinterpret_cast<const uint32_t *>(reinterpret_cast<const char *>(top) - 96 + off);
+    else
+        r.child = *reinterpret_cast<const uint32_t *>(reinterpret_cast<const char *>(P.nodes) - 96 + off);
     // descent (:357-373); at the leaf level this is the HIT (:346-355): level
     // becomes depth + 1, the stack write lands in the spare top slot
     if (!OCH_DIM_LEVEL) ++r.level;
@@ -297,12 +306,12 @@ __device__ __forceinline__ void ray_push_descend(Ray &r, const DevPool &P, uint3
 }
 
 template <bool kPacked, bool kCount>
-__device__ __forceinline__ void ray_iterate(Ray &r, const DevPool &P, uint32_t stride)
+__device__ __forceinline__ void ray_iterate(Ray &r, const DevPool &P, uint32_t stride, const uint32_t *top = nullptr)
 {
     if (kPacked && OCH_MERGED_DESCEND) {
         if (in_mode(r, kStepping)) ray_phase_step<kPacked>(r, stride);
         // no activity test: a miss leaves the lane kStepping, a HIT ends in this phase
-        if (!in_mode(r, kStepping)) ray_push_descend<kCount>(r, P, stride);
+        if (!in_mode(r, kStepping)) ray_push_descend<kCount>(r, P, stride, top);
         return;
     }
     if (!kPacked && in_mode(r, kPending)) ray_phase_descend<kPacked>(r, P, stride);
@@ -667,6 +676,13 @@ __global__ void k_trace_grid(DevPool P, Src S, Sink K, uint32_t xcd_group, uint6
 {
     extern __shared__ uint32_t lds_stack[];
     const uint64_t t0 = stamps ? realtime() : 0;
+    const uint32_t *top = nullptr;
+    if (OCH_LDS_TOP && kPacked) {
+        uint32_t *t = lds_stack + (P.depth + 1) * blockDim.x;
+        for (uint32_t i = threadIdx.x; i < 8u * P.top_ids[OCH_LDS_TOP]; i += blockDim.x) t[i] = P.nodes[i];
+        __syncthreads();
+        top = t;
+    }
     const uint32_t wave_base = xcd_block(blockIdx.x, gridDim.x, xcd_group) * blockDim.x + (threadIdx.x & ~63u);
     const uint32_t lane = threadIdx.x & 63u;
     float o[3], d[3];
@@ -675,7 +691,7 @@ __global__ void k_trace_grid(DevPool P, Src S, Sink K, uint32_t xcd_group, uint6
         Ray r;
         ray_init<kPacked, kCount>(r, P, o, d, lds_stack + threadIdx.x, blockDim.x);
         do {
-            ray_iterate<kPacked, kCount>(r, P, blockDim.x);
+            ray_iterate<kPacked, kCount>(r, P, blockDim.x, top);
         } while (ray_active(r, P));
         K.put(out, ray_result(r, P));
     }
@@ -956,7 +972,8 @@ hipError_t launch_as(const DevPool &p, const Src &s, const Sink &k, uint32_t n, 
 #ifndef OCH_LDS_MIN
 #define OCH_LDS_MIN 0     // occupancy experiments: pad each block's LDS to this many bytes
 #endif
-    const size_t lds = stack_bytes(p.depth, block) > OCH_LDS_MIN ? stack_bytes(p.depth, block) : OCH_LDS_MIN;
+    size_t lds = stack_bytes(p.depth, block) > OCH_LDS_MIN ? stack_bytes(p.depth, block) : OCH_LDS_MIN;
+    if (OCH_LDS_TOP && kPacked && sc.kind == 0) lds += 32u * p.top_ids[OCH_LDS_TOP];
     if (sc.kind == 2) {
         const uint32_t chunk = 64u * (uint32_t)sc.chunk_tiles;
         const uint32_t waves = (n + chunk - 1) / chunk, wpb = (uint32_t)block / 64u;

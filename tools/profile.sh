@@ -8,7 +8,8 @@ TAG=${1:-r01}; shift
 OUT=gpurun_out/prof_$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
-BENCH="python -u bench.py --steps 10 --warmup 3 --no-cpu-baseline $*"
+export OCH_TREE_CACHE=${OCH_TREE_CACHE:-/tmp/och_tree_d12.npz}
+BENCH="python -u bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-parity --sustain 0 $*"
 step() {   # step <name> <rocprofv3 args...>
     local name=$1; shift
     echo "[profile] $name" >&2
@@ -19,5 +20,6 @@ step pmc_fetch --pmc FETCH_SIZE || exit 1
 step pmc_write --pmc WRITE_SIZE || exit 1
 step pmc_tcc --pmc TCC_HIT_sum TCC_MISS_sum || exit 1
 step pmc_sq --pmc SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VMEM_RD SQ_INSTS_LDS || exit 1
+step pmc_sq2 --pmc SQ_INSTS_SALU SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_ANY SQ_WAIT_INST_ANY SQ_WAIT_ANY || exit 1
 step pmc_grbm --pmc GRBM_GUI_ACTIVE || exit 1
 python tools/pmc_summary.py $OUT > $OUT/summary.json

@@ -186,6 +186,73 @@ static void wave_sched0(Ray *R, int n, Stats *S)
     S->waves += 1;
 }
 
+/* schedules 2 and 3: the merged kernel (och_kernels.hip ray_push_descend,
+ * OCH_MERGED_DESCEND): phase A = STEP (+ advance or POP) for stepping lanes,
+ * phase B = PUSH (+ descent when the child is present) for the others.
+ * Schedule 3 repeats phase A for lanes that just popped until none pops.
+ * VALU per block from the gfx950 ISA of the merged loop. */
+enum { M_LOOP = 4, M_AENTRY = 1, M_STEP = 10, M_ADV = 7, M_POP = 15, M_BENTRY = 8, M_DESC = 25 };
+
+static void wave_merged(Ray *R, int n, Stats *S, int popwhile)
+{
+    int mode[64];   /* 0 push, 1 stepping */
+    for (int i = 0; i < n; ++i) mode[i] = R[i].stepping ? 1 : 0;
+    for (;;) {
+        int any = 0;
+        for (int i = 0; i < n; ++i) any |= active(&R[i]);
+        if (!any) break;
+        S->iters += 1;
+        S->valu += M_LOOP + M_AENTRY;
+        int popped[64];
+        for (int i = 0; i < n; ++i) popped[i] = 1;   /* first pass: every stepping lane */
+        for (int pass = 0;; ++pass) {
+            int ns = 0, nadv = 0, npop = 0;
+            int again[64] = {0};
+            for (int i = 0; i < n; ++i) {
+                Ray *r = &R[i];
+                if (!active(r) || mode[i] != 1 || !popped[i]) continue;
+                ++ns;
+                if (pass == 0) ++r->iters;
+                const int k = step_one(r);
+                if (k == 1) { ++nadv; mode[i] = 0; }
+                else { ++npop; again[i] = k == 2; }
+            }
+            if (ns) S->valu += M_STEP;
+            if (nadv) S->valu += M_ADV;
+            if (npop) S->valu += M_POP;
+            if (pass) S->valu += 3;                       /* the repeat test */
+            if (!popwhile) break;
+            int more = 0;
+            for (int i = 0; i < n; ++i) { popped[i] = again[i]; more |= again[i]; }
+            if (!more) break;
+        }
+        int nb = 0, npres = 0;
+        for (int i = 0; i < n; ++i) {
+            Ray *r = &R[i];
+            if (!active(r) || mode[i] != 0) continue;
+            ++nb; ++r->push;
+            const uint32_t ch = N[(size_t)(r->cur - 1) * 8 + ((r->idx ^ r->inv) & 7)];
+            if (!ch) { mode[i] = 1; continue; }
+            ++npres;
+            if (r->level == DEPTH) { r->level = DEPTH + 1; continue; }
+            r->stack[r->sp++] = r->cur; ++r->level; r->cur = ch; r->dim >>= 1;
+            uint32_t ni = 0;
+            for (int a = 0; a < 3; ++a) {
+                const uint32_t mid = r->p[a] | r->dim;
+                const int up = fmaf(u2f(mid), r->c[a], r->b[a]) >= u2f(r->t_min);
+                ni |= up << a; if (up) r->p[a] = mid;
+            }
+            r->idx = ni;
+        }
+        if (nb) S->valu += M_BENTRY;
+        if (npres) S->valu += M_DESC;
+    }
+    for (int i = 0; i < n; ++i) S->rays_it += R[i].iters;
+    S->waves += 1;
+}
+
+static void wave_merged_init(Ray *R, int n, Stats *S, int popwhile) { wave_merged(R, n, S, popwhile); }
+
 static void camera(float yaw, float pitch, int W, int H, int col, int row, float *d)
 {
     /* tree_camera::update_position (ORT/test_och_h_octree.cpp:87-138), float math */
@@ -227,7 +294,28 @@ int main(int argc, char **argv)
                 camera(0.3F, pitch, W, H, tx * 8 + l % 8, ty * 8 + l / 8, d);
                 ray_setup(&R[l], o, d);
             }
-            wave_sched0(R, 64, &S);
+            if (SCHED >= 2) {
+                /* merged kernel: ray_init does the root PUSH + descent itself */
+                for (int l = 0; l < 64; ++l) {
+                    Ray *r = &R[l];
+                    const uint32_t ch = N[(size_t)(r->cur - 1) * 8 + ((r->idx ^ r->inv) & 7)];
+                    ++r->push;
+                    if (!ch) { r->stepping = 1; continue; }
+                    r->stack[r->sp++] = r->cur; ++r->level; r->cur = ch; r->dim >>= 1;
+                    uint32_t ni = 0;
+                    for (int a = 0; a < 3; ++a) {
+                        const uint32_t mid = r->p[a] | r->dim;
+                        const int up = fmaf(u2f(mid), r->c[a], r->b[a]) >= u2f(r->t_min);
+                        ni |= up << a; if (up) r->p[a] = mid;
+                    }
+                    r->idx = ni;
+                }
+                /* mode from the root PUSH: stepping lanes start in phase A */
+                Ray tmp[64];
+                memcpy(tmp, R, sizeof tmp);
+                wave_merged_init(R, 64, &S, SCHED == 3);
+            } else
+                wave_sched0(R, 64, &S);
         }
     printf("{\"waves\": %.0f, \"valu_per_wave\": %.1f, \"iters_per_wave\": %.2f, \"ray_iters\": %.2f, "
            "\"lane_util_iter\": %.3f, \"step_util\": %.3f, \"desc_util\": %.3f, \"push_util\": %.3f, "
