@@ -150,7 +150,9 @@ typedef enum och_option {
                                   (node, level) pairs): per-level breadth-first ids, interior slots carry the
                                   child's occupancy mask so only descents and hits touch memory */
     OCH_OPT_TILE_ORDER = 5,    /* camera rays (render): 0 = 8x8-pixel tiles row-major; 1 = 64x64-pixel supertiles,
-                                  each handed to one XCD so neighbouring rays share that XCD's L2 */
+                                  each handed to one XCD so neighbouring rays share that XCD's L2; 2 = the launch
+                                  order planned by och_gpu_plan_views (costliest tiles first) for frames of the
+                                  planned geometry, else 0.  Dispatch order only: frames are identical */
     OCH_OPT_BOUNCE_COMPACT = 6,/* config 5: 1 (default) = compact each block's secondary rays into its first lanes
                                   (wave ballot/popcount + LDS queue) before tracing them; 0 = trace in place */
     OCH_OPT_CHUNK_TILES = 7    /* schedule 2: 64-ray tiles per wave, a power of two in 1..64 (default 4) */
@@ -223,6 +225,14 @@ OCH_API int och_shard_rows(int height, int row_chunk, int n_shards);
  * One launch keeps the GPU busy with other views while a view's slowest rays finish. */
 OCH_API int och_gpu_render_views_dev(och_gpu_pool *pool, const och_camera *cams, int n_views, uint32_t *rgba_slices,
                                      int row_chunk, int shard, int n_shards);
+/* Plan the launch order of frames of this geometry (size, views, sharding,
+ * block): one render of these cameras times every workgroup, and later
+ * renders with OCH_OPT_TILE_ORDER = 2 dispatch the costliest tiles first, so
+ * a frame does not end on a few late grazing tiles.  Synchronous.  A plan
+ * made from one camera stays valid (and approximately right) while the
+ * camera moves; re-plan at will. */
+OCH_API int och_gpu_plan_views(och_gpu_pool *pool, const och_camera *cams, int n_views, int row_chunk, int shard,
+                               int n_shards);
 /* Config 5 frame: och_gpu_render_views_dev with one bounce per hit; a hit
  * pixel keeps its face colour when its secondary ray escapes (exit) and is
  * halved (RGB >> 1, alpha kept) when the secondary ray is blocked. */

@@ -87,6 +87,7 @@ PROTOTYPES = {
     "och_gpu_render_dev": (C.c_int, [_P, C.POINTER(Camera), _P, C.c_int, C.c_int, C.c_int]),
     "och_shard_rows": (C.c_int, [C.c_int, C.c_int, C.c_int]),
     "och_gpu_render_views_dev": (C.c_int, [_P, _P, C.c_int, _P, C.c_int, C.c_int, C.c_int]),
+    "och_gpu_plan_views": (C.c_int, [_P, _P, C.c_int, C.c_int, C.c_int, C.c_int]),
     "och_gpu_render_bounce_views_dev": (C.c_int, [_P, _P, C.c_int, _P, C.c_int, C.c_int, C.c_int]),
     "och_gpu_unshard_dev": (C.c_int, [_P, _P, _P, C.c_int, C.c_int, C.c_int, C.c_int]),
     "och_gpu_unshard_views_dev": (C.c_int, [_P, _P, _P, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int]),

@@ -87,6 +87,8 @@ struct Schedule {
     uint32_t *counter;      // device ray counter (persistent)
     uint64_t *stamps;       // optional per-wave residency records
     uint32_t stamp_cap;
+    const uint32_t *order;  // grid: optional workgroup permutation (och_gpu_plan_views)
+    uint32_t *cost;         // grid: optional per-workgroup duration output (the planning launch)
 };
 
 hipError_t launch_trace_batch(const DevPool &p, const float *origin, int origin_stride, const float *dirs,

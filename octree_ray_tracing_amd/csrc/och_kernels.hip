@@ -671,11 +671,17 @@ __device__ __forceinline__ uint32_t xcd_block(uint32_t b, uint32_t nb, uint32_t 
     return ((s / group) * 8u + x) * group + s % group;
 }
 
+// order: optional block permutation (a cost-planned launch order: the
+// most expensive workgroups of the planning frame first, so the frame does not
+// end on a few late grazing tiles); cost: optional per-block duration in
+// shader clocks (the planning launch).  Placement only: results are the same.
 template <class Src, class Sink, bool kPacked, bool kCount>
-__global__ void k_trace_grid(DevPool P, Src S, Sink K, uint32_t xcd_group, uint64_t *stamps, uint32_t stamp_cap)
+__global__ void k_trace_grid(DevPool P, Src S, Sink K, uint32_t xcd_group, const uint32_t *__restrict__ order,
+                             uint32_t *__restrict__ cost, uint64_t *stamps, uint32_t stamp_cap)
 {
     extern __shared__ uint32_t lds_stack[];
     const uint64_t t0 = stamps ? realtime() : 0;
+    const uint64_t c0 = cost ? __builtin_amdgcn_s_memtime() : 0;
     const uint32_t *top = nullptr;
     if (OCH_LDS_TOP && kPacked) {
         uint32_t *t = lds_stack + (P.depth + 1) * blockDim.x;
@@ -683,7 +689,8 @@ __global__ void k_trace_grid(DevPool P, Src S, Sink K, uint32_t xcd_group, uint6
         __syncthreads();
         top = t;
     }
-    const uint32_t wave_base = xcd_block(blockIdx.x, gridDim.x, xcd_group) * blockDim.x + (threadIdx.x & ~63u);
+    const uint32_t blk = order ? order[blockIdx.x] : xcd_block(blockIdx.x, gridDim.x, xcd_group);
+    const uint32_t wave_base = blk * blockDim.x + (threadIdx.x & ~63u);
     const uint32_t lane = threadIdx.x & 63u;
     float o[3], d[3];
     uint32_t out;
@@ -695,6 +702,7 @@ __global__ void k_trace_grid(DevPool P, Src S, Sink K, uint32_t xcd_group, uint6
         } while (ray_active(r, P));
         K.put(out, ray_result(r, P));
     }
+    if (cost && threadIdx.x == 0) cost[blk] = (uint32_t)(__builtin_amdgcn_s_memtime() - c0);
     if (stamps) stamp(stamps, stamp_cap, t0, 64);
 }
 
@@ -991,7 +999,7 @@ hipError_t launch_as(const DevPool &p, const Src &s, const Sink &k, uint32_t n, 
     } else {
         const uint32_t xcd_group = supertile_rays >= (uint32_t)block ? supertile_rays / (uint32_t)block : 0u;
         hipLaunchKernelGGL((k_trace_grid<Src, Sink, kPacked, kCount>), dim3((n + block - 1) / block), dim3(block), lds,
-                           stream, p, s, k, xcd_group, sc.stamps, sc.stamp_cap);
+                           stream, p, s, k, xcd_group, sc.order, sc.cost, sc.stamps, sc.stamp_cap);
     }
     return hipGetLastError();
 }
@@ -1035,7 +1043,7 @@ CameraSource camera_source(const DevFrame &f, const Schedule &sc)
     src.width = f.cams[0].width;
     src.height = f.cams[0].height;
     src.tiles_x = (uint32_t)(src.width + kTileW - 1) / kTileW;
-    src.order = sc.tile_order;
+    src.order = sc.tile_order == 1 ? 1 : 0;       // 2 = row-major tiles in a planned launch order
     const uint32_t tiles_y = (uint32_t)(f.slice_rows + kTileH - 1) / kTileH;
     src.supertiles_x = (src.tiles_x + 7) / 8;
     src.per_view = sc.tile_order == 1 ? src.supertiles_x * ((tiles_y + 7) / 8) * 64u * 64u : src.tiles_x * tiles_y * 64u;

@@ -236,6 +236,15 @@ class GpuPool:
         call("och_gpu_render_views_dev", self._h, C.cast(arr, C.c_void_p), len(cams), _dev_ptr(rgba_slices),
              int(row_chunk), int(shard), int(n_shards))
 
+    def plan_views(self, cams, row_chunk: int | None = None, shard: int = 0, n_shards: int = 1):
+        """Plan the launch order of frames of this geometry (och_gpu_plan_views); used with
+        set_option("tile_order", 2).  Synchronous."""
+        arr = (Camera * len(cams))(*cams)
+        if row_chunk is None:
+            row_chunk = cams[0].height
+        call("och_gpu_plan_views", self._h, C.cast(arr, C.c_void_p), len(cams), int(row_chunk), int(shard),
+             int(n_shards))
+
     def render_bounce_views_dev(self, cams, rgba_slices, row_chunk: int | None = None, shard: int = 0,
                                 n_shards: int = 1):
         """Config 5 frames: one bounce per hit pixel, shaded (see och_gpu_render_bounce_views_dev)."""

@@ -69,6 +69,8 @@ def test_bench_instance_d12_1080p(ort, O, gpu_device, d12, d12_ref, pal):
     assert pool.get_option("layout") == 1 and pool.get_option("schedule") == 0
     want = oracle_frames(O, d12_ref, pal, W, H)
     cams = [ort.camera(tuple(ORIGIN), YAW, p, FOV, W, H) for p in PITCHES]
+    pool.plan_views(cams, 8, 0, 1)          # bench.py's launch order
+    pool.set_option("tile_order", 2)
     # three frames in flight on three streams, as the bench pipelines them
     streams = [torch.cuda.current_stream()] + [torch.cuda.Stream() for _ in range(2)]
     sfs = []
@@ -84,7 +86,11 @@ def test_bench_instance_d12_1080p(ort, O, gpu_device, d12, d12_ref, pal):
     for sf in sfs:
         assert_frames(sf.frames, want)
     pool.set_stream(torch.cuda.current_stream())
-    # the RGBA8 render path of the same frames
+    # natural launch order, and the RGBA8 render path of the same frames
+    pool.set_option("tile_order", 0)
+    sfs[0].render(cams)
+    torch.cuda.synchronize()
+    assert_frames(sfs[0].frames, want)
     sf = ShardedFrame(pool, W, H, 8, n_views=2, indexed=False)
     sf.render(cams)
     torch.cuda.synchronize()

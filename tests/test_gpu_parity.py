@@ -469,3 +469,38 @@ def test_refill_schedule_variants(ort, O, gpu_device, chunk, refill):
         for v in range(2):
             assert np.array_equal(frames[v].cpu().numpy().view(np.uint32), want[v]), (order, v)
     pool.close()
+
+
+def test_planned_launch_order(ort, O, gpu_device):
+    """OCH_OPT_TILE_ORDER = 2: the costliest tiles of a planning frame go first
+    (och_gpu_plan_views).  Dispatch order only: frames of the planned geometry,
+    of another geometry (natural order) and after the camera moved are all
+    the oracle's."""
+    import torch
+    tree = ort.build_terrain(9)
+    pal = ort.VoxelData().get_colours()
+    pool = ort.HOctree(tree.nodes, tree.root, 9, device=0)
+    pool.set_palette(pal)
+    pool.set_stream(torch.cuda.current_stream())
+    ref_pool = O.OraclePool(tree.nodes, tree.root, 9, 1)
+    W, H = 803, 451
+    cams = [ort.camera((1.5, 1.5, 1.5), 0.3, p, 1.25, W, H) for p in (0.0, -0.6)]
+    pool.plan_views(cams, 8, 0, 1)
+    pool.set_option("tile_order", 2)
+    for yaw in (0.3, 0.9):                   # the planned views, then a moved camera
+        cams = [ort.camera((1.5, 1.5, 1.5), yaw, p, 1.25, W, H) for p in (0.0, -0.6)]
+        want = []
+        for p in (0.0, -0.6):
+            r = O.trace_batch(ref_pool, O.Rcp(None), ORIGIN, O.raygen(yaw, p, 1.25, W, H), nthreads=16)
+            want.append(O.shade(r["dir"], r["voxel"], pal).reshape(H, W))
+        for n, rc in ((1, 8), (3, 8), (1, H)):    # planned geometry, then two others
+            rows = ort.shard_rows(H, rc, n)
+            gathered = torch.full((n, 2, rows, W), 255, dtype=torch.uint8, device="cuda")
+            for s_ in range(n):
+                pool.render_codes_views_dev(cams, gathered[s_], rc, s_, n)
+            full = torch.empty((2, H, W), dtype=torch.int32, device="cuda")
+            pool.shade_unshard_dev(gathered, full, W, H, rc, n, 2)
+            torch.cuda.synchronize()
+            for v in range(2):
+                assert np.array_equal(full[v].cpu().numpy().view(np.uint32), want[v]), (yaw, n, rc, v)
+    pool.close()
