@@ -418,8 +418,12 @@ def main():
         if rank == 0:
             bounce_host = sfs[(a.steps - 1) % len(sfs)].frames.cpu().numpy()
         pool.set_option("bounce_compact", 0)
+        if pool.get_option("tile_order") == 2:
+            pool.plan_views(cams, a.row_chunk, rank, world)       # the plan is per compaction setting
         nc_el, nc_kms = bounce_run(max(a.steps // 2, 3))
         pool.set_option("bounce_compact", 1)
+        if pool.get_option("tile_order") == 2:
+            pool.plan_views(cams, a.row_chunk, rank, world)
         pool.set_stream(stream)
         hits = torch.tensor([hits_total], dtype=torch.int64, device=dev)
         if world > 1:

@@ -46,6 +46,7 @@ int main(int argc, char **argv)
             cam.height = H;
             cams.push_back(cam.update_position());
         }
+        group.plan(cams);                         // costliest tiles first (one timed render per device)
         group.render(cams);                       // warm-up
         group.synchronize();
         const auto t0 = std::chrono::steady_clock::now();

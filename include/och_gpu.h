@@ -226,11 +226,12 @@ OCH_API int och_shard_rows(int height, int row_chunk, int n_shards);
 OCH_API int och_gpu_render_views_dev(och_gpu_pool *pool, const och_camera *cams, int n_views, uint32_t *rgba_slices,
                                      int row_chunk, int shard, int n_shards);
 /* Plan the launch order of frames of this geometry (size, views, sharding,
- * block): one render of these cameras times every workgroup, and later
- * renders with OCH_OPT_TILE_ORDER = 2 dispatch the costliest tiles first, so
- * a frame does not end on a few late grazing tiles.  Synchronous.  A plan
- * made from one camera stays valid (and approximately right) while the
- * camera moves; re-plan at will. */
+ * block, bounce compaction): one render of these cameras per kernel (primary
+ * and config-5 bounce frames) times every workgroup, and later renders with
+ * OCH_OPT_TILE_ORDER = 2 dispatch the costliest tiles first, so a frame does
+ * not end on a few late grazing tiles.  Synchronous.  A plan made from one
+ * camera stays valid (and approximately right) while the camera moves;
+ * re-plan at will. */
 OCH_API int och_gpu_plan_views(och_gpu_pool *pool, const och_camera *cams, int n_views, int row_chunk, int shard,
                                int n_shards);
 /* Config 5 frame: och_gpu_render_views_dev with one bounce per hit; a hit
@@ -280,6 +281,8 @@ OCH_API int och_frame_group_size(const och_frame_group *group, int *n_devices);
 OCH_API int och_frame_group_pool(och_frame_group *group, int rank, och_gpu_pool **pool);
 OCH_API int och_frame_group_set_palette(och_frame_group *group, const uint32_t *rgba, uint32_t n_voxels);
 OCH_API int och_frame_group_set_option(och_frame_group *group, int option, int value);
+/* och_gpu_plan_views on every device for this geometry, then OCH_OPT_TILE_ORDER = 2. */
+OCH_API int och_frame_group_plan(och_frame_group *group, const och_camera *cams, int n_views, int row_chunk);
 /* Enqueue one frame of n_views equal-size cameras on every device (bounce = 1:
  * config 5's secondary rays).  Asynchronous; frames are valid once the
  * group is synchronised (or downloaded). */

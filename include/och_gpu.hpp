@@ -161,6 +161,11 @@ public:
     {
         check(och_frame_group_set_option(g_, option, value), "och_frame_group_set_option");
     }
+    // Cost-planned launch order for frames of these cameras' geometry.
+    void plan(const std::vector<och_camera> &cams, int row_chunk = 8)
+    {
+        check(och_frame_group_plan(g_, cams.data(), static_cast<int>(cams.size()), row_chunk), "och_frame_group_plan");
+    }
     // One frame of every view, asynchronous on all devices.
     void render(const std::vector<och_camera> &cams, int row_chunk = 8, bool bounce = false)
     {

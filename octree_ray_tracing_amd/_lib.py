@@ -111,6 +111,7 @@ PROTOTYPES = {
     "och_frame_group_set_palette": (C.c_int, [_P, _P, _u32]),
     "och_frame_group_set_option": (C.c_int, [_P, C.c_int, C.c_int]),
     "och_frame_group_render": (C.c_int, [_P, _P, C.c_int, C.c_int, C.c_int]),
+    "och_frame_group_plan": (C.c_int, [_P, _P, C.c_int, C.c_int]),
     "och_frame_group_frames_dev": (C.c_int, [_P, C.c_int, C.POINTER(_P)]),
     "och_frame_group_download": (C.c_int, [_P, C.c_int, _P]),
     "och_frame_group_synchronize": (C.c_int, [_P]),

@@ -157,9 +157,10 @@ struct och_gpu_pool {
     void *d_scratch = nullptr;
     size_t scratch_bytes = 0;
     // cost-planned launch order (och_gpu_plan_views, OCH_OPT_TILE_ORDER = 2)
-    uint32_t *d_order = nullptr;
-    uint32_t order_blocks = 0;
-    int64_t plan_key[7] = {0, 0, 0, 0, 0, 0, 0};
+    // [0] primary frames (grid kernel), [1] config-5 frames (bounce kernel)
+    uint32_t *d_order[2] = {nullptr, nullptr};
+    uint32_t order_blocks[2] = {0, 0};
+    int64_t plan_key[2][8] = {};
 
     hipStream_t stream() const { return use_ext ? ext_stream : own_stream; }
 
@@ -461,7 +462,8 @@ OCH_API int och_gpu_pool_destroy(och_gpu_pool *p)
     if (p->d_palette) (void)hipFree(p->d_palette);
     if (p->d_code_table) (void)hipFree(p->d_code_table);
     if (p->d_scratch) (void)hipFree(p->d_scratch);
-    if (p->d_order) (void)hipFree(p->d_order);
+    for (uint32_t *o : p->d_order)
+        if (o) (void)hipFree(o);
     if (p->d_counter) (void)hipFree(p->d_counter);
     if (p->ev_start) (void)hipEventDestroy(p->ev_start);
     if (p->ev_stop) (void)hipEventDestroy(p->ev_stop);
@@ -882,9 +884,11 @@ int render_views(och_gpu_pool *p, const och_camera *cams, int n_views, uint32_t 
     f.n_shards = n_shards;
     f.slice_rows = och_shard_rows(cams[0].height, row_chunk, n_shards);
     och::Schedule sc = p->schedule();
-    if (p->opt_tile_order == 2 && p->opt_schedule == 0 && p->d_order) {
-        const int64_t key[7] = {cams[0].width, cams[0].height, n_views, row_chunk, shard, n_shards, p->opt_block};
-        if (std::memcmp(key, p->plan_key, sizeof key) == 0) sc.order = p->d_order;
+    const int which = bounce ? 1 : 0;
+    if (p->opt_tile_order == 2 && (bounce || p->opt_schedule == 0) && p->d_order[which]) {
+        const int64_t key[8] = {cams[0].width, cams[0].height, n_views, row_chunk, shard, n_shards, p->opt_block,
+                                bounce ? p->opt_bounce_compact : 0};
+        if (std::memcmp(key, p->plan_key[which], sizeof key) == 0) sc.order = p->d_order[which];
     }
     OCH_HIP(hipEventRecord(p->ev_start, p->stream()));
     if (code_slices)
@@ -906,16 +910,17 @@ OCH_API int och_gpu_plan_views(och_gpu_pool *p, const och_camera *cams, int n_vi
     if (!p || !cams) return fail(OCH_E_INVALID, "NULL argument");
     if (n_views < 1 || n_views > OCH_MAX_VIEWS || row_chunk <= 0 || n_shards <= 0 || shard < 0 || shard >= n_shards)
         return fail(OCH_E_INVALID, "bad plan arguments");
+    if (!p->d_lut) return fail(OCH_E_RCP_MODEL, "no RCPPS table on this pool (call och_gpu_set_rcp_lut)");
     DeviceGuard g(p->device);
-    // One planning render (RGBA8 into scratch) in natural order, timing every workgroup.
+    // One planning render per kernel (primary grid, config-5 bounce) into
+    // scratch in natural order, timing every workgroup.
     const int W = cams[0].width, H = cams[0].height;
     const int rows = och_shard_rows(H, row_chunk, n_shards);
     const size_t frame_bytes = (size_t)n_views * rows * W * 4;
-    const uint32_t max_blocks = (uint32_t)(((size_t)n_views * (rows + 7) / 8 * ((W + 7) / 8) * 64 + 63) / 64) + 1024;
+    const uint32_t max_blocks = (uint32_t)((size_t)n_views * ((rows + 7) / 8) * ((W + 7) / 8)) + 1024;
     int st = ensure_scratch(p, frame_bytes + (size_t)max_blocks * 4);
     if (st != OCH_OK) return st;
     uint32_t *cost = reinterpret_cast<uint32_t *>(static_cast<char *>(p->d_scratch) + frame_bytes);
-    OCH_HIP(hipMemsetAsync(cost, 0xFF, (size_t)max_blocks * 4, p->stream()));
     och::DevFrame f;
     for (int v = 0; v < n_views; ++v) f.cams[v] = cams[v];
     f.n_views = n_views;
@@ -927,30 +932,36 @@ OCH_API int och_gpu_plan_views(och_gpu_pool *p, const och_camera *cams, int n_vi
     f.shard = shard;
     f.n_shards = n_shards;
     f.slice_rows = rows;
-    och::Schedule sc = p->schedule();
-    sc.kind = 0;
-    sc.tile_order = 0;
-    sc.cost = cost;
-    if (!p->d_lut) return fail(OCH_E_RCP_MODEL, "no RCPPS table on this pool (call och_gpu_set_rcp_lut)");
-    OCH_HIP(och::launch_render(p->dev(), f, sc, p->stream()));
-    std::vector<uint32_t> c(max_blocks);
-    OCH_HIP(hipMemcpyAsync(c.data(), cost, (size_t)max_blocks * 4, hipMemcpyDeviceToHost, p->stream()));
-    OCH_HIP(hipStreamSynchronize(p->stream()));
-    uint32_t n_blocks = 0;
-    while (n_blocks < max_blocks && c[n_blocks] != 0xFFFFFFFFu) ++n_blocks;   // launched blocks wrote a cost
-    std::vector<uint32_t> order(n_blocks);
-    for (uint32_t i = 0; i < n_blocks; ++i) order[i] = i;
-    std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return c[a] > c[b]; });
-    if (p->order_blocks < n_blocks) {
-        if (p->d_order) OCH_HIP(hipFree(p->d_order));
-        p->d_order = nullptr;
-        p->order_blocks = 0;
-        OCH_HIP(hipMalloc(&p->d_order, (size_t)n_blocks * 4));
-        p->order_blocks = n_blocks;
+    for (int which = 0; which < 2; ++which) {
+        OCH_HIP(hipMemsetAsync(cost, 0xFF, (size_t)max_blocks * 4, p->stream()));
+        och::Schedule sc = p->schedule();
+        sc.kind = 0;
+        sc.tile_order = 0;
+        sc.cost = cost;
+        if (which == 0)
+            OCH_HIP(och::launch_render(p->dev(), f, sc, p->stream()));
+        else
+            OCH_HIP(och::launch_render_bounce(p->dev(), f, sc, p->stream()));
+        std::vector<uint32_t> c(max_blocks);
+        OCH_HIP(hipMemcpyAsync(c.data(), cost, (size_t)max_blocks * 4, hipMemcpyDeviceToHost, p->stream()));
+        OCH_HIP(hipStreamSynchronize(p->stream()));
+        uint32_t n_blocks = 0;
+        while (n_blocks < max_blocks && c[n_blocks] != 0xFFFFFFFFu) ++n_blocks;   // launched blocks wrote a cost
+        std::vector<uint32_t> order(n_blocks);
+        for (uint32_t i = 0; i < n_blocks; ++i) order[i] = i;
+        std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return c[a] > c[b]; });
+        if (p->order_blocks[which] < n_blocks) {
+            if (p->d_order[which]) OCH_HIP(hipFree(p->d_order[which]));
+            p->d_order[which] = nullptr;
+            p->order_blocks[which] = 0;
+            OCH_HIP(hipMalloc(&p->d_order[which], (size_t)n_blocks * 4));
+            p->order_blocks[which] = n_blocks;
+        }
+        OCH_HIP(hipMemcpy(p->d_order[which], order.data(), (size_t)n_blocks * 4, hipMemcpyHostToDevice));
+        const int64_t key[8] = {W, H, n_views, row_chunk, shard, n_shards, p->opt_block,
+                                which ? p->opt_bounce_compact : 0};
+        std::memcpy(p->plan_key[which], key, sizeof key);
     }
-    OCH_HIP(hipMemcpy(p->d_order, order.data(), (size_t)n_blocks * 4, hipMemcpyHostToDevice));
-    const int64_t key[7] = {W, H, n_views, row_chunk, shard, n_shards, p->opt_block};
-    std::memcpy(p->plan_key, key, sizeof key);
     return OCH_OK;
 }
 

@@ -239,6 +239,17 @@ OCH_API int och_frame_group_set_option(och_frame_group *g, int option, int value
     return OCH_OK;
 }
 
+OCH_API int och_frame_group_plan(och_frame_group *g, const och_camera *cams, int n_views, int row_chunk)
+{
+    if (!g || !cams) return group_fail(OCH_E_INVALID, "NULL argument");
+    for (int r = 0; r < g->n; ++r) {
+        int st = och_gpu_plan_views(g->pools[r], cams, n_views, row_chunk, r, g->n);
+        if (st == OCH_OK) st = och_gpu_set_option(g->pools[r], OCH_OPT_TILE_ORDER, 2);
+        if (st != OCH_OK) return st;
+    }
+    return OCH_OK;
+}
+
 OCH_API int och_frame_group_render(och_frame_group *g, const och_camera *cams, int n_views, int row_chunk, int bounce)
 {
     if (!g || !cams || n_views < 1 || n_views > OCH_MAX_VIEWS || row_chunk < 1)

@@ -713,15 +713,18 @@ __global__ void k_trace_grid(DevPool P, Src S, Sink K, uint32_t xcd_group, const
 // a few bounced lanes.  The queue (8 words per thread, SoA) reuses the
 // parent stacks' LDS between the passes.
 template <class Src, class Sink, bool kPacked, bool kCount>
-__global__ void k_trace_bounce(DevPool P, Src S, Sink K, int compact, uint64_t *stamps, uint32_t stamp_cap)
+__global__ void k_trace_bounce(DevPool P, Src S, Sink K, int compact, const uint32_t *__restrict__ order,
+                               uint32_t *__restrict__ cost, uint64_t *stamps, uint32_t stamp_cap)
 {
     extern __shared__ uint32_t lds_stack[];
     __shared__ uint32_t wave_count[16];
+    const uint64_t c0 = cost ? __builtin_amdgcn_s_memtime() : 0;
+    const uint32_t blk = order ? order[blockIdx.x] : blockIdx.x;
     const uint64_t t0 = stamps ? realtime() : 0;
     uint32_t *stack = lds_stack + threadIdx.x;
     uint32_t *queue = lds_stack;
     const uint32_t nb = blockDim.x;
-    const uint32_t wave_base = blockIdx.x * nb + (threadIdx.x & ~63u);
+    const uint32_t wave_base = blk * nb + (threadIdx.x & ~63u);
     float o[3], d[3], o2[3], d2[3];
     uint32_t out = 0, payload = 0;
     bool want = false;
@@ -744,6 +747,7 @@ __global__ void k_trace_bounce(DevPool P, Src S, Sink K, int compact, uint64_t *
         }
     }
     if (!compact) {
+        if (cost && threadIdx.x == 0) cost[blk] = (uint32_t)(__builtin_amdgcn_s_memtime() - c0);
         if (stamps) stamp(stamps, stamp_cap, t0, 0);
         return;
     }
@@ -788,6 +792,7 @@ __global__ void k_trace_bounce(DevPool P, Src S, Sink K, int compact, uint64_t *
         } while (ray_active(r, P));
         K.put_secondary(sout, spay, ray_result(r, P));
     }
+    if (cost && threadIdx.x == 0) cost[blk] = (uint32_t)(__builtin_amdgcn_s_memtime() - c0);
     if (stamps) stamp(stamps, stamp_cap, t0, total);
 }
 
@@ -1024,10 +1029,10 @@ hipError_t launch_bounce(const DevPool &p, const Src &s, const Sink &k, uint32_t
     const dim3 grid((n + block - 1) / block);
     if (p.packed)
         hipLaunchKernelGGL((k_trace_bounce<Src, Sink, true, kCount>), grid, dim3(block), lds, stream, p, s, k,
-                           sc.bounce_compact, sc.stamps, sc.stamp_cap);
+                           sc.bounce_compact, sc.order, sc.cost, sc.stamps, sc.stamp_cap);
     else
         hipLaunchKernelGGL((k_trace_bounce<Src, Sink, false, kCount>), grid, dim3(block), lds, stream, p, s, k,
-                           sc.bounce_compact, sc.stamps, sc.stamp_cap);
+                           sc.bounce_compact, sc.order, sc.cost, sc.stamps, sc.stamp_cap);
     return hipGetLastError();
 }
 

@@ -148,6 +148,12 @@ class FrameGroup:
     def set_option(self, name: str, value: int):
         call("och_frame_group_set_option", self._h, GpuPool.OPTIONS[name], int(value))
 
+    def plan(self, cams, row_chunk: int = 8):
+        """Cost-planned launch order on every device (och_frame_group_plan)."""
+        cams = list(cams) if isinstance(cams, (list, tuple)) else [cams]
+        arr = (Camera * len(cams))(*cams)
+        call("och_frame_group_plan", self._h, C.cast(arr, C.c_void_p), len(cams), int(row_chunk))
+
     def render(self, cams, row_chunk: int = 8, bounce: bool = False):
         cams = list(cams) if isinstance(cams, (list, tuple)) else [cams]
         arr = (Camera * len(cams))(*cams)

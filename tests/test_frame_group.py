@@ -49,6 +49,12 @@ def test_group_one_device_matches_oracle(ort, O, gpu_device, bounce):
             got = g.download(0)
             for v in range(2):
                 assert np.array_equal(got[v], want[v]), (sched, chunk, v)
+    g.set_option("schedule", 0)
+    g.plan(cams, row_chunk=8)                   # planned launch order (tile_order 2)
+    g.render(cams, row_chunk=8, bounce=bounce)
+    got = g.download(0)
+    for v in range(2):
+        assert np.array_equal(got[v], want[v]), ("planned", v)
     # a palette of more than OCH_CODE_MAX_VOXELS ids: RGBA8 slices travel instead of codes
     big = np.resize(np.asarray(pal, np.uint32).reshape(-1), 6 * 24)
     g.set_palette(big)

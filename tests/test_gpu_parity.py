@@ -503,4 +503,15 @@ def test_planned_launch_order(ort, O, gpu_device):
             torch.cuda.synchronize()
             for v in range(2):
                 assert np.array_equal(full[v].cpu().numpy().view(np.uint32), want[v]), (yaw, n, rc, v)
+    # config 5 frames in their planned order (the bounce kernel's own plan)
+    cams = [ort.camera((1.5, 1.5, 1.5), 0.3, p, 1.25, W, H) for p in (0.0, -0.6)]
+    gathered = torch.full((1, 2, H, W), 255, dtype=torch.uint8, device="cuda")
+    pool.render_codes_views_dev(cams, gathered[0], 8, 0, 1, bounce=True)
+    full = torch.empty((2, H, W), dtype=torch.int32, device="cuda")
+    pool.shade_unshard_dev(gathered, full, W, H, 8, 1, 2)
+    torch.cuda.synchronize()
+    for v, p in enumerate((0.0, -0.6)):
+        r = O.trace_bounce_batch(ref_pool, O.Rcp(None), ORIGIN, O.raygen(0.3, p, 1.25, W, H), nthreads=16)
+        want = O.shade_bounce(r["dir"], r["voxel"], r["dir2"], pal).reshape(H, W)
+        assert np.array_equal(full[v].cpu().numpy().view(np.uint32), want), ("bounce", v)
     pool.close()
