@@ -208,6 +208,82 @@ def cpu_leg(nodes, root, depth, width, height, frames, bounce_frames, time_it: b
     return base, parity
 
 
+def other_configs(a, dev, stream):
+    """configs[1] (depth 10, 1920x1080, two views per pipelined step) and
+    configs[0] (depth-8 och::octree, 512x512, trace batch + CPU oracle)."""
+    import torch
+    import octree_ray_tracing_amd as ort
+    from octree_ray_tracing_amd.frame import ShardedFrame
+
+    out = {}
+    tree = ort.build_terrain(10, use_gpu=True)
+    pool = ort.HOctree(tree.nodes, tree.root, 10, device=dev.index)
+    pool.set_palette(ort.VoxelData().get_colours())
+    pool.set_stream(stream)
+    cams = [ort.camera(ORIGIN, YAW, p, FOV, 1920, 1080) for p in PITCHES]
+    pool.plan_views(cams, a.row_chunk, 0, 1)
+    pool.set_option("tile_order", 2)
+    streams = [stream] + [torch.cuda.Stream(device=dev) for _ in range(2)]
+    sfs = []
+    for s_ in streams:
+        with torch.cuda.stream(s_):
+            sfs.append(ShardedFrame(pool, 1920, 1080, a.row_chunk, n_views=2, indexed=True))
+
+    def run(n):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for k in range(n):
+            pool.set_stream(streams[k % 3])
+            with torch.cuda.stream(streams[k % 3]):
+                sfs[k % 3].render(cams)
+        torch.cuda.synchronize()
+        return time.perf_counter() - t0
+
+    run(5)
+    el = run(a.steps)
+    n_s = max(a.steps, int(1.0 / (el / a.steps)))
+    sus = statistics.median([2 * 1920 * 1080 * n_s / run(n_s) / 1e6 for _ in range(3)])
+    out["configs[1]"] = {"workload": "depth-10 och_h_octree DAG (334 025 nodes), 1920x1080, two views per step, 1 MI355X",
+                         "value": round(2 * 1920 * 1080 * a.steps / el / 1e6, 2), "sustained": round(sus, 2),
+                         "unit": "Mrays/s", "ms_per_step": round(el / a.steps * 1e3, 4)}
+    pool.set_stream(stream)
+    pool.close()
+    # configs[0]: the pointer octree (index base 0, miss t = 0) at depth 8
+    oct_ = ort.build_terrain(8, dedup=False, use_gpu=True)
+    opool = ort.Octree(oct_.nodes, 8, device=dev.index)
+    opool.set_stream(stream)
+    cam = ort.camera(ORIGIN, YAW, 0.0, FOV, 512, 512)
+    dirs = torch.empty(512 * 512 * 3, dtype=torch.float32, device=dev)
+    opool.raygen_dev(cam, dirs)
+    o_t = torch.tensor(ORIGIN, dtype=torch.float32, device=dev)
+    bufs = [torch.empty(512 * 512, dtype=t, device=dev) for t in (torch.int32, torch.int32, torch.float32)]
+    for _ in range(3):
+        opool.trace_batch_dev(o_t, dirs, *bufs)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(50):
+        opool.trace_batch_dev(o_t, dirs, *bufs)
+    torch.cuda.synchronize()
+    g_el = (time.perf_counter() - t0) / 50
+    gpu_rec = [b.cpu().numpy() for b in bufs]
+    cpu_mrays, match = None, None
+    if not a.no_parity:
+        from oracle import oracle as O
+        rays = O.raygen(YAW, 0.0, FOV, 512, 512)
+        ref_pool = O.OraclePool(oct_.nodes, 0, 8, 0)
+        t0 = time.perf_counter()
+        ref = O.trace_batch(ref_pool, O.Rcp(None), np.array(ORIGIN, np.float32), rays, nthreads=1)
+        cpu_mrays = 512 * 512 / (time.perf_counter() - t0) / 1e6
+        match = bool(np.array_equal(gpu_rec[0], ref["dir"]) and np.array_equal(gpu_rec[1].view(np.uint32), ref["voxel"])
+                     and np.array_equal(gpu_rec[2].view(np.uint32), ref["t"].view(np.uint32)))
+    out["configs[0]"] = {"workload": "depth-8 och::octree (548 325 nodes, 0-based, miss t = 0), 512x512 primary rays",
+                         "gpu_mrays_s": round(512 * 512 / g_el / 1e6, 2), "gpu_ms_per_frame": round(g_el * 1e3, 4),
+                         "cpu_oracle_mrays_s_1core": None if cpu_mrays is None else round(cpu_mrays, 2),
+                         "records_match_oracle": match}
+    opool.close()
+    return out
+
+
 def load_pmc(kernel: str, config_key: str):
     """The committed rocprofv3 PMC summary of this configuration, if it was
     taken of the kernel source in this tree (profiles/pmc_summary.json,
@@ -244,6 +320,7 @@ def main():
     ap.add_argument("--opt", action="append", default=[], metavar="NAME=VALUE",
                     help="pool launch option (och_gpu_set_option), e.g. tile_order=1")
     ap.add_argument("--no-bounce", action="store_true", help="skip the config-5 (secondary rays) measurement")
+    ap.add_argument("--no-other-configs", action="store_true", help="skip the configs[0] / configs[1] side measurements")
     ap.add_argument("--rgba-frames", action="store_true",
                     help="render and exchange RGBA8 slices instead of 1-byte indexed-colour codes")
     ap.add_argument("--inflight", type=int, default=3,
@@ -474,6 +551,15 @@ def main():
     else:
         roof.update({k: hbm[k] for k in ("bound", "achieved", "peak", "unit", "frac")})
 
+    # The other BASELINE configs on this GPU, N = 1 only (each a separate,
+    # smaller workload; not the headline): configs[1] = depth-10 DAG at
+    # 1920x1080 through the same pipelined two-view step; configs[0] = the
+    # depth-8 och::octree (0-based pool) at 512x512, one trace batch of
+    # resident rays, next to the CPU oracle on the same rays.
+    others = None
+    if world == 1 and not a.no_other_configs:
+        others = other_configs(a, dev, stream)
+
     cpu, parity = None, None
     if rank == 0 and not a.no_parity:
         cpu, parity = cpu_leg(nodes, root, a.depth, W, H, frames_host, bounce_host,
@@ -516,6 +602,7 @@ def main():
             "sustained": sustained,
             "trace_batch": trace_only,
             "bounce": bounce,
+            "other_configs": others,
         }
         print(json.dumps(line), flush=True)
     pool.close()

@@ -156,6 +156,9 @@ struct och_gpu_pool {
     // host-call staging
     void *d_scratch = nullptr;
     size_t scratch_bytes = 0;
+    // editor flush staging (och::pool_scatter_slots): pinned host + device, grown on demand
+    uint32_t *h_stage = nullptr, *d_stage = nullptr;
+    size_t stage_words = 0;
     // cost-planned launch order (och_gpu_plan_views, OCH_OPT_TILE_ORDER = 2)
     // [0] primary frames (grid kernel), [1] config-5 frames (bounce kernel)
     uint32_t *d_order[2] = {nullptr, nullptr};
@@ -462,6 +465,8 @@ OCH_API int och_gpu_pool_destroy(och_gpu_pool *p)
     if (p->d_palette) (void)hipFree(p->d_palette);
     if (p->d_code_table) (void)hipFree(p->d_code_table);
     if (p->d_scratch) (void)hipFree(p->d_scratch);
+    if (p->h_stage) (void)hipHostFree(p->h_stage);
+    if (p->d_stage) (void)hipFree(p->d_stage);
     for (uint32_t *o : p->d_order)
         if (o) (void)hipFree(o);
     if (p->d_counter) (void)hipFree(p->d_counter);
@@ -570,6 +575,42 @@ int och::pool_write_slots(och_gpu_pool *p, uint32_t first, uint32_t count, const
     }
     if (count)
         OCH_HIP(hipMemcpy(p->d_packed + (size_t)first * 8, packed, (size_t)count * 32, hipMemcpyHostToDevice));
+    return OCH_OK;
+}
+
+int och::pool_scatter_slots(och_gpu_pool *p, const uint32_t *ids, uint32_t count, const uint32_t *raw,
+                            const uint32_t *packed)
+{
+    if (!p || p->index_base != 1 || (count && (!ids || !raw))) return fail(OCH_E_INVALID, "bad editor flush");
+    if (packed && (!p->d_packed || !p->packed_by_slot))
+        return fail(OCH_E_INVALID, "packed buffer is not in editor numbering");
+    if (count == 0) return OCH_OK;
+    for (uint32_t i = 0; i < count; ++i)
+        if (ids[i] == 0 || ids[i] >= p->n_nodes) return fail(OCH_E_INVALID, "editor slot %u outside the pool", ids[i]);
+    DeviceGuard g(p->device);
+    p->last_writer = 0;                 // until pool_commit
+    // staging: [ids | raw | packed]
+    const size_t words = (size_t)count * (packed ? 17 : 9);
+    if (words > p->stage_words) {
+        if (p->h_stage) OCH_HIP(hipHostFree(p->h_stage));
+        if (p->d_stage) OCH_HIP(hipFree(p->d_stage));
+        p->h_stage = p->d_stage = nullptr;
+        p->stage_words = 0;
+        const size_t cap = std::max<size_t>(words, 1 << 16);
+        OCH_HIP(hipHostMalloc(&p->h_stage, cap * 4, hipHostMallocDefault));
+        OCH_HIP(hipMalloc(&p->d_stage, cap * 4));
+        p->stage_words = cap;
+    }
+    std::memcpy(p->h_stage, ids, (size_t)count * 4);
+    std::memcpy(p->h_stage + count, raw, (size_t)count * 32);
+    if (packed) std::memcpy(p->h_stage + 9 * (size_t)count, packed, (size_t)count * 32);
+    for (uint32_t i = 0; i < count; ++i)       // host mirror (user numbering, slot s at row s - 1)
+        std::memcpy(p->mirror.data() + (size_t)(ids[i] - 1) * 8, raw + (size_t)i * 8, 32);
+    const hipStream_t s = p->stream();
+    OCH_HIP(hipMemcpyAsync(p->d_stage, p->h_stage, words * 4, hipMemcpyHostToDevice, s));
+    OCH_HIP(och::launch_scatter_slots(p->d_stage, p->d_stage + count, packed ? p->d_stage + 9 * (size_t)count : nullptr,
+                                      count, p->d_nodes, packed ? p->d_packed : nullptr, s));
+    OCH_HIP(hipStreamSynchronize(s));
     return OCH_OK;
 }
 

@@ -7,8 +7,8 @@
 // placement follows the FNV hash, so an edit touches slots scattered over the
 // whole 2^L table.  Here a node keeps its slot until it dies, new nodes take
 // the lowest free slots, and every written slot is recorded, so
-// och_editor_flush re-uploads only the runs of dirty slots (och::pool_write_slots)
-// instead of the pool.
+// och_editor_flush re-uploads only the dirty slots (staged in one copy and
+// scattered by one kernel, och::pool_scatter_slots) instead of the pool.
 //
 // Differences from the reference that do not change any traced record (the
 // tracer reads children only, never slot positions or counts):
@@ -66,20 +66,6 @@ struct och_editor {
     uint32_t *slot(uint32_t s) { return nodes.data() + (size_t)(s - 1) * 8; }
     const uint32_t *slot(uint32_t s) const { return nodes.data() + (size_t)(s - 1) * 8; }
     void mark(uint32_t s) { dirty.push_back(s); }
-    // Sorted distinct dirty slots, coalesced into runs [first, last] that skip
-    // gaps of at most kGap clean slots (one copy then beats two).
-    std::vector<std::pair<uint32_t, uint32_t>> dirty_runs()
-    {
-        constexpr uint32_t kGap = 32;
-        std::sort(dirty.begin(), dirty.end());
-        dirty.erase(std::unique(dirty.begin(), dirty.end()), dirty.end());
-        std::vector<std::pair<uint32_t, uint32_t>> runs;
-        for (uint32_t s : dirty) {
-            if (!runs.empty() && s - runs.back().second <= kGap + 1) runs.back().second = s;
-            else runs.emplace_back(s, s);
-        }
-        return runs;
-    }
     uint32_t mask_of(uint32_t s) const
     {
         uint32_t m = 0;
@@ -401,12 +387,17 @@ OCH_API int och_editor_flush(och_editor *e, och_gpu_pool *pool)
         std::memcpy(raw.data() + 8, e->nodes.data(), e->nodes.size() * 4);
         st = och::pool_write_slots(pool, 0, e->capacity + 1, raw.data(), pk, true);
     } else if (st == OCH_OK) {
-        const auto runs = e->dirty_runs();
-        for (size_t r = 0; r < runs.size() && st == OCH_OK; ++r) {
-            const uint32_t first = runs[r].first, count = runs[r].second - runs[r].first + 1;
-            st = och::pool_write_slots(pool, first, count, e->slot(first), pk ? pk + (size_t)first * 8 : nullptr,
-                                       false);
+        // the dirty slots, staged in one buffer and scattered by one kernel
+        std::sort(e->dirty.begin(), e->dirty.end());
+        e->dirty.erase(std::unique(e->dirty.begin(), e->dirty.end()), e->dirty.end());
+        const uint32_t n = (uint32_t)e->dirty.size();
+        std::vector<uint32_t> raw((size_t)n * 8), packed(pk ? (size_t)n * 8 : 0);
+        for (uint32_t i = 0; i < n; ++i) {
+            const uint32_t sl = e->dirty[i];
+            std::memcpy(raw.data() + (size_t)i * 8, e->slot(sl), 32);
+            if (pk) std::memcpy(packed.data() + (size_t)i * 8, pk + (size_t)sl * 8, 32);
         }
+        st = och::pool_scatter_slots(pool, e->dirty.data(), n, raw.data(), pk ? packed.data() : nullptr);
     }
     // The roots go out last, once every slot they reach is on the device.
     if (st == OCH_OK) st = och::pool_commit(pool, e->root, e->packed_root(), pk != nullptr, e->id);

@@ -56,6 +56,13 @@ int pool_drain(och_gpu_pool *pool);
 int pool_write_slots(och_gpu_pool *pool, uint32_t first, uint32_t count, const uint32_t *raw,
                      const uint32_t *packed, bool full);
 int pool_commit(och_gpu_pool *pool, uint32_t root, uint32_t packed_root, bool packed, uint64_t writer);
+// pool_write_slots for scattered slots: ids[count] (1..n_nodes-1, distinct),
+// raw / packed = count x 8 words; one staged copy and one scatter kernel,
+// complete on return.
+int pool_scatter_slots(och_gpu_pool *pool, const uint32_t *ids, uint32_t count, const uint32_t *raw,
+                       const uint32_t *packed);
+hipError_t launch_scatter_slots(const uint32_t *ids, const uint32_t *raw, const uint32_t *packed, uint32_t count,
+                                uint32_t *d_raw, uint32_t *d_packed, hipStream_t stream);
 uint64_t pool_serial(const och_gpu_pool *pool);
 // The stream the pool enqueues on (hipStream_t) and its palette size
 // (och_group.cpp drives several pools from one thread).

@@ -30,6 +30,11 @@ namespace {
 
 constexpr uint32_t kX86DefaultNaN = 0xFFC00000u;
 
+typedef float float2v __attribute__((ext_vector_type(2)));
+#ifndef OCH_PK_FMA
+#define OCH_PK_FMA 0
+#endif
+
 constexpr int kMaxViews = OCH_MAX_VIEWS;
 
 __device__ __forceinline__ uint32_t fbits(float f) { return __float_as_uint(f); }
@@ -192,8 +197,15 @@ __device__ __forceinline__ void ray_phase_step(Ray &r, uint32_t stride)
     // STEP :378-419.  The reference's cascade (x if tx <= ty && tx <= tz,
     // else y if ty < tx && ty <= tz, else z) picks the first axis holding
     // the unsigned minimum.
+#if OCH_PK_FMA
+    // x and y as one packed FMA (v_pk_fma_f32: two lanes of f32, each rounded once, as v_fma_f32)
+    const float2v pxy = {ffrom(r.p[0]), ffrom(r.p[1])}, cxy = {r.c[0], r.c[1]}, bxy = {r.b[0], r.b[1]};
+    const float2v txy = __builtin_elementwise_fma(pxy, cxy, bxy);
+    const uint32_t tx = fbits(txy.x), ty = fbits(txy.y);
+#else
     const uint32_t tx = fbits(__builtin_fmaf(ffrom(r.p[0]), r.c[0], r.b[0]));
     const uint32_t ty = fbits(__builtin_fmaf(ffrom(r.p[1]), r.c[1], r.b[1]));
+#endif
     const uint32_t tz = fbits(__builtin_fmaf(ffrom(r.p[2]), r.c[2], r.b[2]));
     const uint32_t tm = min(min(tx, ty), tz);
     const bool sx = tx == tm;
@@ -295,6 +307,16 @@ __device__ __forceinline__ void ray_push_descend(Ray &r, const DevPool &P, uint3
     r.dim >>= 1;
     const float tm = ffrom(r.t_min);
     uint32_t nidx = 0;
+#if OCH_PK_FMA
+    const uint32_t mx = r.p[0] | r.dim, my = r.p[1] | r.dim, mz = r.p[2] | r.dim;
+    const float2v mxy = {ffrom(mx), ffrom(my)}, cxy = {r.c[0], r.c[1]}, bxy = {r.b[0], r.b[1]};
+    const float2v txy = __builtin_elementwise_fma(mxy, cxy, bxy);
+    const bool ux = txy.x >= tm, uy = txy.y >= tm, uz = __builtin_fmaf(ffrom(mz), r.c[2], r.b[2]) >= tm;
+    nidx = (uint32_t)ux | ((uint32_t)uy << 1) | ((uint32_t)uz << 2);
+    r.p[0] = ux ? mx : r.p[0];
+    r.p[1] = uy ? my : r.p[1];
+    r.p[2] = uz ? mz : r.p[2];
+#else
 #pragma unroll
     for (int a = 0; a < 3; ++a) {
         const uint32_t mid = r.p[a] | r.dim;
@@ -302,6 +324,7 @@ __device__ __forceinline__ void ray_push_descend(Ray &r, const DevPool &P, uint3
         nidx |= (uint32_t)upper << a;
         r.p[a] = upper ? mid : r.p[a];
     }
+#endif
     r.idx = nidx;
 }
 
@@ -972,6 +995,20 @@ __global__ __launch_bounds__(256) void k_shade_unshard4(const uint8_t *__restric
     *reinterpret_cast<uint4 *>(frames + ((size_t)view * height + row) * width + col) = px;
 }
 
+// Editor flush: `count` staged slots (8 words each, raw and optionally packed)
+// scattered to their slot ids in both device layouts; one thread per word.
+__global__ __launch_bounds__(256) void k_scatter_slots(const uint32_t *__restrict__ ids,
+                                                       const uint32_t *__restrict__ raw,
+                                                       const uint32_t *__restrict__ packed, uint32_t count,
+                                                       uint32_t *__restrict__ d_raw, uint32_t *__restrict__ d_packed)
+{
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    if (i >= count * 8u) return;
+    const uint32_t slot = ids[i >> 3], w = i & 7u;
+    d_raw[(size_t)slot * 8 + w] = raw[i];
+    if (packed) d_packed[(size_t)slot * 8 + w] = packed[i];
+}
+
 // Per lane: parents of levels 1..depth-1 in slots 1..depth-1, plus a spare
 // slot below (the miss POP's read) and above (the hit descent's write).
 size_t stack_bytes(int depth, int block) { return (size_t)(depth + 1) * block * sizeof(uint32_t); }
@@ -1155,6 +1192,15 @@ hipError_t launch_trace_bounce_batch(const DevPool &p, const float *origin, int 
         p, src, BounceHitSink<false>{HitSink<false>{hit_dir, hit_voxel, hit_time, nullptr}, bounce_dir, bounce_voxel,
                                      bounce_time},
         n, sc, stream);
+}
+
+hipError_t launch_scatter_slots(const uint32_t *ids, const uint32_t *raw, const uint32_t *packed, uint32_t count,
+                                uint32_t *d_raw, uint32_t *d_packed, hipStream_t stream)
+{
+    if (count == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_scatter_slots, dim3((count * 8u + 255u) / 256u), dim3(256), 0, stream, ids, raw, packed, count,
+                       d_raw, d_packed);
+    return hipGetLastError();
 }
 
 hipError_t launch_unshard(const uint32_t *gathered, uint32_t *frames, int width, int height, int row_chunk,
