@@ -229,19 +229,28 @@ uint32_t reduce_brick(NodeStore &ns, int s_log2, std::vector<uint32_t> &ids, Bri
     int n = (1 << s_log2) / 2;
     for (int h = 1; h < s_log2; ++h) {
         const int m = n / 2;
+        // nodes of eight equal children (solid stone) repeat: the last one per
+        // level skips the hash table (a DAG only; an expanded tree shares nothing)
+        uint32_t last_child = 0, last_id = 0;
         for (int z = 0; z < m; ++z)
             for (int y = 0; y < m; ++y)
                 for (int x = 0; x < m; ++x) {
                     uint32_t c[8];
-                    bool any = false;
+                    bool any = false, same = true;
                     for (int k = 0; k < 8; ++k) {
                         const int cx = 2 * x + (k & 1), cy = 2 * y + ((k >> 1) & 1), cz = 2 * z + ((k >> 2) & 1);
                         c[k] = ids[((size_t)cz * n + cy) * n + cx];
                         any |= c[k] != 0;
+                        same &= c[k] == c[0];
                     }
                     uint32_t id = 0;
                     if (any) {
-                        id = ns.intern(c, h);
+                        if (same && ns.dedup && c[0] == last_child) {
+                            id = last_id;
+                        } else {
+                            id = ns.intern(c, h);
+                            if (same) last_child = c[0], last_id = id;
+                        }
                         ++st.tree_nodes;
                     }
                     ids[((size_t)z * m + y) * m + x] = id;   // safe: writes trail reads
