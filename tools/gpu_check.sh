@@ -16,7 +16,7 @@ import json, sys
 tag = sys.argv[1]
 d = json.load(open(f"gpurun_out/bench_{tag}.json"))
 print("bench", d["value"], "Mrays/s", d["ms_per_step"], "ms/step, kernel", d["roofline"]["kernel_ms"],
-      "idle-gpu kernel", d["roofline"]["kernel_ms_idle_gpu"], "| bounce", d["bounce"] and d["bounce"]["value"],
+      "serial kernel", d["roofline"]["kernel_ms_serial"], "| bounce", d["bounce"] and d["bounce"]["value"],
       d["bounce"] and d["bounce"]["ms_per_step"])
 for line in open(f"gpurun_out/lat_{tag}.log"):
     if line.startswith("{") or line.startswith("pitch"):
