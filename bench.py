@@ -545,6 +545,7 @@ def main():
         roof.update({"bound": "valu-issue", "achieved": round(ach, 1), "peak": VALU_PEAK_GINST_S,
                      "unit": "G VALU wave-instructions/s", "frac": round(ach / VALU_PEAK_GINST_S, 4),
                      "valu_insts_per_launch": int(insts), "valu_insts_per_wave": pmc.get("valu_insts_per_wave"),
+                     "valu_lane_utilization": pmc.get("valu_lane_utilization"),
                      "achieved_per_launch": round(insts / (k_avg_ms * 1e-3) / 1e9, 1),
                      "note": "issue rate over the pipelined step (frames overlap, so per-launch durations overlap "
                              "too); the DAG is L2/MALL-resident, so HBM is far from binding (see hbm)"})

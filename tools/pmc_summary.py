@@ -82,6 +82,9 @@ def summarise(root: Path) -> dict:
             # SQ_ACTIVE_INST_VALU is per-SIMD quad-cycles summed over the chip; normalise by
             # busy cycles x 4 SIMDs x CUs (256) / 4 (quad) -- reported as a ratio, see DESIGN.md
             d["valu_active_per_busy"] = round(d["SQ_ACTIVE_INST_VALU"] / d["SQ_BUSY_CYCLES"], 4)
+        if "SQ_THREAD_CYCLES_VALU" in d and d.get("SQ_ACTIVE_INST_VALU"):
+            # active lanes per VALU issue cycle / 64 (both counters from the same SQ, same units)
+            d["valu_lane_utilization"] = round(d["SQ_THREAD_CYCLES_VALU"] / (64.0 * d["SQ_ACTIVE_INST_VALU"]), 4)
         if "SQ_INSTS_VALU" in d and "SQ_WAVES" in d and d["SQ_WAVES"]:
             d["valu_insts_per_wave"] = round(d["SQ_INSTS_VALU"] / d["SQ_WAVES"], 1)
         if "GRBM_GUI_ACTIVE" in d and d.get("mean_ms"):

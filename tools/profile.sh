@@ -21,5 +21,6 @@ step pmc_write --pmc WRITE_SIZE || exit 1
 step pmc_tcc --pmc TCC_HIT_sum TCC_MISS_sum || exit 1
 step pmc_sq --pmc SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VMEM_RD SQ_INSTS_LDS || exit 1
 step pmc_sq2 --pmc SQ_INSTS_SALU SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_ANY SQ_WAIT_INST_ANY SQ_WAIT_ANY || exit 1
+step pmc_sq3 --pmc SQ_THREAD_CYCLES_VALU SQ_INST_CYCLES_SALU SQ_INSTS_BRANCH SQ_INSTS_SMEM SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE || exit 1
 step pmc_grbm --pmc GRBM_GUI_ACTIVE || exit 1
 python tools/pmc_summary.py $OUT > $OUT/summary.json
