@@ -9,7 +9,7 @@ OUT=gpurun_out/prof_$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
 export OCH_TREE_CACHE=${OCH_TREE_CACHE:-/tmp/och_tree_d12.npz}
-BENCH="python -u bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-parity --sustain 0 $*"
+BENCH="python -u bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-parity --sustain 0 --no-other-configs $*"
 step() {   # step <name> <rocprofv3 args...>
     local name=$1; shift
     echo "[profile] $name" >&2
@@ -23,4 +23,8 @@ step pmc_sq --pmc SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_B
 step pmc_sq2 --pmc SQ_INSTS_SALU SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_ANY SQ_WAIT_INST_ANY SQ_WAIT_ANY || exit 1
 step pmc_sq3 --pmc SQ_THREAD_CYCLES_VALU SQ_INST_CYCLES_SALU SQ_INSTS_BRANCH SQ_INSTS_SMEM SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE || exit 1
 step pmc_grbm --pmc GRBM_GUI_ACTIVE || exit 1
-python tools/pmc_summary.py $OUT > $OUT/summary.json
+python tools/pmc_summary.py $OUT --update gpurun_out/pmc_summary_$TAG.json --key ${PMC_KEY:-d12_1920x1080_n1} \
+    > $OUT/summary.json
+# keep what is judged (summary, kernel stats); the per-dispatch CSVs stay on the box
+cp $OUT/trace/run_kernel_stats.csv $OUT/kernel_stats.csv
+find $OUT -name "run_*.csv" -delete
