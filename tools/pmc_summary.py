@@ -53,9 +53,9 @@ def summarise(root: Path) -> dict:
             continue
         fam = family(row["Kernel_Name"])
         dur[fam].append((int(row["End_Timestamp"]) - int(row["Start_Timestamp"])) / 1e6)
-        out[fam].setdefault("vgpr", int(row.get("VGPR_Count") or row.get("Arch_VGPR_Count") or 0))
-        out[fam].setdefault("sgpr", int(row.get("SGPR_Count") or 0))
-        out[fam].setdefault("lds_bytes", int(row.get("LDS_Block_Size") or 0))
+        # register and LDS sizes are not copied from the trace: its VGPR/LDS fields are
+        # allocation granules, not counts; the compiler's -Rpass-analysis=kernel-resource-usage
+        # figures are in DESIGN.md
         out[fam].setdefault("kernel_name", row["Kernel_Name"][:160])
     for fam, d in dur.items():
         out[fam]["dispatches"] = len(d)
