@@ -362,8 +362,8 @@ __global__ __launch_bounds__(256) void k_brick_codes(const int32_t *__restrict__
 
 // Voxelise `work` on the current GPU in batches and hash-cons the codes on
 // `threads` host threads, overlapping batch k + 1 on the GPU with batch k on
-// the host.  Returns false when the GPU path is unavailable (the caller then
-// builds on the host); node ids written so far are dropped by the renumbering.
+// the host.  Returns false when no GPU could run the voxel kernel; the caller
+// then fails the build with OCH_E_NODEV (no host fallback).
 bool build_bricks_gpu(const Terrain &tr, NodeStore &ns, int threads, const std::vector<uint32_t> &work, int G,
                       std::vector<uint32_t> &brick_root, std::vector<BrickStats> &stats, double *gpu_seconds)
 {
