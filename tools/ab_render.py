@@ -26,6 +26,8 @@ def main():
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--cache", default="/tmp/och_terrain_cache.npz")
     ap.add_argument("--out", default="gpurun_out/ab.json")
+    ap.add_argument("--bounce", action="store_true",
+                    help="time config 5 instead (codes render with one secondary ray per hit pixel)")
     ap.add_argument("--pipelined", type=int, default=0,
                     help="also time this many bench-style steps per arm and round (codes render + shade over 3 "
                          "streams in flight, as bench.py), reporting wall-clock Mrays/s")
@@ -51,24 +53,34 @@ def main():
     pool.set_stream(stream)
     W, H = a.width, a.height
     cams = [ort.camera((1.5, 1.5, 1.5), 0.3, p, 1.25, W, H) for p in (0.0, -0.6)]
-    frames = [torch.empty(2 * W * H, dtype=torch.int32, device=dev) for _ in arms]
+    if a.bounce:
+        frames = [torch.empty(2 * W * H, dtype=torch.uint8, device=dev) for _ in arms]
+    else:
+        frames = [torch.empty(2 * W * H, dtype=torch.int32, device=dev) for _ in arms]
     defaults = {k: pool.get_option(k) for k in pool.OPTIONS}
 
     def apply(arm):
         for k, v in defaults.items():
             pool.set_option(k, arm.get(k, v))
 
-    if any(arm.get("tile_order") == 2 for arm in arms):
-        pool.plan_views(cams, 8, 0, 1)      # the launch order of tile_order=2 (same geometry as below)
+    def plan_for(arm):
+        # the launch order of tile_order=2 (same geometry as below); the plan is
+        # keyed by the block size and the bounce compaction, so each arm plans its own
+        if arm.get("tile_order") == 2:
+            pool.plan_views(cams, 8, 0, 1)
 
     times = [[] for _ in arms]
     for r in range(a.rounds + 1):
         for i, arm in enumerate(arms):
             apply(arm)
+            plan_for(arm)
             for _ in range(a.reps):
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record(stream)
-                pool.render_views_dev(cams, frames[i], 8, 0, 1)
+                if a.bounce:
+                    pool.render_codes_views_dev(cams, frames[i], 8, 0, 1, True)
+                else:
+                    pool.render_views_dev(cams, frames[i], 8, 0, 1)
                 e1.record(stream)
                 torch.cuda.synchronize()
                 if r:
@@ -86,12 +98,13 @@ def main():
         for r in range(a.rounds + 1):
             for i, arm in enumerate(arms):
                 apply(arm)
+                plan_for(arm)
                 torch.cuda.synchronize()
                 t0 = time.perf_counter()
                 for k in range(a.pipelined):
                     pool.set_stream(streams[k % 3])
                     with torch.cuda.stream(streams[k % 3]):
-                        sfs[k % 3].render(cams)
+                        sfs[k % 3].render(cams, a.bounce)
                 torch.cuda.synchronize()
                 if r:
                     walls[i].append(time.perf_counter() - t0)
