@@ -307,8 +307,9 @@ typedef struct och_terrain_params {
     int32_t rand_kind;      /* 0 = glibc rand() default seed, 1 = MSVC rand() */
     int32_t threads;        /* 0 = all hardware threads */
     int32_t use_gpu;        /* 1: voxelise 32^3 bricks on the current GPU (depth >= 5; smaller trees
-                               are built on the host), host threads hash-cons the leaf codes;
-                               OCH_E_NODEV if no GPU can run the kernel.  0: host threads only.
+                               are built on the host); a DAG (dedup = 1) is also hash-consed on
+                               the GPU, an expanded tree allocated by host threads;
+                               OCH_E_NODEV if no GPU can run the kernels.  0: host threads only.
                                Both give the same pool, slot for slot. */
 } och_terrain_params;
 

@@ -96,9 +96,9 @@ class NodePool:
 
 def build_terrain(depth: int, tunnels: bool = True, dedup: bool = True, rand_kind: str = "glibc",
                   threads: int = 0, use_gpu: bool = False) -> NodePool:
-    """The demo world as a node pool.  use_gpu=True voxelises on the current
-    GPU (och_terrain_params.use_gpu; raises OchError OCH_E_NODEV without
-    one); the pool is the same either way."""
+    """The demo world as a node pool.  use_gpu=True voxelises (and, for a DAG,
+    hash-conses) on the current GPU (och_terrain_params.use_gpu; raises
+    OchError OCH_E_NODEV without one); the pool is the same either way."""
     params = TerrainParams(int(depth), int(tunnels), int(dedup), 1 if rand_kind == "msvc" else 0,
                            int(threads), int(bool(use_gpu)))
     hp = HostPool()

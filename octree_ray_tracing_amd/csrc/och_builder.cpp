@@ -19,10 +19,10 @@
 // surface, 2 * 10^10 evaluations at depth 12 -- runs on the GPU instead
 // (k_brick_codes): one workgroup per 32^3 brick writes the brick's 4096
 // leaf-level nodes as 24-bit codes (3 bits per child voxel), its voxel
-// histogram and whether all its leaves are equal.  Host threads hash-cons the
-// codes bottom-up exactly as they do their own voxels, batch after batch,
-// while the GPU computes the next batch; bricks of one repeated leaf (solid
-// stone away from the tunnels) reuse one reduction.  Same DAG, same numbering.
+// histogram and whether all its leaves are equal.  A DAG is then hash-consed
+// on the GPU too (build_dag_gpu, below) and only renumbered on the host; an
+// expanded tree's nodes are allocated by host threads from the codes, batch
+// after batch, while the GPU computes the next batch.  Same pool either way.
 #include <hip/hip_runtime.h>
 #include <sched.h>
 #include <sys/mman.h>
@@ -58,11 +58,15 @@ int default_threads()
     return std::max(1u, std::min(std::thread::hardware_concurrency(), 256u));
 }
 
+// Zeroed, lazily backed; transparent huge pages where the kernel allows them
+// (the hash table and the leaf map are probed at random: fewer TLB misses).
 template <class T>
 T *map_zeroed(size_t count)
 {
     void *p = mmap(nullptr, count * sizeof(T), PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS | MAP_NORESERVE, -1, 0);
-    return p == MAP_FAILED ? nullptr : static_cast<T *>(p);
+    if (p == MAP_FAILED) return nullptr;
+    (void)madvise(p, count * sizeof(T), MADV_HUGEPAGE);
+    return static_cast<T *>(p);
 }
 
 template <class T>
@@ -71,7 +75,7 @@ void unmap(T *p, size_t count)
     if (p) munmap(p, count * sizeof(T));
 }
 
-inline uint64_t mix64(uint64_t h)
+__host__ __device__ inline uint64_t mix64(uint64_t h)
 {
     h ^= h >> 33;
     h *= 0xFF51AFD7ED558CCDull;
@@ -432,9 +436,14 @@ bool build_bricks_gpu(const Terrain &tr, NodeStore &ns, int threads, const std::
         std::vector<std::vector<uint32_t>> ids(threads, std::vector<uint32_t>(kLeaves));
         const auto t0 = std::chrono::steady_clock::now();
         if (n_batches && !launch(0)) return false;
+        double wait_s = 0.0, host_s = 0.0;
+        size_t mixed = 0;
         for (size_t batch = 0; batch < n_batches; ++batch) {
             const int k = (int)(batch & 1);
+            const auto w0 = std::chrono::steady_clock::now();
             BUILD_HIP(hipEventSynchronize(done[k]));
+            const auto w1 = std::chrono::steady_clock::now();
+            wait_s += std::chrono::duration<double>(w1 - w0).count();
             // the other buffer is free: its batch was consumed in the previous round
             if (batch + 1 < n_batches && !launch(batch + 1)) return false;
             const size_t lo = batch * B, n = std::min(B, n_work - lo);
@@ -482,13 +491,345 @@ bool build_bricks_gpu(const Terrain &tr, NodeStore &ns, int threads, const std::
                 }
                 brick_root[work[lo + i]] = root;
             });
+            for (size_t i = 0; i < n; ++i) mixed += h_info[k][i * 8] == kMixed;
+            host_s += std::chrono::duration<double>(std::chrono::steady_clock::now() - w1).count();
         }
+        if (std::getenv("OCH_BUILD_TRACE"))
+            std::fprintf(stderr, "[och_build] bricks: %zu (%zu mixed), %zu batches, waited %.3f s, host %.3f s\n", n_work,
+                         mixed, (size_t)n_batches, wait_s, host_s);
         if (gpu_seconds) *gpu_seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
         return true;
     };
     const bool ok = run();
     cleanup();
     return ok;
+}
+
+// ------------------------------------------------------------ GPU hash-consing
+//
+// A DAG build (dedup) with use_gpu interns on the GPU as well; the host only
+// renumbers.  Leaf-level nodes are interned by their 24-bit code through a
+// direct map (k_intern_codes).  Every level above is one pair of dispatches
+// over all its nodes:
+//   k_intern -- each node gathers its eight child ids (written by an earlier
+//               dispatch); empty nodes stop there.  The rest probe one open-
+//               addressing table shared by all levels.  An empty slot is
+//               claimed by compare-and-swap with the node's own index (kCand |
+//               index) and the claimant allocates the node's id and writes its
+//               record.  A node meeting a claimed slot compares its children
+//               with the claimant's, gathered again from the same earlier
+//               dispatch's ids; a slot holding a finished id is compared with
+//               that node's record, written by an earlier dispatch.
+//   k_settle -- each node takes its id (its own or its claimant's) and each
+//               claimant turns its slot into the finished id.
+// No dispatch reads what another workgroup writes in the same dispatch except
+// through the atomics, so the per-XCD L2s need no coherence beyond dispatch
+// boundaries.  Ids come from one counter in claim order and differ from run to
+// run; the breadth-first renumbering makes the pool identical to the host
+// build's, slot for slot.
+
+constexpr uint32_t kCand = 0x80000000u;
+constexpr uint32_t kNoSlot = 0xFFFFFFFFu;
+
+struct GpuStore {
+    uint32_t *nodes;                 // cap x 8 child words
+    uint8_t *level;                  // height above the voxels of each id
+    uint32_t *next;                  // id counter, starts at 1 (0 = empty)
+    uint32_t *table;                 // tmask + 1 slots: 0, kCand | node index (this level), or an id
+    uint32_t *leaf_id;               // 2^24 leaf codes -> id
+    uint32_t *overflow;              // 1: capacity exhausted, 2: table exhausted
+    unsigned long long *tree_nodes;  // nodes of the expanded tree
+    uint32_t cap, tmask;
+};
+
+// One level: nb grids of side n (node index = grid * n^3 + (z * n + y) * n + x),
+// children in the previous level's grids of side 2n.
+struct GpuLevel {
+    const uint32_t *src;   // child ids, or leaf codes (codes = 1: the child id is leaf_id[code])
+    int codes;
+    int log2n;
+    uint32_t count;        // nb * n^3
+    int h;
+};
+
+__device__ inline void count_nodes(const GpuStore &S, bool nz)
+{
+    const uint64_t b = __ballot(nz);
+    if ((threadIdx.x & 63u) == 0 && b) atomicAdd(S.tree_nodes, (unsigned long long)__popcll(b));
+}
+
+__device__ inline uint32_t alloc_node(const GpuStore &S, const uint32_t c[8], int h)
+{
+    const uint32_t id = atomicAdd(S.next, 1u);
+    if (id >= S.cap) {
+        atomicOr(S.overflow, 1u);
+        return 0;
+    }
+    uint4 *dst = reinterpret_cast<uint4 *>(S.nodes + (size_t)id * 8);
+    dst[0] = make_uint4(c[0], c[1], c[2], c[3]);
+    dst[1] = make_uint4(c[4], c[5], c[6], c[7]);
+    S.level[id] = (uint8_t)h;
+    return id;
+}
+
+__device__ inline bool gather(const GpuStore &S, const GpuLevel &L, uint32_t idx, uint32_t c[8])
+{
+    const uint32_t n = 1u << L.log2n, m = 2u * n;
+    const uint32_t g = idx >> (3 * L.log2n), r = idx & ((1u << (3 * L.log2n)) - 1u);
+    const uint32_t x = r & (n - 1u), y = (r >> L.log2n) & (n - 1u), z = r >> (2 * L.log2n);
+    const size_t base = (size_t)g * m * m * m;
+    bool any = false;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        const uint32_t cx = 2u * x + (k & 1), cy = 2u * y + ((k >> 1) & 1), cz = 2u * z + ((k >> 2) & 1);
+        uint32_t v = L.src[base + ((size_t)cz * m + cy) * m + cx];
+        if (L.codes && v) v = S.leaf_id[v];
+        c[k] = v;
+        any |= v != 0;
+    }
+    return any;
+}
+
+__device__ inline uint32_t node_slot(const uint32_t c[8], int h, uint32_t mask)
+{
+    uint64_t hs = mix64((uint64_t)h * 0x9E3779B97F4A7C15ull ^ ((uint64_t)c[1] << 32 | c[0]));
+    hs = mix64(hs ^ ((uint64_t)c[3] << 32 | c[2]));
+    hs = mix64(hs ^ ((uint64_t)c[5] << 32 | c[4]));
+    hs = mix64(hs ^ ((uint64_t)c[7] << 32 | c[6]));
+    return (uint32_t)hs & mask;
+}
+
+__global__ __launch_bounds__(256) void k_intern_codes(GpuStore S, const uint32_t *__restrict__ codes, uint32_t count)
+{
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t code = i < count ? codes[i] : 0u;
+    count_nodes(S, code != 0);
+    if (!code) return;
+    const uint32_t v = __hip_atomic_load(&S.leaf_id[code], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (v != 0 || atomicCAS(&S.leaf_id[code], 0u, kCand) != 0u) return;
+    uint32_t c[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) c[k] = (code >> (3 * k)) & 7u;
+    __hip_atomic_store(&S.leaf_id[code], alloc_node(S, c, 0), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__global__ __launch_bounds__(256) void k_intern(GpuStore S, GpuLevel L, uint32_t *__restrict__ rep,
+                                                uint32_t *__restrict__ slot)
+{
+    const uint32_t idx = blockIdx.x * blockDim.x + threadIdx.x;
+    uint32_t c[8];
+    const bool any = idx < L.count && gather(S, L, idx, c);
+    count_nodes(S, any);
+    if (idx >= L.count) return;
+    slot[idx] = kNoSlot;
+    if (!any) {
+        rep[idx] = 0;
+        return;
+    }
+    uint32_t i = node_slot(c, L.h, S.tmask);
+    for (uint32_t probe = 0; probe <= S.tmask; ++probe, i = (i + 1u) & S.tmask) {
+        uint32_t v = __hip_atomic_load(&S.table[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (v == 0) {
+            v = atomicCAS(&S.table[i], 0u, kCand | idx);
+            if (v == 0) {
+                rep[idx] = alloc_node(S, c, L.h);
+                slot[idx] = i;
+                return;
+            }
+        }
+        bool same = true;
+        if (v & kCand) {
+            uint32_t d[8];
+            gather(S, L, v & ~kCand, d);
+#pragma unroll
+            for (int k = 0; k < 8; ++k) same &= d[k] == c[k];
+        } else {
+            const uint4 *rec = reinterpret_cast<const uint4 *>(S.nodes + (size_t)v * 8);
+            const uint4 a = rec[0], b = rec[1];
+            same = S.level[v] == (uint8_t)L.h && a.x == c[0] && a.y == c[1] && a.z == c[2] && a.w == c[3] &&
+                   b.x == c[4] && b.y == c[5] && b.z == c[6] && b.w == c[7];
+        }
+        if (same) {
+            rep[idx] = v;
+            return;
+        }
+    }
+    atomicOr(S.overflow, 2u);
+    rep[idx] = 0;
+}
+
+// dst[dst_index ? dst_index[idx] : idx] = the node's id.
+__global__ __launch_bounds__(256) void k_settle(GpuStore S, uint32_t count, const uint32_t *__restrict__ rep,
+                                                const uint32_t *__restrict__ slot, uint32_t *__restrict__ dst,
+                                                const uint32_t *__restrict__ dst_index)
+{
+    const uint32_t idx = blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= count) return;
+    uint32_t r = rep[idx];
+    if (r & kCand) r = rep[r & ~kCand];
+    dst[dst_index ? dst_index[idx] : idx] = r;
+    const uint32_t s = slot[idx];
+    if (s != kNoSlot) S.table[s] = r;
+}
+
+// The whole DAG on the current GPU: bricks voxelised (k_brick_codes) and
+// interned batch by batch, then the levels above the bricks.  On return the
+// store's records are on the host: nodes (used x 8), level (used); ids 1 ..
+// used - 1, `root` its root id.  Returns a status.
+int build_dag_gpu(const Terrain &tr, uint32_t cap, const std::vector<uint32_t> &work, int G, std::vector<uint32_t> &nodes,
+                  std::vector<uint8_t> &level, uint32_t &used, uint32_t &root, BrickStats &total, bool trace)
+{
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return OCH_E_NODEV;
+    const size_t n_work = work.size();
+    const size_t B = 8192;                                    // bricks per batch
+    const size_t cols = (size_t)tr.dim * tr.dim, grid_cells = (size_t)G * G * G;
+    uint32_t tsize = 1;
+    while (tsize < 2 * cap) tsize <<= 1;
+    const size_t rep_cap = std::max(B * 512, grid_cells / 8);
+    std::vector<void *> bufs;
+    hipStream_t st = nullptr;
+    auto dalloc = [&](void **p, size_t bytes) {
+        if (hipMalloc(p, bytes) != hipSuccess) return false;
+        bufs.push_back(*p);
+        return true;
+    };
+    int status = OCH_OK;
+    auto run = [&]() -> int {
+        int32_t *d_heights;
+        uint8_t *d_tops;
+        uint32_t *d_enc, *d_work, *d_codes, *d_info, *d_rep, *d_slot, *d_a, *d_b, *d_grid[2];
+        GpuStore S{};
+        S.cap = cap;
+        S.tmask = tsize - 1;
+        bool ok = dalloc((void **)&d_heights, cols * 4) && dalloc((void **)&d_tops, cols) &&
+                  dalloc((void **)&d_enc, std::max<size_t>(n_work, 1) * 4) &&
+                  dalloc((void **)&d_work, std::max<size_t>(n_work, 1) * 4) && dalloc((void **)&d_codes, B * kLeaves * 4) &&
+                  dalloc((void **)&d_info, std::max<size_t>(n_work, 1) * 32) && dalloc((void **)&d_rep, rep_cap * 4) &&
+                  dalloc((void **)&d_slot, rep_cap * 4) && dalloc((void **)&d_a, B * 512 * 4) &&
+                  dalloc((void **)&d_b, B * 64 * 4) && dalloc((void **)&d_grid[0], grid_cells * 4) &&
+                  dalloc((void **)&d_grid[1], grid_cells * 4) && dalloc((void **)&S.nodes, (size_t)cap * 32) &&
+                  dalloc((void **)&S.level, cap) && dalloc((void **)&S.next, 64) &&
+                  dalloc((void **)&S.table, (size_t)tsize * 4) && dalloc((void **)&S.leaf_id, (size_t)4 << 24);
+        if (!ok) return OCH_E_NOMEM;
+        S.overflow = S.next + 1;
+        S.tree_nodes = reinterpret_cast<unsigned long long *>(S.next + 2);
+        if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) return OCH_E_HIP;
+        std::vector<uint32_t> enc(n_work);
+        for (size_t i = 0; i < n_work; ++i) {
+            const uint32_t w = work[i];
+            enc[i] = (w % G) | ((w / G) % G) << 10 | (w / (G * G)) << 20;
+        }
+        const uint32_t one = 1;
+#define DAG_HIP(expr)                          \
+    do {                                       \
+        if ((expr) != hipSuccess) return OCH_E_HIP; \
+    } while (0)
+        DAG_HIP(hipMemcpyAsync(d_heights, tr.heights.data(), cols * 4, hipMemcpyHostToDevice, st));
+        DAG_HIP(hipMemcpyAsync(d_tops, tr.tops.data(), cols, hipMemcpyHostToDevice, st));
+        DAG_HIP(hipMemcpyAsync(d_enc, enc.data(), n_work * 4, hipMemcpyHostToDevice, st));
+        DAG_HIP(hipMemcpyAsync(d_work, work.data(), n_work * 4, hipMemcpyHostToDevice, st));
+        DAG_HIP(hipMemsetAsync(S.next, 0, 64, st));
+        DAG_HIP(hipMemcpyAsync(S.next, &one, 4, hipMemcpyHostToDevice, st));
+        DAG_HIP(hipMemsetAsync(S.table, 0, (size_t)tsize * 4, st));
+        DAG_HIP(hipMemsetAsync(S.leaf_id, 0, (size_t)4 << 24, st));
+        DAG_HIP(hipMemsetAsync(S.nodes, 0, 32, st));
+        DAG_HIP(hipMemsetAsync(d_grid[0], 0, grid_cells * 4, st));
+        auto blocks = [](size_t n) { return dim3((unsigned)((n + 255) / 256)); };
+        auto level_pass = [&](const GpuLevel &L, uint32_t *dst, const uint32_t *dst_index) -> bool {
+            if (L.count == 0) return true;
+            hipLaunchKernelGGL(k_intern, blocks(L.count), dim3(256), 0, st, S, L, d_rep, d_slot);
+            hipLaunchKernelGGL(k_settle, blocks(L.count), dim3(256), 0, st, S, L.count, d_rep, d_slot, dst, dst_index);
+            return hipGetLastError() == hipSuccess;
+        };
+        for (size_t lo = 0; lo < n_work; lo += B) {
+            const uint32_t n = (uint32_t)std::min(B, n_work - lo);
+            hipLaunchKernelGGL(k_brick_codes, dim3(n), dim3(256), 0, st, d_heights, d_tops, tr.dim, tr.tunnels ? 1 : 0,
+                               d_enc + lo, d_codes, d_info + lo * 8);
+            hipLaunchKernelGGL(k_intern_codes, blocks((size_t)n * kLeaves), dim3(256), 0, st, S, d_codes,
+                               n * (uint32_t)kLeaves);
+            DAG_HIP(hipGetLastError());
+            // brick levels 1..4: 8^3, 4^3, 2^3, 1 node per brick; the roots land in the grid
+            if (!level_pass({d_codes, 1, 3, n * 512u, 1}, d_a, nullptr) ||
+                !level_pass({d_a, 0, 2, n * 64u, 2}, d_b, nullptr) || !level_pass({d_b, 0, 1, n * 8u, 3}, d_a, nullptr) ||
+                !level_pass({d_a, 0, 0, n, 4}, d_grid[0], d_work + lo))
+                return OCH_E_HIP;
+        }
+        // levels above the bricks, one grid of side G / 2, G / 4, ... 1
+        int cur = 0, log2n = 0;
+        while ((1 << (log2n + 1)) < G) ++log2n;   // G = 2^(log2n + 1)
+        for (int h = kBrickLog2; h < tr.depth; ++h, --log2n) {
+            if (!level_pass({d_grid[cur], 0, log2n, 1u << (3 * log2n), h}, d_grid[cur ^ 1], nullptr)) return OCH_E_HIP;
+            cur ^= 1;
+        }
+        uint32_t head[4] = {0, 0, 0, 0};
+        DAG_HIP(hipMemcpyAsync(head, S.next, 16, hipMemcpyDeviceToHost, st));
+        DAG_HIP(hipMemcpyAsync(&root, d_grid[cur], 4, hipMemcpyDeviceToHost, st));
+        std::vector<uint32_t> info(n_work * 8);
+        DAG_HIP(hipMemcpyAsync(info.data(), d_info, n_work * 32, hipMemcpyDeviceToHost, st));
+        DAG_HIP(hipStreamSynchronize(st));
+        if (head[1]) return OCH_E_CAPACITY;
+        used = std::min(head[0], cap);
+        total.tree_nodes = (uint64_t)head[2] | (uint64_t)head[3] << 32;
+        for (size_t i = 0; i < n_work; ++i)
+            for (int v = 0; v < 6; ++v) total.hist[v] += info[i * 8 + 1 + v];
+        nodes.resize((size_t)used * 8);
+        level.resize(used);
+        DAG_HIP(hipMemcpyAsync(nodes.data(), S.nodes, (size_t)used * 32, hipMemcpyDeviceToHost, st));
+        DAG_HIP(hipMemcpyAsync(level.data(), S.level, used, hipMemcpyDeviceToHost, st));
+        DAG_HIP(hipStreamSynchronize(st));
+#undef DAG_HIP
+        if (trace) std::fprintf(stderr, "[och_build] gpu dag: %zu bricks, %u ids\n", n_work, used);
+        return OCH_OK;
+    };
+    status = run();
+    if (st) {
+        (void)hipStreamSynchronize(st);
+        (void)hipStreamDestroy(st);
+    }
+    for (void *p : bufs) (void)hipFree(p);
+    return status;
+}
+
+// Breadth-first renumbering of a node store (ids 1 .. used - 1, records of 8
+// child words, level[id] = height above the voxels): level by level from the
+// root, children in slot order; 1-based (h_octree, slot 0 never used) or
+// 0-based octree.  *out: malloc'd n_out x 8 words (one zero node when empty).
+int renumber(const uint32_t *store, const uint8_t *level, uint32_t used, uint32_t root, int depth, int base,
+             uint32_t **out, uint32_t *n_out)
+{
+    std::vector<uint32_t> newid(used, 0);
+    std::vector<uint32_t> order;
+    if (root) {
+        order.reserve(1024);
+        std::vector<uint32_t> lv{root};
+        newid[root] = (uint32_t)base;
+        order.push_back(root);
+        for (int l = 1; l < depth; ++l) {
+            std::vector<uint32_t> nxt;
+            for (uint32_t v : lv) {
+                const uint32_t *c = store + (size_t)v * 8;
+                for (int k = 0; k < 8; ++k)
+                    if (c[k] && !(newid[c[k]] || c[k] == root)) {
+                        newid[c[k]] = (uint32_t)(order.size() + base);
+                        order.push_back(c[k]);
+                        nxt.push_back(c[k]);
+                    }
+            }
+            lv.swap(nxt);
+        }
+    }
+    *n_out = (uint32_t)std::max<size_t>(order.size(), 1);
+    uint32_t *nodes = static_cast<uint32_t *>(std::calloc((size_t)*n_out * 8, 4));
+    if (!nodes) return OCH_E_NOMEM;
+    for (size_t i = 0; i < order.size(); ++i) {
+        const uint32_t v = order[i];
+        const uint32_t *c = store + (size_t)v * 8;
+        const bool leaf = level[v] == 0;
+        for (int k = 0; k < 8; ++k) nodes[i * 8 + k] = (leaf || !c[k]) ? c[k] : newid[c[k]];
+    }
+    *out = nodes;
+    return OCH_OK;
 }
 
 }  // namespace
@@ -510,6 +851,14 @@ OCH_API int och_build_terrain(const och_terrain_params *params, och_host_pool *o
     if (depth < 1 || depth > 12) return OCH_E_INVALID;
     if (!params->dedup && depth > 10) return OCH_E_INVALID;   // expanded tree would exceed 1 GB
     const auto t_start = std::chrono::steady_clock::now();
+    // OCH_BUILD_TRACE=1: phase times on stderr
+    const bool trace = std::getenv("OCH_BUILD_TRACE") != nullptr;
+    auto phase = [&, t_last = t_start](const char *name) mutable {
+        if (!trace) return;
+        const auto now = std::chrono::steady_clock::now();
+        std::fprintf(stderr, "[och_build] %-10s %8.3f s\n", name, std::chrono::duration<double>(now - t_last).count());
+        t_last = now;
+    };
     std::memset(out, 0, sizeof *out);
     const int threads = params->threads > 0 ? params->threads : default_threads();
 
@@ -534,6 +883,7 @@ OCH_API int och_build_terrain(const och_terrain_params *params, och_host_pool *o
         for (size_t i = 0; i < tr.tops.size(); ++i) tr.tops[i] = (uint8_t)(2 + (r.next() > 0x7FFFFFFF / 2));
     }
 
+    phase("columns");
     const int s_log2 = std::min(depth, 5);
     const int S = 1 << s_log2, G = dim / S;
     tr.brick_hmax.assign((size_t)G * G, -1);
@@ -545,113 +895,101 @@ OCH_API int och_build_terrain(const och_terrain_params *params, och_host_pool *o
             tr.brick_hmax[(size_t)by * G + bx] = hm;
         }
 
-    NodeStore ns;
-    const uint32_t cap = params->dedup ? (depth <= 8 ? (1u << 20) : depth <= 10 ? (1u << 23) : (1u << 28))
+    // DAG capacity: 3x the unique nodes of the default terrain (19 318 / 334 025 /
+    // 4 980 409 at depth 8 / 10 / 12); the hash table is twice the capacity
+    const uint32_t cap = params->dedup ? (depth <= 8 ? (1u << 20) : depth <= 10 ? (1u << 23) : (1u << 24))
                                        : (uint32_t)std::min<uint64_t>(1ull << 28, 48ull << (2 * depth));
-    if (!ns.init(cap, params->dedup != 0)) {
-        ns.release();
-        return OCH_E_NOMEM;
-    }
-
+    phase("init");
     // Bricks that reach below the highest surface of their columns.
     std::vector<uint32_t> work;
     for (int bz = 0; bz < G; ++bz)
         for (int by = 0; by < G; ++by)
             for (int bx = 0; bx < G; ++bx)
                 if (bz * S <= tr.brick_hmax[(size_t)by * G + bx]) work.push_back(((uint32_t)bz * G + by) * G + bx);
-    std::vector<uint32_t> brick_root((size_t)G * G * G, 0);
-    std::vector<BrickStats> stats(threads);
-    double gpu_s = 0.0;
-    if (params->use_gpu && s_log2 == kBrickLog2) {
-        if (!build_bricks_gpu(tr, ns, threads, work, G, brick_root, stats, &gpu_s)) {
-            ns.release();
-            return OCH_E_NODEV;   // asked for the GPU and none could run the voxel kernel
-        }
-    } else {
-        std::vector<std::vector<uint8_t>> vox(threads, std::vector<uint8_t>((size_t)S * S * S));
-        std::vector<std::vector<uint32_t>> ids(threads, std::vector<uint32_t>((size_t)S * S * S / 8));
-        parallel_for(threads, work.size(), [&](uint64_t i, int t) {
-            const uint32_t b = work[i];
-            const int bx = b % G, by = (b / G) % G, bz = b / (G * G);
-            brick_root[b] = build_brick(tr, ns, s_log2, bx, by, bz, vox[t], ids[t], stats[t]);
-        });
-    }
-    BrickStats total;
-    for (auto &s : stats) {
-        for (int k = 0; k < 8; ++k) total.hist[k] += s.hist[k];
-        total.tree_nodes += s.tree_nodes;
-    }
-    // Levels above the bricks.
-    uint32_t root = 0;
-    {
-        std::vector<uint32_t> cur = brick_root, nxt;
-        int n = G;
-        for (int h = s_log2; h < depth; ++h) {
-            const int m = n / 2;
-            nxt.assign((size_t)m * m * m, 0);
-            for (int z = 0; z < m; ++z)
-                for (int y = 0; y < m; ++y)
-                    for (int x = 0; x < m; ++x) {
-                        uint32_t c[8];
-                        bool any = false;
-                        for (int k = 0; k < 8; ++k) {
-                            const int cx = 2 * x + (k & 1), cy = 2 * y + ((k >> 1) & 1), cz = 2 * z + ((k >> 2) & 1);
-                            c[k] = cur[((size_t)cz * n + cy) * n + cx];
-                            any |= c[k] != 0;
-                        }
-                        if (any) {
-                            nxt[((size_t)z * m + y) * m + x] = ns.intern(c, h);
-                            ++total.tree_nodes;
-                        }
-                    }
-            cur.swap(nxt);
-            n = m;
-        }
-        root = cur[0];
-    }
-    if (ns.full.load()) {
-        ns.release();
-        return OCH_E_CAPACITY;
-    }
-
-    // Breadth-first renumbering: level by level from the root, children in
-    // slot order.  1-based (h_octree, slot 0 never used) or 0-based octree.
-    const uint32_t used = std::min(ns.next.load(), ns.cap);
     const int base = params->dedup ? 1 : 0;
-    std::vector<uint32_t> newid(used, 0);
-    std::vector<uint32_t> order;
-    if (root) {
-        order.reserve(1024);
-        std::vector<uint32_t> level{root};
-        newid[root] = (uint32_t)base;
-        order.push_back(root);
-        for (int l = 1; l < depth; ++l) {
-            std::vector<uint32_t> nxt;
-            for (uint32_t v : level) {
-                const uint32_t *c = ns.nodes + (size_t)v * 8;
-                for (int k = 0; k < 8; ++k)
-                    if (c[k] && !(newid[c[k]] || c[k] == root)) {
-                        newid[c[k]] = (uint32_t)(order.size() + base);
-                        order.push_back(c[k]);
-                        nxt.push_back(c[k]);
-                    }
-            }
-            level.swap(nxt);
+    BrickStats total;
+    uint32_t root = 0, n_out = 0;
+    uint32_t *nodes = nullptr;
+    if (params->use_gpu && params->dedup && s_log2 == kBrickLog2) {
+        // the whole DAG on the GPU; the host renumbers
+        std::vector<uint32_t> store;
+        std::vector<uint8_t> lvl;
+        uint32_t used = 0;
+        const int st = build_dag_gpu(tr, cap, work, G, store, lvl, used, root, total, trace);
+        if (st != OCH_OK)
+            return och::report(st, st == OCH_E_NODEV    ? "use_gpu: no HIP device"
+                                   : st == OCH_E_CAPACITY ? "GPU builder: node capacity exhausted"
+                                   : st == OCH_E_NOMEM    ? "GPU builder: device allocation failed"
+                                                          : "GPU builder: HIP error");
+        phase("gpu dag");
+        const int rs = renumber(store.data(), lvl.data(), used, root, depth, base, &nodes, &n_out);
+        if (rs != OCH_OK) return rs;
+    } else {
+        NodeStore ns;
+        if (!ns.init(cap, params->dedup != 0)) {
+            ns.release();
+            return OCH_E_NOMEM;
         }
-    }
-    const uint32_t n_out = (uint32_t)std::max<size_t>(order.size(), 1);
-    uint32_t *nodes = static_cast<uint32_t *>(std::calloc((size_t)n_out * 8, 4));
-    if (!nodes) {
+        std::vector<uint32_t> brick_root((size_t)G * G * G, 0);
+        std::vector<BrickStats> stats(threads);
+        double gpu_s = 0.0;
+        if (params->use_gpu && s_log2 == kBrickLog2) {
+            // an expanded tree: voxels from the GPU, one node per tree node on the host
+            if (!build_bricks_gpu(tr, ns, threads, work, G, brick_root, stats, &gpu_s)) {
+                ns.release();
+                return och::report(OCH_E_NODEV, "use_gpu: no HIP device could run the voxel kernel");
+            }
+        } else {
+            std::vector<std::vector<uint8_t>> vox(threads, std::vector<uint8_t>((size_t)S * S * S));
+            std::vector<std::vector<uint32_t>> ids(threads, std::vector<uint32_t>((size_t)S * S * S / 8));
+            parallel_for(threads, work.size(), [&](uint64_t i, int t) {
+                const uint32_t b = work[i];
+                const int bx = b % G, by = (b / G) % G, bz = b / (G * G);
+                brick_root[b] = build_brick(tr, ns, s_log2, bx, by, bz, vox[t], ids[t], stats[t]);
+            });
+        }
+        phase("bricks");
+        for (auto &s : stats) {
+            for (int k = 0; k < 8; ++k) total.hist[k] += s.hist[k];
+            total.tree_nodes += s.tree_nodes;
+        }
+        // Levels above the bricks.
+        {
+            std::vector<uint32_t> cur = brick_root, nxt;
+            int n = G;
+            for (int h = s_log2; h < depth; ++h) {
+                const int m = n / 2;
+                nxt.assign((size_t)m * m * m, 0);
+                for (int z = 0; z < m; ++z)
+                    for (int y = 0; y < m; ++y)
+                        for (int x = 0; x < m; ++x) {
+                            uint32_t c[8];
+                            bool any = false;
+                            for (int k = 0; k < 8; ++k) {
+                                const int cx = 2 * x + (k & 1), cy = 2 * y + ((k >> 1) & 1), cz = 2 * z + ((k >> 2) & 1);
+                                c[k] = cur[((size_t)cz * n + cy) * n + cx];
+                                any |= c[k] != 0;
+                            }
+                            if (any) {
+                                nxt[((size_t)z * m + y) * m + x] = ns.intern(c, h);
+                                ++total.tree_nodes;
+                            }
+                        }
+                cur.swap(nxt);
+                n = m;
+            }
+            root = cur[0];
+        }
+        phase("upper");
+        if (ns.full.load()) {
+            ns.release();
+            return OCH_E_CAPACITY;
+        }
+        const int rs = renumber(ns.nodes, ns.level, std::min(ns.next.load(), ns.cap), root, depth, base, &nodes, &n_out);
         ns.release();
-        return OCH_E_NOMEM;
+        if (rs != OCH_OK) return rs;
     }
-    for (size_t i = 0; i < order.size(); ++i) {
-        const uint32_t v = order[i];
-        const uint32_t *c = ns.nodes + (size_t)v * 8;
-        const bool leaf = ns.level[v] == 0;
-        for (int k = 0; k < 8; ++k) nodes[i * 8 + k] = (leaf || !c[k]) ? c[k] : newid[c[k]];
-    }
-    ns.release();
+    phase("renumber");
 
     out->nodes = nodes;
     out->n_nodes = n_out;
