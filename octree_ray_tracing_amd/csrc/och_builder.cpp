@@ -313,23 +313,24 @@ __constant__ och_terrain::Tables c_tables = {OCH_PERM_TABLE, OCH_GRAD_TABLE};
 
 // One workgroup per brick (bricks[i] = bx | by << 10 | bz << 20): the 4096
 // leaf codes, (z * 16 + y) * 16 + x order; info[i] = {the common code when
-// every leaf is equal, else kMixed; voxel counts of ids 0..7}.
+// every leaf is equal, else kMixed; voxel counts of ids 0..5; non-empty leaf codes}.
 __global__ __launch_bounds__(256) void k_brick_codes(const int32_t *__restrict__ heights, const uint8_t *__restrict__ tops,
                                                      int dim, int tunnels, const uint32_t *__restrict__ bricks,
                                                      uint32_t *__restrict__ codes, uint32_t *__restrict__ info)
 {
     __shared__ och_terrain::Tables T;
     __shared__ uint32_t hist[8], firsts[256];
+    __shared__ uint32_t leaves;   // non-empty leaf-level nodes of the brick
     __shared__ int mixed;
     for (int i = threadIdx.x; i < (int)sizeof(T); i += blockDim.x)
         reinterpret_cast<uint8_t *>(&T)[i] = reinterpret_cast<const uint8_t *>(&c_tables)[i];
     if (threadIdx.x < 8) hist[threadIdx.x] = 0;
-    if (threadIdx.x == 0) mixed = 0;
+    if (threadIdx.x == 0) mixed = 0, leaves = 0;
     __syncthreads();
     const uint32_t b = bricks[blockIdx.x];
     const int x0 = (int)(b & 1023u) * kBrick, y0 = (int)((b >> 10) & 1023u) * kBrick, z0 = (int)(b >> 20) * kBrick;
     uint32_t cnt[5] = {0, 0, 0, 0, 0}, other = 0;
-    uint32_t first = 0;
+    uint32_t first = 0, nonempty = 0;
     bool same = true;
     for (int leaf = threadIdx.x; leaf < kLeaves; leaf += blockDim.x) {
         const int lx = leaf & 15, ly = (leaf >> 4) & 15, lz = leaf >> 8;
@@ -344,12 +345,14 @@ __global__ __launch_bounds__(256) void k_brick_codes(const int32_t *__restrict__
             else ++other;
         }
         codes[(size_t)blockIdx.x * kLeaves + leaf] = code;
+        nonempty += code != 0;
         if (leaf == (int)threadIdx.x) first = code;
         same &= code == first;
     }
     for (int v = 0; v < 5; ++v)
         if (cnt[v]) atomicAdd(&hist[v], cnt[v]);
     if (other) atomicAdd(&hist[5], other);        // ids above 4 do not occur in this terrain
+    if (nonempty) atomicAdd(&leaves, nonempty);
     firsts[threadIdx.x] = first;
     if (!same) mixed = 1;
     __syncthreads();
@@ -357,6 +360,7 @@ __global__ __launch_bounds__(256) void k_brick_codes(const int32_t *__restrict__
     __syncthreads();
     if (threadIdx.x == 0) info[(size_t)blockIdx.x * 8] = mixed ? kMixed : firsts[0];
     if (threadIdx.x < 6) info[(size_t)blockIdx.x * 8 + 1 + threadIdx.x] = hist[threadIdx.x];
+    if (threadIdx.x == 6) info[(size_t)blockIdx.x * 8 + 7] = leaves;
 }
 
 #define BUILD_HIP(expr)                       \
@@ -538,7 +542,7 @@ struct GpuStore {
     uint32_t *table;                 // tmask + 1 slots: 0, kCand | node index (this level), or an id
     uint32_t *leaf_id;               // 2^24 leaf codes -> id
     uint32_t *overflow;              // 1: capacity exhausted, 2: table exhausted
-    unsigned long long *tree_nodes;  // nodes of the expanded tree
+    unsigned long long *tree_nodes;  // kCounters partial counts of expanded-tree nodes, 128 B apart
     uint32_t cap, tmask;
 };
 
@@ -552,10 +556,19 @@ struct GpuLevel {
     int h;
 };
 
+constexpr int kCounters = 64;
+
+// Block-wide count, then one atomic per block on one of kCounters addresses.
 __device__ inline void count_nodes(const GpuStore &S, bool nz)
 {
+    __shared__ uint32_t block_count;
+    if (threadIdx.x == 0) block_count = 0;
+    __syncthreads();
     const uint64_t b = __ballot(nz);
-    if ((threadIdx.x & 63u) == 0 && b) atomicAdd(S.tree_nodes, (unsigned long long)__popcll(b));
+    if ((threadIdx.x & 63u) == 0 && b) atomicAdd(&block_count, (uint32_t)__popcll(b));
+    __syncthreads();
+    if (threadIdx.x == 0 && block_count)
+        atomicAdd(S.tree_nodes + 16 * (blockIdx.x % kCounters), (unsigned long long)block_count);
 }
 
 __device__ inline uint32_t alloc_node(const GpuStore &S, const uint32_t c[8], int h)
@@ -602,11 +615,11 @@ __device__ inline uint32_t node_slot(const uint32_t c[8], int h, uint32_t mask)
 __global__ __launch_bounds__(256) void k_intern_codes(GpuStore S, const uint32_t *__restrict__ codes, uint32_t count)
 {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    const uint32_t code = i < count ? codes[i] : 0u;
-    count_nodes(S, code != 0);
+    const uint32_t code = i < count ? codes[i] : 0u;   // counted by k_brick_codes (info[7])
     if (!code) return;
-    const uint32_t v = __hip_atomic_load(&S.leaf_id[code], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (v != 0 || atomicCAS(&S.leaf_id[code], 0u, kCand) != 0u) return;
+    // A plain (cached) load: a stale 0 only sends the thread to the CAS, which
+    // sees the truth; most codes were interned by an earlier batch.
+    if (S.leaf_id[code] != 0 || atomicCAS(&S.leaf_id[code], 0u, kCand) != 0u) return;
     uint32_t c[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k) c[k] = (code >> (3 * k)) & 7u;
@@ -628,7 +641,7 @@ __global__ __launch_bounds__(256) void k_intern(GpuStore S, GpuLevel L, uint32_t
     }
     uint32_t i = node_slot(c, L.h, S.tmask);
     for (uint32_t probe = 0; probe <= S.tmask; ++probe, i = (i + 1u) & S.tmask) {
-        uint32_t v = __hip_atomic_load(&S.table[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        uint32_t v = S.table[i];   // a stale 0 is corrected by the CAS; claims and ids are never stale
         if (v == 0) {
             v = atomicCAS(&S.table[i], 0u, kCand | idx);
             if (v == 0) {
@@ -709,11 +722,11 @@ int build_dag_gpu(const Terrain &tr, uint32_t cap, const std::vector<uint32_t> &
                   dalloc((void **)&d_slot, rep_cap * 4) && dalloc((void **)&d_a, B * 512 * 4) &&
                   dalloc((void **)&d_b, B * 64 * 4) && dalloc((void **)&d_grid[0], grid_cells * 4) &&
                   dalloc((void **)&d_grid[1], grid_cells * 4) && dalloc((void **)&S.nodes, (size_t)cap * 32) &&
-                  dalloc((void **)&S.level, cap) && dalloc((void **)&S.next, 64) &&
+                  dalloc((void **)&S.level, cap) && dalloc((void **)&S.next, 256 + 128 * kCounters) &&
                   dalloc((void **)&S.table, (size_t)tsize * 4) && dalloc((void **)&S.leaf_id, (size_t)4 << 24);
         if (!ok) return OCH_E_NOMEM;
         S.overflow = S.next + 1;
-        S.tree_nodes = reinterpret_cast<unsigned long long *>(S.next + 2);
+        S.tree_nodes = reinterpret_cast<unsigned long long *>(S.next + 64);
         if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) return OCH_E_HIP;
         std::vector<uint32_t> enc(n_work);
         for (size_t i = 0; i < n_work; ++i) {
@@ -729,7 +742,7 @@ int build_dag_gpu(const Terrain &tr, uint32_t cap, const std::vector<uint32_t> &
         DAG_HIP(hipMemcpyAsync(d_tops, tr.tops.data(), cols, hipMemcpyHostToDevice, st));
         DAG_HIP(hipMemcpyAsync(d_enc, enc.data(), n_work * 4, hipMemcpyHostToDevice, st));
         DAG_HIP(hipMemcpyAsync(d_work, work.data(), n_work * 4, hipMemcpyHostToDevice, st));
-        DAG_HIP(hipMemsetAsync(S.next, 0, 64, st));
+        DAG_HIP(hipMemsetAsync(S.next, 0, 256 + 128 * kCounters, st));
         DAG_HIP(hipMemcpyAsync(S.next, &one, 4, hipMemcpyHostToDevice, st));
         DAG_HIP(hipMemsetAsync(S.table, 0, (size_t)tsize * 4, st));
         DAG_HIP(hipMemsetAsync(S.leaf_id, 0, (size_t)4 << 24, st));
@@ -763,16 +776,21 @@ int build_dag_gpu(const Terrain &tr, uint32_t cap, const std::vector<uint32_t> &
             cur ^= 1;
         }
         uint32_t head[4] = {0, 0, 0, 0};
+        std::vector<unsigned long long> counts((size_t)16 * kCounters);
         DAG_HIP(hipMemcpyAsync(head, S.next, 16, hipMemcpyDeviceToHost, st));
+        DAG_HIP(hipMemcpyAsync(counts.data(), S.tree_nodes, counts.size() * 8, hipMemcpyDeviceToHost, st));
         DAG_HIP(hipMemcpyAsync(&root, d_grid[cur], 4, hipMemcpyDeviceToHost, st));
         std::vector<uint32_t> info(n_work * 8);
         DAG_HIP(hipMemcpyAsync(info.data(), d_info, n_work * 32, hipMemcpyDeviceToHost, st));
         DAG_HIP(hipStreamSynchronize(st));
         if (head[1]) return OCH_E_CAPACITY;
         used = std::min(head[0], cap);
-        total.tree_nodes = (uint64_t)head[2] | (uint64_t)head[3] << 32;
-        for (size_t i = 0; i < n_work; ++i)
+        total.tree_nodes = 0;
+        for (int k = 0; k < kCounters; ++k) total.tree_nodes += counts[(size_t)16 * k];
+        for (size_t i = 0; i < n_work; ++i) {
             for (int v = 0; v < 6; ++v) total.hist[v] += info[i * 8 + 1 + v];
+            total.tree_nodes += info[i * 8 + 7];
+        }
         nodes.resize((size_t)used * 8);
         level.resize(used);
         DAG_HIP(hipMemcpyAsync(nodes.data(), S.nodes, (size_t)used * 32, hipMemcpyDeviceToHost, st));
