@@ -38,6 +38,8 @@
 #include <unordered_map>
 #include <vector>
 
+#include <hipcub/hipcub.hpp>
+
 #include "och_internal.h"
 #include "och_terrain.h"
 
@@ -685,12 +687,61 @@ __global__ __launch_bounds__(256) void k_settle(GpuStore S, uint32_t count, cons
     if (s != kNoSlot) S.table[s] = r;
 }
 
+// Breadth-first renumbering on the device, one BFS level at a time (ids of
+// one height are reachable at one depth only: the height is part of every
+// node's key).  The frontier is order[off, off + f), in BFS order; its
+// children, in (parent, slot) order, are the candidates q = 8 i + k, and a
+// child's first candidate (k_bfs_first, atomicMin) places it (k_bfs_place,
+// after an exclusive scan of k_bfs_mark's flags) -- the host renumbering's
+// first-occurrence order.
+__global__ __launch_bounds__(256) void k_bfs_first(const uint32_t *__restrict__ store, const uint32_t *__restrict__ front,
+                                                   uint32_t f, uint32_t *__restrict__ first)
+{
+    const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= 8u * f) return;
+    const uint32_t c = store[(size_t)front[q >> 3] * 8 + (q & 7u)];
+    if (c) atomicMin(&first[c], q);
+}
+
+__global__ __launch_bounds__(256) void k_bfs_mark(const uint32_t *__restrict__ store, const uint32_t *__restrict__ front,
+                                                  uint32_t f, const uint32_t *__restrict__ first, uint32_t *__restrict__ mark)
+{
+    const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= 8u * f) return;
+    const uint32_t c = store[(size_t)front[q >> 3] * 8 + (q & 7u)];
+    mark[q] = (c && first[c] == q) ? 1u : 0u;
+}
+
+// order[next + pos[q]] = child, newid[child] = base + next + pos[q]
+__global__ __launch_bounds__(256) void k_bfs_place(const uint32_t *__restrict__ store, const uint32_t *__restrict__ front,
+                                                   uint32_t f, const uint32_t *__restrict__ mark,
+                                                   const uint32_t *__restrict__ pos, uint32_t *__restrict__ order,
+                                                   uint32_t next, uint32_t *__restrict__ newid, uint32_t base)
+{
+    const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= 8u * f || !mark[q]) return;
+    const uint32_t c = store[(size_t)front[q >> 3] * 8 + (q & 7u)];
+    order[next + pos[q]] = c;
+    newid[c] = base + next + pos[q];
+}
+
+__global__ __launch_bounds__(256) void k_bfs_output(const uint32_t *__restrict__ store, const uint8_t *__restrict__ level,
+                                                    const uint32_t *__restrict__ order, const uint32_t *__restrict__ newid,
+                                                    uint32_t n, uint32_t *__restrict__ out)
+{
+    const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= 8u * n) return;
+    const uint32_t v = order[q >> 3];
+    const uint32_t c = store[(size_t)v * 8 + (q & 7u)];
+    out[q] = (level[v] == 0 || !c) ? c : newid[c];
+}
+
 // The whole DAG on the current GPU: bricks voxelised (k_brick_codes) and
-// interned batch by batch, then the levels above the bricks.  On return the
-// store's records are on the host: nodes (used x 8), level (used); ids 1 ..
-// used - 1, `root` its root id.  Returns a status.
-int build_dag_gpu(const Terrain &tr, uint32_t cap, const std::vector<uint32_t> &work, int G, std::vector<uint32_t> &nodes,
-                  std::vector<uint8_t> &level, uint32_t &used, uint32_t &root, BrickStats &total, bool trace)
+// interned batch by batch, then the levels above the bricks, then renumbered
+// breadth-first (1-based).  *out: malloc'd n_out x 8 words, as renumber().
+// Returns a status.
+int build_dag_gpu(const Terrain &tr, uint32_t cap, const std::vector<uint32_t> &work, int G, uint32_t **out,
+                  uint32_t *n_out, uint32_t &root, BrickStats &total, bool trace)
 {
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return OCH_E_NODEV;
@@ -784,18 +835,66 @@ int build_dag_gpu(const Terrain &tr, uint32_t cap, const std::vector<uint32_t> &
         DAG_HIP(hipMemcpyAsync(info.data(), d_info, n_work * 32, hipMemcpyDeviceToHost, st));
         DAG_HIP(hipStreamSynchronize(st));
         if (head[1]) return OCH_E_CAPACITY;
-        used = std::min(head[0], cap);
+        const uint32_t used = std::min(head[0], cap);
         total.tree_nodes = 0;
         for (int k = 0; k < kCounters; ++k) total.tree_nodes += counts[(size_t)16 * k];
         for (size_t i = 0; i < n_work; ++i) {
             for (int v = 0; v < 6; ++v) total.hist[v] += info[i * 8 + 1 + v];
             total.tree_nodes += info[i * 8 + 7];
         }
-        nodes.resize((size_t)used * 8);
-        level.resize(used);
-        DAG_HIP(hipMemcpyAsync(nodes.data(), S.nodes, (size_t)used * 32, hipMemcpyDeviceToHost, st));
-        DAG_HIP(hipMemcpyAsync(level.data(), S.level, used, hipMemcpyDeviceToHost, st));
-        DAG_HIP(hipStreamSynchronize(st));
+        const auto t_bfs = std::chrono::steady_clock::now();
+        if (!root) {   // empty world: one zero node
+            *n_out = 1;
+            *out = static_cast<uint32_t *>(std::calloc(8, 4));
+            return *out ? OCH_OK : OCH_E_NOMEM;
+        }
+        // renumbering: first / newid / order over the ids, mark / pos over one level's candidates
+        uint32_t *d_first, *d_newid, *d_order, *d_mark, *d_pos, *d_out;
+        const size_t max_cand = (size_t)used * 8;
+        if (!dalloc((void **)&d_first, (size_t)used * 4) || !dalloc((void **)&d_newid, (size_t)used * 4) ||
+            !dalloc((void **)&d_order, (size_t)used * 4) || !dalloc((void **)&d_mark, max_cand * 4) ||
+            !dalloc((void **)&d_pos, max_cand * 4) || !dalloc((void **)&d_out, max_cand * 4))
+            return OCH_E_NOMEM;
+        size_t scan_bytes = 0;
+        DAG_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, scan_bytes, d_mark, d_pos, (int)max_cand, st));
+        void *d_scan = nullptr;
+        if (!dalloc(&d_scan, std::max<size_t>(scan_bytes, 4))) return OCH_E_NOMEM;
+        const uint32_t base = 1;
+        DAG_HIP(hipMemsetAsync(d_first, 0xFF, (size_t)used * 4, st));
+        DAG_HIP(hipMemcpyAsync(d_order, &root, 4, hipMemcpyHostToDevice, st));
+        DAG_HIP(hipMemcpyAsync(d_newid + root, &base, 4, hipMemcpyHostToDevice, st));
+        uint32_t off = 0, f = 1;
+        for (int l = 1; l < tr.depth && f; ++l) {
+            const uint32_t nc = 8 * f, next = off + f;
+            hipLaunchKernelGGL(k_bfs_first, blocks(nc), dim3(256), 0, st, S.nodes, d_order + off, f, d_first);
+            hipLaunchKernelGGL(k_bfs_mark, blocks(nc), dim3(256), 0, st, S.nodes, d_order + off, f, d_first, d_mark);
+            DAG_HIP(hipGetLastError());
+            DAG_HIP(hipcub::DeviceScan::ExclusiveSum(d_scan, scan_bytes, d_mark, d_pos, (int)nc, st));
+            hipLaunchKernelGGL(k_bfs_place, blocks(nc), dim3(256), 0, st, S.nodes, d_order + off, f, d_mark, d_pos, d_order,
+                               next, d_newid, base);
+            DAG_HIP(hipGetLastError());
+            uint32_t tail[2];
+            DAG_HIP(hipMemcpyAsync(&tail[0], d_pos + nc - 1, 4, hipMemcpyDeviceToHost, st));
+            DAG_HIP(hipMemcpyAsync(&tail[1], d_mark + nc - 1, 4, hipMemcpyDeviceToHost, st));
+            DAG_HIP(hipStreamSynchronize(st));
+            off = next;
+            f = tail[0] + tail[1];
+        }
+        const uint32_t n = off + f;
+        hipLaunchKernelGGL(k_bfs_output, blocks((size_t)n * 8), dim3(256), 0, st, S.nodes, S.level, d_order, d_newid, n, d_out);
+        DAG_HIP(hipGetLastError());
+        uint32_t *nodes = static_cast<uint32_t *>(std::malloc((size_t)n * 32));
+        if (!nodes) return OCH_E_NOMEM;
+        if (hipMemcpyAsync(nodes, d_out, (size_t)n * 32, hipMemcpyDeviceToHost, st) != hipSuccess ||
+            hipStreamSynchronize(st) != hipSuccess) {
+            std::free(nodes);
+            return OCH_E_HIP;
+        }
+        *out = nodes;
+        *n_out = n;
+        if (trace)
+            std::fprintf(stderr, "[och_build] gpu renumbering %.3f s\n",
+                         std::chrono::duration<double>(std::chrono::steady_clock::now() - t_bfs).count());
 #undef DAG_HIP
         if (trace) std::fprintf(stderr, "[och_build] gpu dag: %zu bricks, %u ids\n", n_work, used);
         return OCH_OK;
@@ -929,19 +1028,14 @@ OCH_API int och_build_terrain(const och_terrain_params *params, och_host_pool *o
     uint32_t root = 0, n_out = 0;
     uint32_t *nodes = nullptr;
     if (params->use_gpu && params->dedup && s_log2 == kBrickLog2) {
-        // the whole DAG on the GPU; the host renumbers
-        std::vector<uint32_t> store;
-        std::vector<uint8_t> lvl;
-        uint32_t used = 0;
-        const int st = build_dag_gpu(tr, cap, work, G, store, lvl, used, root, total, trace);
+        // the whole DAG on the GPU, renumbering included
+        const int st = build_dag_gpu(tr, cap, work, G, &nodes, &n_out, root, total, trace);
         if (st != OCH_OK)
             return och::report(st, st == OCH_E_NODEV    ? "use_gpu: no HIP device"
                                    : st == OCH_E_CAPACITY ? "GPU builder: node capacity exhausted"
                                    : st == OCH_E_NOMEM    ? "GPU builder: device allocation failed"
                                                           : "GPU builder: HIP error");
         phase("gpu dag");
-        const int rs = renumber(store.data(), lvl.data(), used, root, depth, base, &nodes, &n_out);
-        if (rs != OCH_OK) return rs;
     } else {
         NodeStore ns;
         if (!ns.init(cap, params->dedup != 0)) {
