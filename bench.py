@@ -114,7 +114,7 @@ def build_pool_nodes(depth: int, rank: int, world: int, dev):
             nodes, build_s = z["nodes"], float(z["build_s"])
             meta[:] = torch.tensor([nodes.shape[0], int(z["root"]), int(z["tree_nodes"])])
         else:
-            # voxelised on the GPU (k_brick_codes), hash-consed on the host
+            # voxelised (k_brick_codes), hash-consed (k_intern) and renumbered on the GPU
             tree = ort.build_terrain(depth, use_gpu=True)
             nodes, build_s = tree.nodes, tree.build_seconds
             meta[:] = torch.tensor([tree.n_nodes, tree.root, tree.tree_nodes])
@@ -587,13 +587,13 @@ def main():
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic: the reference's terrain fill (simplex heightmap + tunnels) at depth 12, voxelised on the "
-                    "GPU and hash-consed on the host (och_build_terrain)",
+                    "GPU, hash-consed and renumbered on the GPU (och_build_terrain)",
             "config": {"workload": workload,
                        "depth": a.depth, "width": W, "height": H, "frames_per_step": len(cams),
                        "pitches": list(PITCHES), "yaw": YAW, "fov": FOV, "row_chunk": a.row_chunk,
                        "dag_nodes": int(nodes.shape[0]), "tree_nodes": tree_nodes,
                        "pool_mb": round(nodes.nbytes / 2**20, 1), "build_s": round(build_s, 2),
-                       "build": "och_build_terrain, use_gpu=1: 32^3 bricks voxelised on the GPU, hash-consed on the host",
+                       "build": "och_build_terrain, use_gpu=1: 32^3 bricks voxelised, hash-consed and renumbered on the GPU",
                        "parallelism": f"rows{world}",
                        "frames": "indexed-colour codes, shaded after the exchange" if indexed else "rgba8",
                        "options": {k: pool.get_option(k) for k in pool.OPTIONS}},

@@ -219,6 +219,80 @@ struct och_editor {
         dirty.clear();
     }
 
+    // Adoption of a pool that is already a canonical DAG -- every reachable node
+    // at one level only, no two equal (content, level), none empty -- such as
+    // och_build_terrain's: the result of adopt() + renumber_breadth_first() is
+    // then the input renumbered breadth-first, built here in O(n) without the
+    // recursive walk.  False (editor untouched) when the input is not canonical
+    // or does not fit; the caller then takes the general path.
+    bool adopt_canonical(const uint32_t *in, uint32_t n_in, uint32_t in_root)
+    {
+        if (in_root == 0 || in_root > n_in) return false;
+        std::vector<uint32_t> to((size_t)n_in + 1, 0), order{in_root};
+        std::vector<uint8_t> lv((size_t)n_in + 1, 0);
+        to[in_root] = 1;
+        lv[in_root] = (uint8_t)(depth - 1);
+        for (size_t q = 0; q < order.size(); ++q) {
+            const uint32_t v = order[q];
+            const int l = lv[v];
+            const uint32_t *c = in + (size_t)(v - 1) * 8;
+            bool zero = true;
+            for (int k = 0; k < 8; ++k) zero &= c[k] == 0;
+            if (zero) return false;
+            if (l == 0) continue;
+            for (int k = 0; k < 8; ++k) {
+                const uint32_t ch = c[k];
+                if (!ch) continue;
+                if (ch > n_in) return false;
+                if (to[ch]) {
+                    if (lv[ch] != l - 1) return false;   // one slot at two levels
+                    continue;
+                }
+                if (order.size() >= capacity) return false;
+                to[ch] = (uint32_t)order.size() + 1;
+                lv[ch] = (uint8_t)(l - 1);
+                order.push_back(ch);
+            }
+        }
+        const uint32_t n = (uint32_t)order.size();
+        for (uint32_t q = 0; q < n; ++q) {
+            const uint32_t v = order[q], d = q + 1;
+            const uint32_t *c = in + (size_t)(v - 1) * 8;
+            uint32_t *o = slot(d);
+            for (int k = 0; k < 8; ++k) o[k] = lv[v] > 0 && c[k] ? to[c[k]] : c[k];
+            level[d] = lv[v];
+        }
+        // the index, and the uniqueness check: an equal node already indexed
+        // means the input is not canonical
+        for (uint32_t d = 1; d <= n; ++d) {
+            size_t ins;
+            if (lookup(slot(d), level[d], &ins)) {
+                std::fill(table.begin(), table.end(), 0u);
+                std::fill(nodes.begin(), nodes.begin() + (size_t)n * 8, 0u);
+                std::fill(level.begin(), level.begin() + n + 1, 0);
+                return false;
+            }
+            table[ins] = d;
+        }
+        table_used = n;
+        for (uint32_t d = 1; d <= n; ++d)
+            if (level[d] > 0)
+                for (int k = 0; k < 8; ++k)
+                    if (slot(d)[k]) ++refs[slot(d)[k]];
+        root = 1;
+        ++refs[1];
+        next_unused = n + 1;
+        live = n;
+        if (packed_ok)
+            for (uint32_t d = 1; d <= n; ++d)
+                for (int c = 0; c < 8; ++c) {
+                    const uint32_t ch = slot(d)[c];
+                    packed[(size_t)d * 8 + c] = level[d] > 0 && ch ? ch | mask_of(ch) << 24 : ch;
+                }
+        dirty.clear();
+        return true;
+    }
+
     // Copy an input pool in, level by level; memo maps (input id, level) to slots.
     int adopt(const uint32_t *in, uint32_t n_in, uint32_t id, int lvl,
               std::unordered_map<uint64_t, uint32_t> &memo, uint32_t *out)
@@ -275,7 +349,7 @@ OCH_API int och_editor_create(const uint32_t *nodes, uint32_t n_nodes, uint32_t 
         delete e;
         return och::report(OCH_E_NOMEM, "och_editor_create: out of host memory");
     }
-    if (root) {
+    if (root && !e->adopt_canonical(nodes, n_nodes, root)) {
         std::unordered_map<uint64_t, uint32_t> memo;
         const int st = e->adopt(nodes, n_nodes, root, depth - 1, memo, &e->root);
         if (st != OCH_OK) {

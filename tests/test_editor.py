@@ -121,6 +121,60 @@ def test_adopts_builder_pool(ort, O):
     assert np.array_equal(ed.nodes()[:tree.nodes.shape[0]], tree.nodes)
 
 
+def _levels(nodes, root, depth):
+    """Height above the voxels of every node reachable from root (1-based ids)."""
+    lvl, order = {root: depth - 1}, [root]
+    for v in order:
+        if lvl[v]:
+            for c in nodes[v - 1].tolist():
+                if c and c not in lvl:
+                    lvl[c] = lvl[v] - 1
+                    order.append(c)
+    return lvl
+
+
+def test_canonical_adoption_matches_general_path(ort):
+    """och_editor_create adopts a canonical DAG (a builder pool) in O(n),
+    renumbering it breadth-first when it is numbered otherwise (here: ids
+    reversed).  A pool holding a reachable duplicate node is not canonical and
+    takes the general recursive adoption, which merges the duplicate.  All give
+    the same slots, refcounts (the same slots again after the same edits) and
+    statistics."""
+    depth = 6
+    tree = ort.build_terrain(depth)
+    nodes, n = tree.nodes, tree.nodes.shape[0]
+    lvl = _levels(nodes, tree.root, depth)
+    # a node referenced from two slots; one reference is redirected to a copy
+    seen, shared = {}, None
+    for pid, h in lvl.items():
+        if h:
+            for k, c in enumerate(nodes[pid - 1].tolist()):
+                if c and c in seen and shared is None:
+                    shared = (c, pid, k)
+                seen.setdefault(c, (pid, k))
+    assert shared is not None
+    c, pid, k = shared
+    dup = np.vstack([nodes, nodes[c - 1][None, :]])
+    dup[pid - 1, k] = n + 1
+    # the same DAG with ids reversed (old id i -> n + 1 - i)
+    rev = np.zeros_like(nodes)
+    for i in range(1, n + 1):
+        rev[n - i] = [n + 1 - c if (c and lvl.get(i, 0) > 0) else c for c in nodes[i - 1].tolist()]
+
+    eds = [ort.Editor(nodes, tree.root, depth, capacity=1 << 16),
+           ort.Editor(dup, tree.root, depth, capacity=1 << 16),
+           ort.Editor(rev, n + 1 - tree.root, depth, capacity=1 << 16)]
+    for e in eds[1:]:
+        assert e.root == eds[0].root and e.stats() == eds[0].stats()
+        assert np.array_equal(e.nodes(), eds[0].nodes())
+    for x, y, z, v in _edits(5, 600, 0, 64):
+        for e in eds:
+            e.set(x, y, z, v)
+    for e in eds[1:]:
+        assert e.stats() == eds[0].stats()
+        assert np.array_equal(e.nodes(), eds[0].nodes())
+
+
 @pytest.mark.gpu
 def test_gpu_mirror_after_flushes(ort, O, gpu_device):
     """Edits flushed to the device pool in small windows trace bit-identically
