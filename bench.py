@@ -586,8 +586,8 @@ def main():
             "scaling": "weak" if (world > 1 and a.scaling == "weak") else "strong",
             "vs_baseline": None,
             "dtype": "f32",
-            "data": "synthetic: the reference's terrain fill (simplex heightmap + tunnels) at depth 12, voxelised on the "
-                    "GPU, hash-consed and renumbered on the GPU (och_build_terrain)",
+            "data": "synthetic: the reference's terrain fill (simplex heightmap + tunnels) at depth 12, voxelised, "
+                    "hash-consed and renumbered on the GPU (och_build_terrain)",
             "config": {"workload": workload,
                        "depth": a.depth, "width": W, "height": H, "frames_per_step": len(cams),
                        "pitches": list(PITCHES), "yaw": YAW, "fov": FOV, "row_chunk": a.row_chunk,
