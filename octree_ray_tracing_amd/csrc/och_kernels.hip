@@ -439,23 +439,43 @@ constexpr uint32_t kTileW = OCH_TILE_W, kTileH = 64 / OCH_TILE_W;
 // row-major (order 0) or in 64x64-pixel supertiles of 8x8 tiles (order 1),
 // which the grid kernel hands to one XCD as a unit (see xcd_block).  The
 // output token is view * slice_pixels + slice pixel.
+// Division by a launch constant: n / d = (mulhi(n, m) + n) >> s for every
+// 32-bit n, with m, s from the host (round-up multiplier; checked against
+// plain division over all 32-bit edge cases).  A wave-uniform n stays on the
+// scalar unit; the integer-division expansion it replaces is ~10 VALU each.
+struct FastDiv {
+    uint32_t d, m, s;
+    __host__ void init(uint32_t divisor)
+    {
+        d = divisor;
+        s = 0;
+        while ((1ull << s) < divisor) ++s;
+        m = (uint32_t)((((1ull << s) - divisor) << 32) / divisor + 1);
+    }
+    __device__ __forceinline__ uint32_t div(uint32_t n) const
+    {
+        return (uint32_t)(((uint64_t)__umulhi(n, m) + n) >> s);
+    }
+};
+
 struct CameraSource {
     och_camera cam[kMaxViews];
     int32_t n_views, row_chunk, shard, n_shards, slice_rows, width, height, order;
     uint32_t tiles_x, supertiles_x, per_view, slice_pixels;
+    FastDiv by_per_view, by_tiles_x, by_supertiles_x, by_row_chunk;
     __host__ __device__ __forceinline__ uint32_t count() const { return per_view * (uint32_t)n_views; }
     // Tile of ray i (tile-granular index math, identical in get and get_wave).
     __device__ __forceinline__ void tile_of(uint32_t i, uint32_t &view, uint32_t &tx, uint32_t &ty) const
     {
-        view = i / per_view;
+        view = by_per_view.div(i);
         const uint32_t tile = (i - view * per_view) >> 6;
         if (order == 1) {
-            const uint32_t st = tile >> 6, sub = tile & 63u;
-            tx = (st % supertiles_x) * 8u + (sub & 7u);
-            ty = (st / supertiles_x) * 8u + (sub >> 3);
+            const uint32_t st = tile >> 6, sub = tile & 63u, sy = by_supertiles_x.div(st);
+            tx = (st - sy * supertiles_x) * 8u + (sub & 7u);
+            ty = sy * 8u + (sub >> 3);
         } else {
-            tx = tile % tiles_x;
-            ty = tile / tiles_x;
+            ty = by_tiles_x.div(tile);
+            tx = tile - ty * tiles_x;
         }
     }
     __device__ __forceinline__ bool finish(uint32_t view, int col, int srow, int row, float *o, float *d,
@@ -477,7 +497,7 @@ struct CameraSource {
         const int col = (int)(tx * kTileW + lane % kTileW);
         const int srow = (int)(ty * kTileH + lane / kTileW);
         if (col >= width || srow >= slice_rows) return false;
-        const int chunk = srow / row_chunk, within = srow - chunk * row_chunk;
+        const int chunk = (int)by_row_chunk.div((uint32_t)srow), within = srow - chunk * row_chunk;
         return finish(view, col, srow, (chunk * n_shards + shard) * row_chunk + within, o, d, out);
     }
     // One wave's tile: wave_base (a multiple of 64, wave-uniform) moves the
@@ -494,10 +514,10 @@ struct CameraSource {
         if (col >= width || srow >= slice_rows) return false;
         int row;
         if (row_chunk % (int)kTileH == 0) {                // the tile lies inside one row chunk
-            const int chunk = __builtin_amdgcn_readfirstlane(srow0 / row_chunk);
+            const int chunk = __builtin_amdgcn_readfirstlane((int)by_row_chunk.div((uint32_t)srow0));
             row = (chunk * n_shards + shard) * row_chunk + (srow - chunk * row_chunk);
         } else {
-            const int chunk = srow / row_chunk;
+            const int chunk = (int)by_row_chunk.div((uint32_t)srow);
             row = (chunk * n_shards + shard) * row_chunk + (srow - chunk * row_chunk);
         }
         return finish(view, col, srow, row, o, d, out);
@@ -527,12 +547,12 @@ struct CameraSource {
         if (col >= width || srow >= slice_rows) return false;
         int row;
         if (row_chunk % (int)kTileH == 0) {                    // each tile lies inside one row chunk
-            const int ca = __builtin_amdgcn_readfirstlane((int)(tya * kTileH) / row_chunk);
-            const int cb = __builtin_amdgcn_readfirstlane((int)(tyb * kTileH) / row_chunk);
+            const int ca = __builtin_amdgcn_readfirstlane((int)by_row_chunk.div(tya * kTileH));
+            const int cb = __builtin_amdgcn_readfirstlane((int)by_row_chunk.div(tyb * kTileH));
             const int chunk = in_a ? ca : cb;
             row = (chunk * n_shards + shard) * row_chunk + (srow - chunk * row_chunk);
         } else {
-            const int chunk = srow / row_chunk;
+            const int chunk = (int)by_row_chunk.div((uint32_t)srow);
             row = (chunk * n_shards + shard) * row_chunk + (srow - chunk * row_chunk);
         }
         return finish(view, col, srow, row, o, d, out);
@@ -1094,6 +1114,10 @@ CameraSource camera_source(const DevFrame &f, const Schedule &sc)
         src.per_view = (src.per_view + chunk - 1) / chunk * chunk;
     }
     src.slice_pixels = (uint32_t)f.slice_rows * (uint32_t)src.width;
+    src.by_per_view.init(src.per_view);
+    src.by_tiles_x.init(src.tiles_x);
+    src.by_supertiles_x.init(src.supertiles_x);
+    src.by_row_chunk.init((uint32_t)src.row_chunk);
     return src;
 }
 
