@@ -29,6 +29,10 @@ def main():
     ap.add_argument("--repeat", type=int, default=5)
     ap.add_argument("--prio", action="append", default=[],
                     help="per-stream priorities for one arm, e.g. -1,0,0 (torch/HIP: lower = higher priority)")
+    ap.add_argument("--split-post", action="store_true",
+                    help="also time the split arm: renders over 3 streams, every exchange + shade on one "
+                         "post stream, 6 frame buffer sets (a render waits only for the shade that last "
+                         "read its buffers)")
     ap.add_argument("--cache", default="/tmp/och_terrain_cache.npz")
     ap.add_argument("--out", default="gpurun_out/window.json")
     a = ap.parse_args()
@@ -59,31 +63,53 @@ def main():
     print("stream priority range", torch.cuda.Stream.priority_range(), flush=True)
     arms = [(n, None) for n in (a.inflight or [3])] + [(len(p.split(",")), [int(x) for x in p.split(",")])
                                                        for p in a.prio]
+    if a.split_post:
+        arms.append((3, "split"))
     results = []
     for inflight, prio in arms:
-        if prio is None:
+        split = prio == "split"
+        if prio is None or split:
             streams = [stream] + [torch.cuda.Stream() for _ in range(inflight - 1)]
         else:
             streams = [torch.cuda.Stream(priority=q) for q in prio]
+        post = torch.cuda.Stream() if split else None
+        n_sets = 2 * inflight if split else inflight
         sfs = []
-        for s_ in streams:
-            with torch.cuda.stream(s_):
+        for i in range(n_sets):
+            with torch.cuda.stream(streams[i % inflight]):
                 sfs.append(ShardedFrame(pool, W, H, 8, n_views=2, indexed=True))
         pool.set_stream(stream)
+        freed = [None] * n_sets      # split: event after the shade that last read set i
 
         def step(k, marks=None):
-            s_, f_ = streams[k % inflight], sfs[k % inflight]
+            s_, f_ = streams[k % inflight], sfs[k % n_sets]
             pool.set_stream(s_)
             with torch.cuda.stream(s_):
                 if marks is not None:
                     e = [ev(), ev(), ev()]
                     e[0].record(s_)
+                if split and freed[k % n_sets] is not None:
+                    s_.wait_event(freed[k % n_sets])
                 f_.render_local(cams)
                 if marks is not None:
                     e[1].record(s_)
+                if not split:
+                    f_.exchange()
+                    if marks is not None:
+                        e[2].record(s_)
+                        marks.append(e)
+                    return
+                done = ev()
+                done.record(s_)
+            pool.set_stream(post)
+            with torch.cuda.stream(post):
+                post.wait_event(done)
                 f_.exchange()
+                fe = ev()
+                fe.record(post)
+                freed[k % n_sets] = fe
                 if marks is not None:
-                    e[2].record(s_)
+                    e[2] = fe
                     marks.append(e)
 
         for k in range(6):
