@@ -2,6 +2,7 @@ import subprocess
 import sys
 from pathlib import Path
 
+import numpy as np
 import pytest
 
 ROOT = Path(__file__).resolve().parents[1]
@@ -58,3 +59,29 @@ def gpu_device():
         pytest.fail("gpu test selected but no GPU visible")
     torch.cuda.set_device(0)
     return 0
+
+
+def sparse_dag(depth, voxels):
+    """A 1-based, hash-consed h_octree pool holding `voxels` (x, y, z, id > 0);
+    child index x | y << 1 | z << 2 (ORT/och_h_octree.h:38-66).  The
+    reference's own set() packs coordinates with z_encode_16 and stops at
+    depth 16, so deeper test trees are assembled here."""
+    table, nodes = {}, []
+
+    def intern(children, lvl):
+        key = (lvl, tuple(children))
+        if key not in table:
+            nodes.append(children)
+            table[key] = len(nodes)
+        return table[key]
+
+    cells = {}
+    for x, y, z, v in voxels:
+        cells.setdefault((x >> 1, y >> 1, z >> 1), [0] * 8)[(x & 1) | (y & 1) << 1 | (z & 1) << 2] = v
+    ids = {k: intern(c, 0) for k, c in cells.items()}
+    for lvl in range(1, depth):
+        up = {}
+        for (x, y, z), i in ids.items():
+            up.setdefault((x >> 1, y >> 1, z >> 1), [0] * 8)[(x & 1) | (y & 1) << 1 | (z & 1) << 2] = i
+        ids = {k: intern(c, lvl) for k, c in up.items()}
+    return np.array(nodes, np.uint32), ids[(0, 0, 0)]

@@ -9,7 +9,7 @@ import math
 import numpy as np
 import pytest
 
-from conftest import GOLD
+from conftest import GOLD, sparse_dag
 
 pytestmark = pytest.mark.gpu
 
@@ -117,6 +117,42 @@ def test_reference_hash_table_layout(ort, O, gpu_device):
         assert_same(gpu_trace_dev(pool, o, d), ref)
     rays = O.raygen(0.3, -0.6, 1.25, 640, 360)
     assert_same(gpu_trace_dev(pool, ORIGIN, rays), O.trace_batch(T.pool(), O.Rcp(None), ORIGIN, rays, want_push=True))
+    pool.close()
+
+
+@pytest.mark.parametrize("depth", [16, 20, 22])
+def test_deep_sparse_trees(ort, O, gpu_device, depth):
+    """Depths beyond the terrain's, up to the ABI's 22: a sparse DAG of voxel
+    clusters at every scale around the cube's centre, traced from the centre
+    and from random origins, most rays aimed at voxel centres and corners.
+    Exercises deep LDS stacks, child sizes down to the float mantissa's last
+    bits and long POP chains; both layouts against the oracle."""
+    rng = np.random.default_rng(depth)
+    c = 1 << (depth - 1)
+    vox = []
+    for k in range(2, depth - 1):                      # clusters 2^k voxels away, k = 2 .. depth - 2
+        base = c + rng.integers(-(1 << k), 1 << k, 3)
+        for off in rng.integers(-2, 3, (40, 3)):
+            x, y, z = (int(v) for v in np.clip(base + off, 0, (1 << depth) - 1))
+            vox.append((x, y, z, int(1 + (x + y + z) % 4)))
+    nodes, root = sparse_dag(depth, vox)
+    ref_pool = O.OraclePool(nodes, root, depth, 1)
+    n = 20000
+    o = np.tile(ORIGIN.astype(np.float64), (n, 1))
+    o[n // 2:] = rng.uniform(1.25, 1.75, (n - n // 2, 3))
+    tgt = np.array([v[:3] for v in vox], np.float64)[rng.integers(0, len(vox), n)]
+    tgt += np.where(rng.random((n, 1)) < 0.5, 0.5, rng.integers(0, 2, (n, 3)))   # voxel centres or corners
+    d = (1.0 + tgt / (1 << depth)) - o
+    d[::4] = rng.uniform(-1, 1, (d[::4].shape[0], 3))                            # and some random rays
+    norm = np.linalg.norm(d, axis=1, keepdims=True)
+    d = np.where(norm > 0, d / np.where(norm > 0, norm, 1), [[0.6, 0.0, -0.8]]).astype(np.float32)
+    o = o.astype(np.float32)
+    ref = O.trace_batch(ref_pool, O.Rcp(None), o, d, nthreads=16, want_push=True)
+    assert (ref["dir"] < 6).sum() > n // 10, "most aimed rays should hit the clusters"
+    pool = ort.HOctree(nodes, root, depth, device=0)
+    for layout in (0, 1):
+        pool.set_option("layout", layout)
+        assert_same(gpu_trace_dev(pool, o, d), ref)
     pool.close()
 
 

@@ -150,3 +150,38 @@ def test_golden_trace_vectors(O, intel_lut):
         assert np.array_equal(r["voxel"], g[f"{name}_vox"])
         assert np.array_equal(r["t"].view(np.uint32), g[f"{name}_t"])
         assert np.array_equal(r["push"], g[f"{name}_push"])
+
+
+def test_sparse_dag_matches_reference_set(O):
+    """tests/conftest.py's sparse_dag (the deep-tree GPU tests' pool builder)
+    against the reference's own h_octree::set (HRef) at depth 16, the deepest
+    its z_encode_16 coordinates reach: the same records, PUSH counts included."""
+    from conftest import sparse_dag
+    depth = 16
+    rng = np.random.default_rng(16)
+    c = 1 << (depth - 1)
+    vox = []
+    for k in range(2, depth - 1):
+        base = c + rng.integers(-(1 << k), 1 << k, 3)
+        for off in rng.integers(-2, 3, (40, 3)):
+            x, y, z = (int(v) for v in np.clip(base + off, 0, (1 << depth) - 1))
+            vox.append((x, y, z, int(1 + (x + y + z) % 4)))
+    nodes, root = sparse_dag(depth, vox)
+    T = O.HRef(depth, 17)
+    for x, y, z, v in vox:
+        T.set(x, y, z, v)
+    o = np.tile(np.float32(1.5), (4000, 3)).astype(np.float32)
+    d = rng.uniform(-1, 1, (4000, 3))
+    d = (d / np.linalg.norm(d, axis=1, keepdims=True)).astype(np.float32)
+    tgt = np.array([v[:3] for v in vox], np.float64)[rng.integers(0, len(vox), 2000)] + 0.5
+    aimed = (1.0 + tgt / (1 << depth)) - 1.5
+    d[:2000] = (aimed / np.linalg.norm(aimed, axis=1, keepdims=True)).astype(np.float32)
+    a = O.trace_batch(O.OraclePool(nodes, root, depth, 1), O.Rcp(None), o, d, want_push=True)
+    b = O.trace_batch(T.pool(), O.Rcp(None), o, d, want_push=True)
+    assert (a["dir"] < 6).sum() > 500
+    for k in ("dir", "voxel", "push"):
+        assert np.array_equal(a[k], b[k]), k
+    assert np.array_equal(a["t"].view(np.uint32), b["t"].view(np.uint32))
+    final = {(x, y, z): v for x, y, z, v in vox}      # a later set() of a voxel wins
+    for (x, y, z), v in list(final.items())[::7]:
+        assert T.at(x, y, z) == v
