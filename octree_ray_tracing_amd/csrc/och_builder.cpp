@@ -700,7 +700,10 @@ __global__ __launch_bounds__(256) void k_bfs_first(const uint32_t *__restrict__ 
     const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
     if (q >= 8u * f) return;
     const uint32_t c = store[(size_t)front[q >> 3] * 8 + (q & 7u)];
-    if (c) atomicMin(&first[c], q);
+    // first[] only decreases: a cached value at or below q (stale ones are
+    // only larger) makes the atomic unnecessary -- shared children (solid
+    // stone) are named by millions of slots, and one address's atomics serialise
+    if (c && q < first[c]) atomicMin(&first[c], q);
 }
 
 __global__ __launch_bounds__(256) void k_bfs_mark(const uint32_t *__restrict__ store, const uint32_t *__restrict__ front,
