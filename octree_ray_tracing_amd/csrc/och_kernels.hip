@@ -78,8 +78,12 @@ struct Ray {
 };
 
 // Ray phase: due to PUSH (or finished), due to STEP (after a failed PUSH or a
-// POP), or a PUSH found its child and the slot word is in flight.
-constexpr uint32_t kAtPush = 0, kStepping = 1, kPending = 2;
+// POP), or a PUSH found its child and the slot word is in flight.  In the
+// merged loop "due to PUSH" is any of 1, 2, 4 (the advanced axis, see
+// ray_phase_step), so kStepping is 0 and kPending lies outside the axis bits;
+// the encoding saves the phase copies at the loop's joins (2 VALU per
+// iteration, +0.6 % pipelined, profiles/r02/ab/ab_mode.txt).
+constexpr uint32_t kAtPush = 1, kStepping = 0, kPending = 8;
 
 __device__ __forceinline__ void set_mode(Ray &r, uint32_t m) { r.mode = m; }
 
@@ -104,8 +108,8 @@ __device__ __forceinline__ void ray_push(Ray &r, const DevPool &P)
     if (kCount) ++r.push;
     const uint32_t c24 = r.idx ^ r.inv;                                     // 24 + child index
     const uint32_t present = kPacked ? __builtin_amdgcn_ubfe(r.cur, c24, 1u) : 1u;
-    set_mode(r, kStepping + present);                                       // kStepping or kPending
-    asm volatile("" : "+v"(r.mode));                                        // one add, not a move per branch
+    set_mode(r, present * kPending);                                        // kStepping or kPending
+    asm volatile("" : "+v"(r.mode));                                        // one shift, not a move per branch
 #if OCH_PUSH_UNCOND
     // The slot exists whether or not the child does (cur names a pool node),
     // so every PUSH may load it; the word is used only when present.
@@ -214,14 +218,18 @@ __device__ __forceinline__ void ray_phase_step(Ray &r, uint32_t stride)
     const uint32_t axis = sx ? 1u : (sy ? 2u : 4u);
     r.min_axis = axis;
     r.t_min = tm;
-    if (r.idx & axis) {                                                 // advance :413-419
+    const uint32_t adv = r.idx & axis;
+    // merged loop: the phase is the advance test itself -- nonzero (a PUSH is
+    // due) after an advance, kStepping (0) after a POP; no write per branch
+    if (kPacked && OCH_MERGED_DESCEND) r.mode = adv;
+    if (adv) {                                                          // advance :413-419
         // idx bit `axis` set <=> that axis's position has the dim bit set,
         // so clearing it (:415) is a toggle.
         r.p[0] ^= sx ? r.dim : 0u;
         r.p[1] ^= sy ? r.dim : 0u;
         r.p[2] ^= sz ? r.dim : 0u;
         r.idx ^= axis;
-        set_mode(r, kAtPush);
+        if (!(kPacked && OCH_MERGED_DESCEND)) set_mode(r, kAtPush);
         return;
     }
     // POP :421-446.  At the root this is the MISS (:423-431): level 0 ends
@@ -290,7 +298,7 @@ __device__ __forceinline__ void ray_push_descend(Ray &r, const DevPool &P, uint3
     if (kCount) ++r.push;
     const uint32_t c24 = r.idx ^ r.inv;                                     // 24 + child index
     const uint32_t present = __builtin_amdgcn_ubfe(r.cur, c24, 1u);
-    set_mode(r, kStepping + present);                                       // kStepping or kPending
+    set_mode(r, present * kPending);                                        // kStepping or kPending
     asm volatile("" : "+v"(r.mode));
     if (!present) return;
     // 32-bit byte offset from the uniform base: one scaled add, SGPR base address
@@ -334,7 +342,9 @@ __device__ __forceinline__ void ray_iterate(Ray &r, const DevPool &P, uint32_t s
     if (kPacked && OCH_MERGED_DESCEND) {
         if (in_mode(r, kStepping)) ray_phase_step<kPacked>(r, stride);
         // no activity test: a miss leaves the lane kStepping, a HIT ends in this phase
-        if (!in_mode(r, kStepping)) ray_push_descend<kCount>(r, P, stride, top);
+        uint32_t m = r.mode;                  // tested through an opaque copy, so the skipping
+        asm volatile("" : "+v"(m));           // lanes' r.mode is not re-materialised as kStepping
+        if (m != kStepping) ray_push_descend<kCount>(r, P, stride, top);
         return;
     }
     if (!kPacked && in_mode(r, kPending)) ray_phase_descend<kPacked>(r, P, stride);
