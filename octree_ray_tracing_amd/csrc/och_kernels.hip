@@ -242,8 +242,9 @@ __device__ __forceinline__ void ray_phase_step(Ray &r, uint32_t stride)
     for (int a = 0; a < 3; ++a) r.p[a] &= ~r.dim;                       // :436
     r.dim <<= 1;                                                        // :438
     const uint32_t k = __builtin_ctz(r.dim);                            // :440-444, bit k of each position
-    r.idx = (((__builtin_amdgcn_ubfe(r.p[2], k, 1) << 1) | __builtin_amdgcn_ubfe(r.p[1], k, 1)) << 1) |
-            __builtin_amdgcn_ubfe(r.p[0], k, 1);
+    uint32_t zy = (__builtin_amdgcn_ubfe(r.p[2], k, 1) << 1) | __builtin_amdgcn_ubfe(r.p[1], k, 1);
+    asm volatile("" : "+v"(zy));          // two shift-ors, not two shifts and an or3
+    r.idx = (zy << 1) | __builtin_amdgcn_ubfe(r.p[0], k, 1);
 }
 
 template <bool kPacked>
@@ -457,7 +458,8 @@ struct FastDiv {
     uint32_t d, m, s;
     __host__ void init(uint32_t divisor)
     {
-        d = divisor;
+        d = divisor ? divisor : 1u;      // callers validate sizes; never divide by zero here
+        divisor = d;
         s = 0;
         while ((1ull << s) < divisor) ++s;
         m = (uint32_t)((((1ull << s) - divisor) << 32) / divisor + 1);
