@@ -133,6 +133,12 @@ __device__ __forceinline__ void ray_push(Ray &r, const DevPool &P)
 #ifndef OCH_LDS_TOP
 #define OCH_LDS_TOP 0
 #endif
+// OCH_LOAD_INTO_CUR: the merged loop loads a present child's slot word
+// straight into the ray's current-node register (after the parent went to
+// the stack), so the next PUSH needs no "pending" select.
+#ifndef OCH_LOAD_INTO_CUR
+#define OCH_LOAD_INTO_CUR 1
+#endif
 template <bool kCount>
 __device__ __forceinline__ void ray_push_descend(Ray &r, const DevPool &P, uint32_t stride,
                                                  const uint32_t *top = nullptr);
@@ -295,24 +301,28 @@ __device__ __forceinline__ bool ray_active(const Ray &r, const DevPool &P)
 template <bool kCount>
 __device__ __forceinline__ void ray_push_descend(Ray &r, const DevPool &P, uint32_t stride, const uint32_t *top)
 {
-    r.cur = in_mode(r, kPending) ? r.child : r.cur;
+    if (!OCH_LOAD_INTO_CUR) r.cur = in_mode(r, kPending) ? r.child : r.cur;
     if (kCount) ++r.push;
     const uint32_t c24 = r.idx ^ r.inv;                                     // 24 + child index
     const uint32_t present = __builtin_amdgcn_ubfe(r.cur, c24, 1u);
-    set_mode(r, present * kPending);                                        // kStepping or kPending
+    // kStepping (0) or, with the word loaded into cur, any nonzero "PUSH due"
+    set_mode(r, OCH_LOAD_INTO_CUR ? present : present * kPending);
     asm volatile("" : "+v"(r.mode));
     if (!present) return;
     // 32-bit byte offset from the uniform base: one scaled add, SGPR base address
     const uint32_t off = ((r.cur & kIdMask) << 5) + (c24 << 2);
-    if (OCH_LDS_TOP && top && (r.cur & kIdMask) < P.top_ids[OCH_LDS_TOP])
-        r.child = *reinterpret_cast<const uint32_t *>(reinterpret_cast<const char *>(top) - 96 + off);
-    else
-        r.child = *reinterpret_cast<const uint32_t *>(reinterpret_cast<const char *>(P.nodes) - 96 + off);
+    const uint32_t *src = reinterpret_cast<const uint32_t *>(
+        reinterpret_cast<const char *>(OCH_LDS_TOP && top && (r.cur & kIdMask) < P.top_ids[OCH_LDS_TOP] ? top : P.nodes) -
+        96 + off);
     // descent (:357-373); at the leaf level this is the HIT (:346-355): level
     // becomes depth + 1, the stack write lands in the spare top slot
     if (!OCH_DIM_LEVEL) ++r.level;
-    *r.sp = r.cur;
+    *r.sp = r.cur;                          // the parent, before its register takes the child's word
     r.sp += stride;
+    if (OCH_LOAD_INTO_CUR)
+        r.cur = *src;                       // the next PUSH's node, or the voxel id of a HIT
+    else
+        r.child = *src;
     r.dim >>= 1;
     const float tm = ffrom(r.t_min);
     uint32_t nidx = 0;
@@ -354,7 +364,9 @@ __device__ __forceinline__ void ray_iterate(Ray &r, const DevPool &P, uint32_t s
     if (in_mode(r, kAtPush) && ray_active(r, P)) ray_push<kPacked, kCount>(r, P);   // PUSH :342-344
 }
 
-// The hit record of a finished ray (:346-355 hit, :423-431 miss).
+// The hit record of a finished ray (:346-355 hit, :423-431 miss).  The
+// merged loop (OCH_LOAD_INTO_CUR) leaves a HIT's voxel id in cur.
+template <bool kPacked>
 __device__ __forceinline__ Hit ray_result(const Ray &r, const DevPool &P)
 {
     Hit h;
@@ -364,7 +376,7 @@ __device__ __forceinline__ Hit ray_result(const Ray &r, const DevPool &P)
         h.t = P.miss_bits;
     } else {
         h.dir = (int32_t)((r.min_axis >> 1) + 3u * ((r.inv & r.min_axis & 7u) == 0));
-        h.voxel = r.child;
+        h.voxel = (kPacked && OCH_MERGED_DESCEND && OCH_LOAD_INTO_CUR) ? r.cur : r.child;
         h.t = r.t_min;
     }
     h.push = r.push;
@@ -755,7 +767,7 @@ __global__ void k_trace_grid(DevPool P, Src S, Sink K, uint32_t xcd_group, const
         do {
             ray_iterate<kPacked, kCount>(r, P, blockDim.x, top);
         } while (ray_active(r, P));
-        K.put(out, ray_result(r, P));
+        K.put(out, ray_result<kPacked>(r, P));
     }
     if (cost && threadIdx.x == 0) cost[blk] = (uint32_t)(__builtin_amdgcn_s_memtime() - c0);
     if (stamps) stamp(stamps, stamp_cap, t0, 64);
@@ -789,7 +801,7 @@ __global__ void k_trace_bounce(DevPool P, Src S, Sink K, int compact, const uint
         do {
             ray_iterate<kPacked, kCount>(r, P, nb);
         } while (ray_active(r, P));
-        const Hit h1 = ray_result(r, P);
+        const Hit h1 = ray_result<kPacked>(r, P);
         want = h1.dir < OCH_EXIT;
         if (want) bounce_ray(o, d, h1, P.half_voxel, o2, d2);
         payload = K.put_primary(out, h1, want);
@@ -798,7 +810,7 @@ __global__ void k_trace_bounce(DevPool P, Src S, Sink K, int compact, const uint
             do {
                 ray_iterate<kPacked, kCount>(r, P, nb);
             } while (ray_active(r, P));
-            K.put_secondary(out, payload, ray_result(r, P));
+            K.put_secondary(out, payload, ray_result<kPacked>(r, P));
         }
     }
     if (!compact) {
@@ -845,7 +857,7 @@ __global__ void k_trace_bounce(DevPool P, Src S, Sink K, int compact, const uint
         do {
             ray_iterate<kPacked, kCount>(r, P, nb);
         } while (ray_active(r, P));
-        K.put_secondary(sout, spay, ray_result(r, P));
+        K.put_secondary(sout, spay, ray_result<kPacked>(r, P));
     }
     if (cost && threadIdx.x == 0) cost[blk] = (uint32_t)(__builtin_amdgcn_s_memtime() - c0);
     if (stamps) stamp(stamps, stamp_cap, t0, total);
@@ -883,7 +895,7 @@ __global__ void k_trace_refill(DevPool P, Src S, Sink K, uint32_t chunk_rays, in
     for (;;) {
         // Retire: finished lanes write their record.
         if (out != kNoRay && !ray_active(r, P)) {
-            K.put(out, ray_result(r, P));
+            K.put(out, ray_result<kPacked>(r, P));
             out = kNoRay;
             ++finished;
         }
@@ -951,7 +963,7 @@ __global__ void k_trace_persistent(DevPool P, Src S, Sink K, uint32_t *counter, 
         if (active) {
             ray_iterate<kPacked, kCount>(r, P, blockDim.x);
             if (!ray_active(r, P)) {
-                K.put(out, ray_result(r, P));
+                K.put(out, ray_result<kPacked>(r, P));
                 active = false;
                 ++finished;
             }
