@@ -139,6 +139,10 @@ __device__ __forceinline__ void ray_push(Ray &r, const DevPool &P)
 #ifndef OCH_LOAD_INTO_CUR
 #define OCH_LOAD_INTO_CUR 1
 #endif
+// OCH_DUAL: the grid kernel walks two rays per lane (two tiles per wave).
+#ifndef OCH_DUAL
+#define OCH_DUAL 0
+#endif
 template <bool kCount>
 __device__ __forceinline__ void ray_push_descend(Ray &r, const DevPool &P, uint32_t stride,
                                                  const uint32_t *top = nullptr);
@@ -757,8 +761,36 @@ __global__ void k_trace_grid(DevPool P, Src S, Sink K, uint32_t xcd_group, const
         top = t;
     }
     const uint32_t blk = order ? order[blockIdx.x] : xcd_block(blockIdx.x, gridDim.x, xcd_group);
-    const uint32_t wave_base = blk * blockDim.x + (threadIdx.x & ~63u);
     const uint32_t lane = threadIdx.x & 63u;
+#if OCH_DUAL
+    // Two rays per lane (experiment): the wave walks the tiles 2w and 2w + 1
+    // as two independent rays per lane, each with its own LDS stack column,
+    // so one ray's slot load is hidden behind the other's instructions.
+    {
+        const uint32_t wave = blk * (blockDim.x >> 6) + (threadIdx.x >> 6);
+        const uint32_t base_a = wave * 128u, base_b = base_a + 64u;
+        const uint32_t col = (P.depth + 1) * blockDim.x;
+        float oa[3], da[3], ob[3], db[3];
+        uint32_t out_a = 0, out_b = 0;
+        Ray ra, rb;
+        ra.dim = 0;
+        rb.dim = 0;
+        if (base_a + lane < S.count() && S.get_wave(base_a, lane, oa, da, out_a))
+            ray_init<kPacked, kCount>(ra, P, oa, da, lds_stack + threadIdx.x, blockDim.x);
+        if (base_b + lane < S.count() && S.get_wave(base_b, lane, ob, db, out_b))
+            ray_init<kPacked, kCount>(rb, P, ob, db, lds_stack + col + threadIdx.x, blockDim.x);
+        const bool had_a = ra.dim != 0, had_b = rb.dim != 0;
+        for (;;) {
+            const bool ea = ray_active(ra, P), eb = ray_active(rb, P);
+            if (!ea && !eb) break;
+            if (ea) ray_iterate<kPacked, kCount>(ra, P, blockDim.x, top);
+            if (eb) ray_iterate<kPacked, kCount>(rb, P, blockDim.x, top);
+        }
+        if (had_a) K.put(out_a, ray_result<kPacked>(ra, P));
+        if (had_b) K.put(out_b, ray_result<kPacked>(rb, P));
+    }
+#else
+    const uint32_t wave_base = blk * blockDim.x + (threadIdx.x & ~63u);
     float o[3], d[3];
     uint32_t out;
     if (wave_base + lane < S.count() && S.get_wave(wave_base, lane, o, d, out)) {
@@ -769,6 +801,7 @@ __global__ void k_trace_grid(DevPool P, Src S, Sink K, uint32_t xcd_group, const
         } while (ray_active(r, P));
         K.put(out, ray_result<kPacked>(r, P));
     }
+#endif
     if (cost && threadIdx.x == 0) cost[blk] = (uint32_t)(__builtin_amdgcn_s_memtime() - c0);
     if (stamps) stamp(stamps, stamp_cap, t0, 64);
 }
@@ -1084,8 +1117,10 @@ hipError_t launch_as(const DevPool &p, const Src &s, const Sink &k, uint32_t n, 
                            k, sc.counter, sc.refill_min, sc.stamps, sc.stamp_cap);
     } else {
         const uint32_t xcd_group = supertile_rays >= (uint32_t)block ? supertile_rays / (uint32_t)block : 0u;
-        hipLaunchKernelGGL((k_trace_grid<Src, Sink, kPacked, kCount>), dim3((n + block - 1) / block), dim3(block), lds,
-                           stream, p, s, k, xcd_group, sc.order, sc.cost, sc.stamps, sc.stamp_cap);
+        const uint32_t per_block = OCH_DUAL ? 2u * (uint32_t)block : (uint32_t)block;
+        hipLaunchKernelGGL((k_trace_grid<Src, Sink, kPacked, kCount>), dim3((n + per_block - 1) / per_block), dim3(block),
+                           OCH_DUAL ? 2 * lds : lds, stream, p, s, k, xcd_group, sc.order, sc.cost, sc.stamps,
+                           sc.stamp_cap);
     }
     return hipGetLastError();
 }
