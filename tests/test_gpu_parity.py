@@ -216,6 +216,36 @@ def test_raygen_bit_exact(ort, O, gpu_device, W, H, pitch):
     pool.close()
 
 
+def test_edge_sizes(ort, O, gpu_device):
+    """Batches of 0, 1, 63, 64, 65 and 4097 rays (empty, lone, ragged waves and
+    blocks) and frames of 1x1, 7x9, 8x8, 9x7 and 65x3 pixels (partial tiles,
+    single rows), every schedule and both layouts, against the oracle."""
+    tree = ort.build_terrain(8)
+    pal = ort.VoxelData().get_colours()
+    pool = ort.HOctree(tree.nodes, tree.root, 8, device=0)
+    pool.set_palette(pal)
+    ref_pool = O.OraclePool(tree.nodes, tree.root, 8, 1)
+    rng = np.random.default_rng(17)
+    for sched in (0, 1, 2):
+        for layout in (0, 1):
+            pool.set_option("schedule", sched)
+            pool.set_option("layout", layout)
+            for n in (0, 1, 63, 64, 65, 4097):
+                o = rng.uniform(1.05, 1.95, (n, 3)).astype(np.float32)
+                d = rng.uniform(-1, 1, (n, 3))
+                d = (d / np.maximum(np.linalg.norm(d, axis=1, keepdims=True), 1e-6)).astype(np.float32)
+                hd, hv, ht = pool.trace_batch(o, d)
+                assert hd.shape == (n,)
+                if n:
+                    want = O.trace_batch(ref_pool, O.Rcp(None), o, d)
+                    assert_same({"dir": hd, "voxel": hv, "t": ht}, want, push=False)
+            for W, H in ((1, 1), (7, 9), (8, 8), (9, 7), (65, 3)):
+                cam = ort.camera((1.5, 1.5, 1.5), 0.3, -0.6, 1.25, W, H)
+                r = O.trace_batch(ref_pool, O.Rcp(None), ORIGIN, O.raygen(0.3, -0.6, 1.25, W, H))
+                assert np.array_equal(pool.render(cam), O.shade(r["dir"], r["voxel"], pal).reshape(H, W)), (W, H)
+    pool.close()
+
+
 def test_render_frame_and_shards(ort, O, gpu_device):
     import torch
     tree = ort.build_terrain(9)
