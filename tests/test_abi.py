@@ -79,3 +79,49 @@ def test_pool_create_without_gpu_fails_loudly(ort):
 def test_missing_library_raises(ort, tmp_path):
     with pytest.raises(ort.OchError):
         ort._lib.load(tmp_path / "nope.so")
+
+
+def test_header_is_plain_c_and_links(ort, tmp_path):
+    """include/och_gpu.h is what a C FFI (cgo, ctypes, a C host) binds: it
+    compiles as strict C99, and a C program links against liboch_gpu.so and
+    runs the host-only entry points (ABI version, camera setup, pool pack /
+    at on a tiny tree, the error text of a refused call)."""
+    import shutil
+    import subprocess
+    from pathlib import Path
+    gcc = shutil.which("gcc")
+    if gcc is None:
+        pytest.skip("no C compiler")
+    root = Path(ort._lib.HEADER_PATH).resolve().parents[1]
+    libdir = Path(ort.load()._name).resolve().parent
+    src = tmp_path / "abi.c"
+    src.write_text(r'''
+#include <stdio.h>
+#include <string.h>
+#include "och_gpu.h"
+int main(void)
+{
+    och_camera cam;
+    /* one leaf-level node under a root at depth 2: voxel 3 at (0, 0, 0) */
+    const uint32_t nodes[2][8] = {{2, 0, 0, 0, 0, 0, 0, 0}, {3, 0, 0, 0, 0, 0, 0, 0}};
+    uint32_t packed[3 * 8], n_packed = 0, packed_root = 0;
+    och_gpu_pool *pool = NULL;
+    if (och_abi_version() != 1) return 1;
+    if (och_camera_setup(1.5f, 1.5f, 1.5f, 0.3f, -0.6f, 1.25f, 64, 36, &cam) != OCH_OK) return 2;
+    if (och_pool_at(&nodes[0][0], 1, 2, 1, 0, 0, 0) != 3 || och_pool_at(&nodes[0][0], 1, 2, 1, 1, 0, 0) != 0) return 3;
+    if (och_pool_pack(&nodes[0][0], 2, 1, 2, 1, packed, 3, &n_packed, &packed_root) != OCH_OK || n_packed != 3)
+        return 4;
+    /* a refused call reports a status and a message */
+    if (och_gpu_pool_create(&nodes[0][0], 2, 1, 0, 1, 0.0f, -1, &pool) == OCH_OK || pool != NULL) return 5;
+    if (strlen(och_last_error()) == 0) return 6;
+    printf("ok %u %08x\n", n_packed, packed_root);
+    return 0;
+}
+''')
+    exe = tmp_path / "abi"
+    cc = subprocess.run([gcc, "-std=c99", "-Wall", "-Wextra", "-pedantic", "-Werror", f"-I{root / 'include'}",
+                         str(src), f"-L{libdir}", "-loch_gpu", f"-Wl,-rpath,{libdir}", "-o", str(exe)],
+                        capture_output=True, text=True)
+    assert cc.returncode == 0, cc.stderr
+    run = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120)
+    assert run.returncode == 0 and run.stdout.startswith("ok 3 "), (run.returncode, run.stdout, run.stderr)
