@@ -323,6 +323,8 @@ def main():
     ap.add_argument("--no-other-configs", action="store_true", help="skip the configs[0] / configs[1] side measurements")
     ap.add_argument("--rgba-frames", action="store_true",
                     help="render and exchange RGBA8 slices instead of 1-byte indexed-colour codes")
+    ap.add_argument("--fresh-streams", action="store_true",
+                    help="put every frame in flight on a new stream, none on the current stream")
     ap.add_argument("--inflight", type=int, default=3,
                     help="frames in flight: steps alternate over this many HIP streams, so one step's "
                          "slowest rays overlap the next step's bulk (1 = serialised)")
@@ -367,7 +369,10 @@ def main():
     indexed = not a.rgba_frames and ort.VoxelData().get_colours().size // 6 <= pool.CODE_MAX_VOXELS
     cams = [ort.camera(ORIGIN, YAW, p, FOV, W, H) for p in PITCHES]
     # One frame buffer set and one HIP stream per frame in flight.
-    streams = [stream] + [torch.cuda.Stream(device=dev) for _ in range(max(1, a.inflight) - 1)]
+    if a.fresh_streams:      # every frame in flight on a new stream (none on the current one)
+        streams = [torch.cuda.Stream(device=dev) for _ in range(max(1, a.inflight))]
+    else:
+        streams = [stream] + [torch.cuda.Stream(device=dev) for _ in range(max(1, a.inflight) - 1)]
     sfs = []
     for s_ in streams:
         with torch.cuda.stream(s_):

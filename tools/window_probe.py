@@ -33,6 +33,8 @@ def main():
                     help="also time the split arm: renders over 3 streams, every exchange + shade on one "
                          "post stream, 6 frame buffer sets (a render waits only for the shade that last "
                          "read its buffers)")
+    ap.add_argument("--fresh", action="store_true",
+                    help="every in-flight stream a new torch stream (none is the current/null stream)")
     ap.add_argument("--cache", default="/tmp/och_terrain_cache.npz")
     ap.add_argument("--out", default="gpurun_out/window.json")
     a = ap.parse_args()
@@ -69,7 +71,7 @@ def main():
     for inflight, prio in arms:
         split = prio == "split"
         if prio is None or split:
-            streams = [stream] + [torch.cuda.Stream() for _ in range(inflight - 1)]
+            streams = ([] if a.fresh else [stream]) + [torch.cuda.Stream() for _ in range(inflight - (not a.fresh))]
         else:
             streams = [torch.cuda.Stream(priority=q) for q in prio]
         post = torch.cuda.Stream() if split else None
