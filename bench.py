@@ -388,7 +388,7 @@ def main():
     # PUSH counts of this rank's rays (for the algorithmic byte count): trace
     # the rank's own rows once with counting on; not part of the timed region.
     rows = torch.from_numpy(slice_row_map(H, a.row_chunk, world, rank))
-    push_total, hits_total, rays_rank = 0, 0, 0
+    push_total, walk_push, culled, hits_total, rays_rank = 0, 0, 0, 0, 0
     dirs = torch.empty(W * H * 3, dtype=torch.float32, device=dev)
     o_t = torch.tensor(ORIGIN, dtype=torch.float32, device=dev)
     n_px = W * H
@@ -397,12 +397,23 @@ def main():
     ht = torch.empty(n_px, dtype=torch.float32, device=dev)
     hp = torch.empty(n_px, dtype=torch.int32, device=dev)
     mine = rows[rows >= 0].to(dev).long()
+    cull = pool.get_option("cull")
     for cam in cams:
         pool.raygen_dev(cam, dirs)
+        pool.set_option("cull", 0)             # the reference's PUSH counts
         pool.trace_batch_dev(o_t, dirs, hd, hv, ht, hp)
         push_total += int(hp.view(H, W)[mine].sum().item())
         hits_total += int((hd.view(H, W)[mine] < 6).sum().item())
         rays_rank += int(mine.numel()) * W
+        if cull:                               # the PUSHes the timed (culled) launches walk
+            pool.set_option("cull", 2)
+            pool.trace_batch_dev(o_t, dirs, hd, hv, ht, hp)
+            walked = hp.view(H, W)[mine]
+            walk_push += int(walked.sum().item())
+            culled += int((walked == 0).sum().item())
+    if not cull:
+        walk_push = push_total
+    pool.set_option("cull", cull)
     # trace-only throughput over resident rays (the och_gpu_trace_batch_dev path), N=1 only
     trace_only = None
     if world == 1:
@@ -529,9 +540,10 @@ def main():
     # canonical algorithmic bytes, 24 B in + 12 B out + 4 B per PUSH per ray.
     step_s = elapsed / a.steps
     k_avg_ms = float(kms.mean())
-    canon_bytes = 36 * rays_rank + 4 * push_total
+    canon_bytes = 36 * rays_rank + 4 * walk_push
     hbm = {"bound": "hbm", "bytes_per_launch": int(canon_bytes),
-           "bytes_model": "SURVEY 8(d) canonical: 24 B ray in + 12 B hit record out + 4 B per PUSH, per ray",
+           "bytes_model": "SURVEY 8(d) canonical: 24 B ray in + 12 B hit record out per ray + 4 B per PUSH the "
+                          "launch walks (rays the occupied-box cull proves to miss walk none)",
            "achieved": round(canon_bytes / (k_avg_ms * 1e-3) / 1e9, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
            "frac": round(canon_bytes / (k_avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 5),
            "achieved_per_step": round(canon_bytes / step_s / 1e9, 2),
@@ -541,6 +553,7 @@ def main():
             "kernel_ms": round(k_avg_ms, 4), "kernel_ms_serial": round(latency_ms, 4),
             "ms_per_step": round(step_s * 1e3, 4), "frames_in_flight": len(streams),
             "push_per_ray": round(push_total / rays_rank, 3), "rays_per_launch": rays_rank,
+            "walked_push_per_ray": round(walk_push / rays_rank, 3), "culled_frac": round(culled / rays_rank, 4),
             "traffic": None if pmc is None else pmc.get("hbm_bytes_per_launch"),
             "traffic_note": "PMC 2*FETCH_SIZE + WRITE_SIZE per render launch (MI355X_MICROARCH.md HBM): bytes "
                             "leaving L2, Infinity-Cache hits included", "pmc_source": pmc_src, "hbm": hbm}

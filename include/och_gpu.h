@@ -155,7 +155,12 @@ typedef enum och_option {
                                   planned geometry, else 0.  Dispatch order only: frames are identical */
     OCH_OPT_BOUNCE_COMPACT = 6,/* config 5: 1 (default) = compact each block's secondary rays into its first lanes
                                   (wave ballot/popcount + LDS queue) before tracing them; 0 = trace in place */
-    OCH_OPT_CHUNK_TILES = 7    /* schedule 2: 64-ray tiles per wave, a power of two in 1..64 (default 4) */
+    OCH_OPT_CHUNK_TILES = 7,   /* schedule 2: 64-ray tiles per wave, a power of two in 1..64 (default 4) */
+    OCH_OPT_CULL = 8           /* 1 (default) = a ray whose walk provably never enters the bounding box of the
+                                  pool's voxels (och_pool_occupied_box) is recorded as the miss it would end in,
+                                  without walking; exact, for launches that do not count
+                                  PUSHes.  0 = every ray walks.  2 = diagnostic: launches that count PUSHes
+                                  cull too, a culled ray counting 0 (the PUSHes the culled launch walks) */
 } och_option;
 OCH_API int och_gpu_set_option(och_gpu_pool *pool, int option, int value);
 OCH_API int och_gpu_get_option(const och_gpu_pool *pool, int option, int *value);
@@ -333,6 +338,11 @@ OCH_API void och_host_pool_free(och_host_pool *pool);
  * root_id | root_mask << 24.  out = NULL only reports *out_nodes. */
 OCH_API int och_pool_pack(const uint32_t *nodes, uint32_t n_nodes, uint32_t root, int depth, int index_base,
                           uint32_t *out, uint32_t out_capacity, uint32_t *out_nodes, uint32_t *out_root);
+/* Bounding box of every non-empty leaf voxel reachable from root, in voxel
+ * units: voxel (x, y, z) lies in it iff lo <= (x, y, z) < hi per axis.
+ * Returns OCH_OK with lo = hi = {0, 0, 0} for a pool without voxels. */
+OCH_API int och_pool_occupied_box(const uint32_t *nodes, uint32_t n_nodes, uint32_t root, int depth, int index_base,
+                                  int32_t lo[3], int32_t hi[3]);
 /* h_octree::at over any pool (ORT/och_h_octree.h:239-258). */
 OCH_API uint32_t och_pool_at(const uint32_t *nodes, uint32_t root, int depth, int index_base,
                              int x, int y, int z);

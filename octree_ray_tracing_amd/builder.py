@@ -112,6 +112,16 @@ def build_terrain(depth: int, tunnels: bool = True, dedup: bool = True, rand_kin
                     hp.tree_nodes, hp.build_seconds)
 
 
+def occupied_box(nodes: np.ndarray, root: int, depth: int, index_base: int = 1):
+    """Bounding box of the pool's voxels (och_pool_occupied_box): (lo, hi) in
+    voxel units, voxel (x, y, z) inside iff lo <= (x, y, z) < hi; lo = hi = 0
+    for a pool without voxels.  The kernels' cull box (OCH_OPT_CULL)."""
+    nodes = np.ascontiguousarray(nodes, np.uint32).reshape(-1, 8)
+    lo, hi = (C.c_int32 * 3)(), (C.c_int32 * 3)()
+    call("och_pool_occupied_box", nodes.ctypes.data, nodes.shape[0], int(root), int(depth), int(index_base), lo, hi)
+    return tuple(lo), tuple(hi)
+
+
 def pack_pool(nodes: np.ndarray, root: int, depth: int, index_base: int = 1):
     """The packed device layout of a pool (och_pool_pack): (packed nodes, packed root)."""
     nodes = np.ascontiguousarray(nodes, np.uint32).reshape(-1, 8)

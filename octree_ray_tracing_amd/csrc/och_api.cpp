@@ -153,6 +153,10 @@ struct och_gpu_pool {
     int opt_layout = 1;
     int opt_tile_order = 0;
     int opt_bounce_compact = 1;
+    int opt_cull = 1;
+    // bounding box of the pool's voxels (voxel units, [lo, hi)), for the cull
+    bool box_any = false;
+    int32_t box_lo[3] = {0, 0, 0}, box_hi[3] = {0, 0, 0};
     // host-call staging
     void *d_scratch = nullptr;
     size_t scratch_bytes = 0;
@@ -203,6 +207,16 @@ struct och_gpu_pool {
         for (int t = 0; t < 5; ++t) p.top_ids[t] = pk && !packed_by_slot ? packed_top_ids[t] : 1u;
         p.dim_lo = 1u << (23 - depth);
         p.dim_span = (1u << 22) - p.dim_lo;
+        // 1 + k / 2^depth and 3 - that are exact floats for depth <= 22
+        p.cull = box_any ? opt_cull : 0;
+        for (int a = 0; a < 3; ++a) {
+            const float lo = 1.0F + std::ldexp((float)box_lo[a], -depth);
+            const float hi = 1.0F + std::ldexp((float)box_hi[a], -depth);
+            p.cull_lo[0][a] = lo;
+            p.cull_hi[0][a] = hi;
+            p.cull_lo[1][a] = 3.0F - hi;
+            p.cull_hi[1][a] = 3.0F - lo;
+        }
         return p;
     }
 };
@@ -251,6 +265,71 @@ int validate_pool(const uint32_t *nodes, uint32_t n_nodes, uint32_t root, int de
         cur.swap(next);
     }
     return OCH_OK;
+}
+
+}  // namespace
+
+// Bounding box of the voxels: one post-order walk over the (node, level)
+// pairs, each box memoised in node-local voxel units (a DAG shares subtrees;
+// a node the caller's table shares between levels gets one entry per level).
+bool och::occupied_box(const uint32_t *nodes, uint32_t n_nodes, uint32_t root, int depth, int base, int32_t lo[3],
+                       int32_t hi[3])
+{
+    struct Box {
+        int32_t lo[3], hi[3];
+        bool empty() const { return lo[0] >= hi[0]; }
+    };
+    if ((base == 1 && root == 0) || n_nodes == 0) return false;
+    std::vector<uint8_t> memo_level(n_nodes, 0);     // level + 1 of memo[i], 0 = none
+    std::vector<Box> memo(n_nodes);
+    std::unordered_map<uint64_t, Box> extra;
+    auto walk = [&](auto &self, uint32_t v, int level) -> Box {
+        const uint32_t i = v - base;
+        const uint64_t key = ((uint64_t)i << 5) | (uint64_t)level;
+        if (memo_level[i] == level + 1) return memo[i];
+        if (memo_level[i]) {
+            auto it = extra.find(key);
+            if (it != extra.end()) return it->second;
+        }
+        Box b{{INT32_MAX, INT32_MAX, INT32_MAX}, {INT32_MIN, INT32_MIN, INT32_MIN}};
+        const int32_t half = 1 << (depth - level - 1);   // a child's size in voxels
+        const uint32_t *c = nodes + (size_t)i * 8;
+        for (int k = 0; k < 8; ++k) {
+            if (!c[k]) continue;
+            Box cb{{0, 0, 0}, {1, 1, 1}};                // leaf level: the voxel itself
+            if (level + 1 < depth) {
+                cb = self(self, c[k], level + 1);
+                if (cb.empty()) continue;
+            }
+            for (int a = 0; a < 3; ++a) {
+                const int32_t off = ((k >> a) & 1) * half;
+                b.lo[a] = std::min(b.lo[a], off + cb.lo[a]);
+                b.hi[a] = std::max(b.hi[a], off + cb.hi[a]);
+            }
+        }
+        if (b.lo[0] == INT32_MAX) b = Box{{0, 0, 0}, {0, 0, 0}};
+        if (!memo_level[i]) {
+            memo_level[i] = (uint8_t)(level + 1);
+            memo[i] = b;
+        } else {
+            extra.emplace(key, b);
+        }
+        return b;
+    };
+    const Box b = walk(walk, root, 0);
+    if (b.empty()) return false;
+    for (int a = 0; a < 3; ++a) {
+        lo[a] = b.lo[a];
+        hi[a] = b.hi[a];
+    }
+    return true;
+}
+
+namespace {
+
+void set_box(och_gpu_pool *p, const uint32_t *nodes, uint32_t n_nodes)
+{
+    p->box_any = och::occupied_box(nodes, n_nodes, p->root, p->depth, p->index_base, p->box_lo, p->box_hi);
 }
 
 // Packed layout: every reachable (node, level) pair gets a breadth-first id
@@ -433,6 +512,7 @@ OCH_API int och_gpu_pool_create(const uint32_t *nodes, uint32_t n_nodes, uint32_
     if (hipMemcpy(p->d_nodes + 8 * index_base, nodes, (size_t)n_nodes * 32, hipMemcpyHostToDevice) != hipSuccess)
         return bail(fail(OCH_E_HIP, "node upload failed"));
     p->mirror.assign(nodes, nodes + (size_t)n_nodes * 8);
+    set_box(p, nodes, n_nodes);
     st = upload_packed(p, nodes, n_nodes);
     if (st != OCH_OK) return bail(st);
     hipDeviceProp_t prop;
@@ -516,6 +596,7 @@ OCH_API int och_gpu_pool_update(och_gpu_pool *p, uint32_t first, uint32_t count,
     OCH_HIP(hipStreamSynchronize(p->stream()));
     p->root = root;
     p->last_writer = 0;
+    set_box(p, p->mirror.data(), n_user);
     return upload_packed(p, p->mirror.data(), n_user);
 }
 
@@ -614,7 +695,8 @@ int och::pool_scatter_slots(och_gpu_pool *p, const uint32_t *ids, uint32_t count
     return OCH_OK;
 }
 
-int och::pool_commit(och_gpu_pool *p, uint32_t root, uint32_t packed_root, bool packed, uint64_t writer)
+int och::pool_commit(och_gpu_pool *p, uint32_t root, uint32_t packed_root, bool packed, uint64_t writer,
+                     const int32_t *box_lo, const int32_t *box_hi)
 {
     if (!p || p->index_base != 1) return fail(OCH_E_INVALID, "bad editor flush");
     if (packed && (!p->d_packed || !p->packed_by_slot))
@@ -628,6 +710,11 @@ int och::pool_commit(och_gpu_pool *p, uint32_t root, uint32_t packed_root, bool 
     }
     p->root = root;
     p->packed_root = packed ? packed_root : 0;
+    p->box_any = box_lo && box_hi;
+    for (int a = 0; a < 3; ++a) {
+        p->box_lo[a] = p->box_any ? box_lo[a] : 0;
+        p->box_hi[a] = p->box_any ? box_hi[a] : 0;
+    }
     p->last_writer = writer;
     return OCH_OK;
 }
@@ -717,6 +804,10 @@ OCH_API int och_gpu_set_option(och_gpu_pool *p, int option, int value)
             return fail(OCH_E_INVALID, "chunk tiles %d: a power of two in 1..64", value);
         p->opt_chunk_tiles = value;
         return OCH_OK;
+    case OCH_OPT_CULL:
+        if (value < 0 || value > 2) return fail(OCH_E_INVALID, "cull must be 0, 1 or 2");
+        p->opt_cull = value;
+        return OCH_OK;
     default:
         return fail(OCH_E_INVALID, "unknown option %d", option);
     }
@@ -734,6 +825,7 @@ OCH_API int och_gpu_get_option(const och_gpu_pool *p, int option, int *value)
     case OCH_OPT_TILE_ORDER: *value = p->opt_tile_order; return OCH_OK;
     case OCH_OPT_BOUNCE_COMPACT: *value = p->opt_bounce_compact; return OCH_OK;
     case OCH_OPT_CHUNK_TILES: *value = p->opt_chunk_tiles; return OCH_OK;
+    case OCH_OPT_CULL: *value = p->opt_cull; return OCH_OK;
     default: return fail(OCH_E_INVALID, "unknown option %d", option);
     }
 }
@@ -1092,6 +1184,18 @@ OCH_API int och_pool_pack(const uint32_t *nodes, uint32_t n_nodes, uint32_t root
         if (out_capacity < *out_nodes) return fail(OCH_E_CAPACITY, "output holds %u nodes, %u needed", out_capacity, *out_nodes);
         std::memcpy(out, packed.data(), packed.size() * 4);
     }
+    return OCH_OK;
+}
+
+OCH_API int och_pool_occupied_box(const uint32_t *nodes, uint32_t n_nodes, uint32_t root, int depth, int index_base,
+                                  int32_t lo[3], int32_t hi[3])
+{
+    if (!nodes || !lo || !hi) return fail(OCH_E_INVALID, "NULL argument");
+    if (index_base != 0 && index_base != 1) return fail(OCH_E_INVALID, "index_base must be 0 or 1");
+    const int st = validate_pool(nodes, n_nodes, root, depth, index_base);
+    if (st != OCH_OK) return st;
+    if (!och::occupied_box(nodes, n_nodes, root, depth, index_base, lo, hi))
+        for (int a = 0; a < 3; ++a) lo[a] = hi[a] = 0;
     return OCH_OK;
 }
 

@@ -62,6 +62,20 @@ struct och_editor {
     size_t table_used = 0;                // entries + tombstones
     std::vector<uint32_t> dirty;          // slots written since the last flush (repeats allowed)
     bool root_dirty = false;
+    // A bounding box of the voxels (voxel units, [lo, hi)), handed to the pool
+    // at flush for its cull (OCH_OPT_CULL): exact after adoption, grown by
+    // every set() of a voxel, never shrunk by a removal (a superset is valid).
+    bool box_any = false;
+    int32_t box_lo[3] = {0, 0, 0}, box_hi[3] = {0, 0, 0};
+    void box_add(int x, int y, int z)
+    {
+        const int32_t v[3] = {x, y, z};
+        for (int a = 0; a < 3; ++a) {
+            box_lo[a] = box_any ? std::min(box_lo[a], v[a]) : v[a];
+            box_hi[a] = box_any ? std::max(box_hi[a], v[a] + 1) : v[a] + 1;
+        }
+        box_any = true;
+    }
 
     uint32_t *slot(uint32_t s) { return nodes.data() + (size_t)(s - 1) * 8; }
     const uint32_t *slot(uint32_t s) const { return nodes.data() + (size_t)(s - 1) * 8; }
@@ -362,6 +376,7 @@ OCH_API int och_editor_create(const uint32_t *nodes, uint32_t n_nodes, uint32_t 
         e->renumber_breadth_first();
     }
     e->root_dirty = true;
+    e->box_any = och::occupied_box(e->nodes.data(), e->capacity, e->root, depth, 1, e->box_lo, e->box_hi);
     *out = e;
     return OCH_OK;
 }
@@ -387,6 +402,7 @@ OCH_API int och_editor_set(och_editor *e, int xi, int yi, int zi, uint32_t v)
         cur = cur ? e->slot(cur)[child_of(xi, yi, zi, l)] : 0;
     }
     if (cur == v) return OCH_OK;   // unchanged voxel: the path re-registers to itself
+    if (v) e->box_add(xi, yi, zi);
     uint32_t child = v;
     for (int l = 0; l < e->depth; ++l) {
         uint32_t n[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -474,7 +490,9 @@ OCH_API int och_editor_flush(och_editor *e, och_gpu_pool *pool)
         st = och::pool_scatter_slots(pool, e->dirty.data(), n, raw.data(), pk ? packed.data() : nullptr);
     }
     // The roots go out last, once every slot they reach is on the device.
-    if (st == OCH_OK) st = och::pool_commit(pool, e->root, e->packed_root(), pk != nullptr, e->id);
+    if (st == OCH_OK)
+        st = och::pool_commit(pool, e->root, e->packed_root(), pk != nullptr, e->id, e->box_any ? e->box_lo : nullptr,
+                              e->box_any ? e->box_hi : nullptr);
     if (st != OCH_OK) {
         e->synced = 0;   // the next flush rewrites the pool whole
         return st;

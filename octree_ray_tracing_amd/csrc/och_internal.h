@@ -30,7 +30,17 @@ struct DevPool {
     uint32_t top_ids[5];    // packed layout: ids below top_ids[T] belong to levels 1..T (OCH_LDS_TOP)
     uint32_t dim_lo;        // child-size bit at the leaf level, 1 << (23 - depth)
     uint32_t dim_span;      // (1 << 22) - dim_lo: a walk is active while dim - dim_lo <= dim_span
+    // Occupied-box cull (OCH_OPT_CULL, och_kernels.hip ray_cull): the bounding
+    // box of the pool's voxels in the reflected frame of each direction sign,
+    // [sign][axis]: sign 0 (d <= 0) = world coordinates, sign 1 = 3 - them.
+    int32_t cull;           // 0 off, 1 launches without PUSH counts, 2 all launches
+    float cull_lo[2][3], cull_hi[2][3];
 };
+
+// Bounding box of the reachable non-empty leaf voxels, voxel units, [lo, hi)
+// per axis; false when there are none (och_pool_occupied_box).
+bool occupied_box(const uint32_t *nodes, uint32_t n_nodes, uint32_t root, int depth, int base, int32_t lo[3],
+                  int32_t hi[3]);
 
 // The editor's flush (och_editor.cpp) writes a 1-based pool in three steps:
 //   pool_drain       -- waits for all work on the pool's device (kernels on any
@@ -44,7 +54,9 @@ struct DevPool {
 //                       Roots are not touched, so a failed flush leaves the
 //                       pool tracing its old tree;
 //   pool_commit      -- publishes both roots (packed == false drops the packed
-//                       layout) and records `writer` as the pool's last writer.
+//                       layout) and the editor's voxel bounding box (the cull
+//                       box, OCH_OPT_CULL), and records `writer` as the pool's
+//                       last writer.
 // No re-validation: the editor only writes ids it handed out.
 // pool_serial: a process-unique id of the pool (never reused, unlike its
 // address); pool_last_writer: the editor id of the last commit, 0 after
@@ -55,7 +67,10 @@ int report(int status, const char *msg);
 int pool_drain(och_gpu_pool *pool);
 int pool_write_slots(och_gpu_pool *pool, uint32_t first, uint32_t count, const uint32_t *raw,
                      const uint32_t *packed, bool full);
-int pool_commit(och_gpu_pool *pool, uint32_t root, uint32_t packed_root, bool packed, uint64_t writer);
+// box: the editor's bounding box of its voxels (a superset is fine), or
+// nullptr when it holds none.
+int pool_commit(och_gpu_pool *pool, uint32_t root, uint32_t packed_root, bool packed, uint64_t writer,
+                const int32_t *box_lo, const int32_t *box_hi);
 // pool_write_slots for scattered slots: ids[count] (1..n_nodes-1, distinct),
 // raw / packed = count x 8 words; one staged copy and one scatter kernel,
 // complete on return.

@@ -147,10 +147,42 @@ template <bool kCount>
 __device__ __forceinline__ void ray_push_descend(Ray &r, const DevPool &P, uint32_t stride,
                                                  const uint32_t *top = nullptr);
 
+// Occupied-box cull (OCH_OPT_CULL; DESIGN.md §4b has the proof).  With
+// t_a(q) = fma(q, c_a, b_a), the walk's t of plane q on axis a in the
+// reflected frame (non-increasing in q when c_a < 0), every cell the walk
+// enters -- the HIT cell included -- satisfies
+//     max_a t_a(hi_a) <= t_min <= min_a t_a(lo_a),  t_min >= +0,
+// (its far planes are not yet crossed, its near planes are), so a box holding
+// every voxel that fails  max_a t_a(B.hi_a) <= min_a t_a(B.lo_a) >= 0  is
+// never entered and the ray ends in the MISS the walk would reach.  Holds
+// for c_a negative normal with |c_a| < 2^125 (finite t) and an origin inside
+// the root, (1, 2)^3; other rays walk.
+__device__ __forceinline__ bool ray_cull(const Ray &r, const DevPool &P, const float *o)
+{
+    bool ok = true;
+    float enter = -INFINITY, leave = INFINITY;
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        const uint32_t e = (fbits(r.c[a]) >> 23) & 0xFFu;
+        ok &= e - 1u < 251u;                                                // 1..251
+        ok &= o[a] > 1.0F && o[a] < 2.0F;
+        const bool pos = (r.inv >> a) & 1u;
+        const float lo = pos ? P.cull_lo[1][a] : P.cull_lo[0][a];
+        const float hi = pos ? P.cull_hi[1][a] : P.cull_hi[0][a];
+        enter = fmaxf(enter, __builtin_fmaf(hi, r.c[a], r.b[a]));
+        leave = fminf(leave, __builtin_fmaf(lo, r.c[a], r.b[a]));
+    }
+    return ok && (enter > leave || leave < 0.0F);
+}
+
 // Setup, ORT/och_h_octree.h:294-338, then the first PUSH at the root.
-// stack: this lane's first LDS slot.
 // stack: this lane's LDS column, depth + 1 slots `stride` words apart.
-template <bool kPacked, bool kCount>
+// kCull: a ray that ray_cull proves a miss ends here (ray_active false,
+// ray_result the miss record, 0 PUSHes); the kernel's loop tests ray_active
+// before iterating.  Launches that count PUSHes cull only at OCH_OPT_CULL = 2
+// (a diagnostic: how many PUSHes the culled launch walks), so their counts
+// stay the reference's.
+template <bool kPacked, bool kCount, bool kCull = false>
 __device__ __forceinline__ void ray_init(Ray &r, const DevPool &P, const float *o, const float *d, uint32_t *stack,
                                          uint32_t stride)
 {
@@ -187,6 +219,12 @@ __device__ __forceinline__ void ray_init(Ray &r, const DevPool &P, const float *
     set_mode(r, kAtPush);
     r.child = 0;
     r.push = 0;
+    if (kCull && (kCount ? P.cull == 2 : P.cull != 0) && ray_cull(r, P, o)) {
+        r.dim = 1u << 23;                                                   // finished: the MISS
+        set_mode(r, kStepping);
+        if (!OCH_DIM_LEVEL) r.level = 0;
+        return;
+    }
     if (kPacked && OCH_MERGED_DESCEND)
         ray_push_descend<true>(r, P, stride);
     else
@@ -795,8 +833,8 @@ __global__ void k_trace_grid(DevPool P, Src S, Sink K, uint32_t xcd_group, const
     uint32_t out;
     if (wave_base + lane < S.count() && S.get_wave(wave_base, lane, o, d, out)) {
         Ray r;
-        ray_init<kPacked, kCount>(r, P, o, d, lds_stack + threadIdx.x, blockDim.x);
-        do {
+        ray_init<kPacked, kCount, true>(r, P, o, d, lds_stack + threadIdx.x, blockDim.x);
+        if (ray_active(r, P)) do {
             ray_iterate<kPacked, kCount>(r, P, blockDim.x, top);
         } while (ray_active(r, P));
         K.put(out, ray_result<kPacked>(r, P));
@@ -830,8 +868,8 @@ __global__ void k_trace_bounce(DevPool P, Src S, Sink K, int compact, const uint
     bool want = false;
     if (wave_base + (threadIdx.x & 63u) < S.count() && S.get_wave(wave_base, threadIdx.x & 63u, o, d, out)) {
         Ray r;
-        ray_init<kPacked, kCount>(r, P, o, d, stack, nb);
-        do {
+        ray_init<kPacked, kCount, true>(r, P, o, d, stack, nb);
+        if (ray_active(r, P)) do {
             ray_iterate<kPacked, kCount>(r, P, nb);
         } while (ray_active(r, P));
         const Hit h1 = ray_result<kPacked>(r, P);
@@ -839,8 +877,8 @@ __global__ void k_trace_bounce(DevPool P, Src S, Sink K, int compact, const uint
         if (want) bounce_ray(o, d, h1, P.half_voxel, o2, d2);
         payload = K.put_primary(out, h1, want);
         if (want && !compact) {                                             // in place, no compaction
-            ray_init<kPacked, kCount>(r, P, o2, d2, stack, nb);
-            do {
+            ray_init<kPacked, kCount, true>(r, P, o2, d2, stack, nb);
+            if (ray_active(r, P)) do {
                 ray_iterate<kPacked, kCount>(r, P, nb);
             } while (ray_active(r, P));
             K.put_secondary(out, payload, ray_result<kPacked>(r, P));
@@ -886,8 +924,8 @@ __global__ void k_trace_bounce(DevPool P, Src S, Sink K, int compact, const uint
     __syncthreads();                                  // the queue is read: its LDS becomes stacks again
     if (has) {
         Ray r;
-        ray_init<kPacked, kCount>(r, P, so, sd, stack, nb);
-        do {
+        ray_init<kPacked, kCount, true>(r, P, so, sd, stack, nb);
+        if (ray_active(r, P)) do {
             ray_iterate<kPacked, kCount>(r, P, nb);
         } while (ray_active(r, P));
         K.put_secondary(sout, spay, ray_result<kPacked>(r, P));

@@ -143,11 +143,12 @@ class GpuPool:
         call("och_gpu_pool_update", self._h, int(first), nodes.shape[0], _np_ptr(nodes), int(root))
 
     OPTIONS = {"schedule": 0, "block": 1, "waves_per_cu": 2, "refill": 3, "layout": 4, "tile_order": 5,
-               "bounce_compact": 6, "chunk_tiles": 7}
+               "bounce_compact": 6, "chunk_tiles": 7, "cull": 8}
 
     def set_option(self, name: str, value: int):
         """Launch options (och_gpu_set_option): schedule (0 grid / 1 persistent / 2 grid with lane
-        refill), block, waves_per_cu, refill, layout, tile_order, bounce_compact, chunk_tiles."""
+        refill), block, waves_per_cu, refill, layout, tile_order, bounce_compact, chunk_tiles,
+        cull (1 = rays proven to miss the voxels' bounding box skip the walk; exact)."""
         call("och_gpu_set_option", self._h, self.OPTIONS[name], int(value))
 
     def get_option(self, name: str) -> int:

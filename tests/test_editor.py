@@ -199,6 +199,9 @@ def test_gpu_mirror_after_flushes(ort, O, gpu_device):
         for layout in (1, 0):
             pool.set_option("layout", layout)
             assert_same(gpu_trace_dev(pool, ORIGIN, rays), ref)
+            # launches without PUSH counts cull by the editor's voxel box, grown by
+            # the edits above the terrain (OCH_OPT_CULL)
+            assert_same(gpu_trace_dev(pool, ORIGIN, rays, want_push=False), ref, push=False)
     pool.close()
     ed.close()
 
@@ -230,6 +233,8 @@ def test_gpu_mirror_cleared_and_regrown(ort, O, gpu_device):
         pool.set_option("layout", layout)
         got = gpu_trace_dev(pool, ORIGIN, rays)
         assert np.array_equal(got["dir"], ref["dir"]) and np.array_equal(got["voxel"], ref["voxel"])
+        nc = gpu_trace_dev(pool, ORIGIN, rays, want_push=False)
+        assert np.array_equal(nc["dir"], ref["dir"]) and np.array_equal(nc["t"], ref["t"].view(np.uint32))
         assert np.array_equal(got["t"], ref["t"].view(np.uint32)) and np.array_equal(got["push"], ref["push"])
     pool.close()
 
