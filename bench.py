@@ -382,8 +382,9 @@ def main():
     # the costliest tiles go first (och_gpu_plan_views; dispatch order only,
     # frames identical), so no frame ends on a few late grazing tiles.
     if not any(kv.startswith("tile_order=") for kv in a.opt):
-        pool.plan_views(cams, a.row_chunk, rank, world)
         pool.set_option("tile_order", 2)
+    if pool.get_option("tile_order") >= 2:
+        pool.plan_views(cams, a.row_chunk, rank, world)
 
     # PUSH counts of this rank's rays (for the algorithmic byte count): trace
     # the rank's own rows once with counting on; not part of the timed region.
@@ -511,11 +512,11 @@ def main():
         if rank == 0:
             bounce_host = sfs[(a.steps - 1) % len(sfs)].frames.cpu().numpy()
         pool.set_option("bounce_compact", 0)
-        if pool.get_option("tile_order") == 2:
+        if pool.get_option("tile_order") >= 2:
             pool.plan_views(cams, a.row_chunk, rank, world)       # the plan is per compaction setting
         nc_el, nc_kms = bounce_run(max(a.steps // 2, 3))
         pool.set_option("bounce_compact", 1)
-        if pool.get_option("tile_order") == 2:
+        if pool.get_option("tile_order") >= 2:
             pool.plan_views(cams, a.row_chunk, rank, world)
         pool.set_stream(stream)
         hits = torch.tensor([hits_total], dtype=torch.int64, device=dev)

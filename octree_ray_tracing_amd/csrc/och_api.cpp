@@ -166,6 +166,7 @@ struct och_gpu_pool {
     // cost-planned launch order (och_gpu_plan_views, OCH_OPT_TILE_ORDER = 2)
     // [0] primary frames (grid kernel), [1] config-5 frames (bounce kernel)
     uint32_t *d_order[2] = {nullptr, nullptr};
+    uint32_t *d_order_xcd[2] = {nullptr, nullptr};   // OCH_OPT_TILE_ORDER = 3: the same, grouped per XCD
     uint32_t order_blocks[2] = {0, 0};
     int64_t plan_key[2][8] = {};
 
@@ -549,6 +550,8 @@ OCH_API int och_gpu_pool_destroy(och_gpu_pool *p)
     if (p->d_stage) (void)hipFree(p->d_stage);
     for (uint32_t *o : p->d_order)
         if (o) (void)hipFree(o);
+    for (uint32_t *o : p->d_order_xcd)
+        if (o) (void)hipFree(o);
     if (p->d_counter) (void)hipFree(p->d_counter);
     if (p->ev_start) (void)hipEventDestroy(p->ev_start);
     if (p->ev_stop) (void)hipEventDestroy(p->ev_stop);
@@ -792,7 +795,7 @@ OCH_API int och_gpu_set_option(och_gpu_pool *p, int option, int value)
         p->opt_layout = value;
         return OCH_OK;
     case OCH_OPT_TILE_ORDER:
-        if (value < 0 || value > 2) return fail(OCH_E_INVALID, "tile order must be 0, 1 or 2");
+        if (value < 0 || value > 3) return fail(OCH_E_INVALID, "tile order must be 0..3");
         p->opt_tile_order = value;
         return OCH_OK;
     case OCH_OPT_BOUNCE_COMPACT:
@@ -1018,10 +1021,11 @@ int render_views(och_gpu_pool *p, const och_camera *cams, int n_views, uint32_t 
     f.slice_rows = och_shard_rows(cams[0].height, row_chunk, n_shards);
     och::Schedule sc = p->schedule();
     const int which = bounce ? 1 : 0;
-    if (p->opt_tile_order == 2 && (bounce || p->opt_schedule == 0) && p->d_order[which]) {
+    if (p->opt_tile_order >= 2 && (bounce || p->opt_schedule == 0) && p->d_order[which]) {
         const int64_t key[8] = {cams[0].width, cams[0].height, n_views, row_chunk, shard, n_shards, p->opt_block,
                                 bounce ? p->opt_bounce_compact : 0};
-        if (std::memcmp(key, p->plan_key[which], sizeof key) == 0) sc.order = p->d_order[which];
+        if (std::memcmp(key, p->plan_key[which], sizeof key) == 0)
+            sc.order = p->opt_tile_order == 3 ? p->d_order_xcd[which] : p->d_order[which];
     }
     OCH_HIP(hipEventRecord(p->ev_start, p->stream()));
     if (code_slices)
@@ -1083,14 +1087,42 @@ OCH_API int och_gpu_plan_views(och_gpu_pool *p, const och_camera *cams, int n_vi
         std::vector<uint32_t> order(n_blocks);
         for (uint32_t i = 0; i < n_blocks; ++i) order[i] = i;
         std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return c[a] > c[b]; });
+        // Grouped per XCD (OCH_OPT_TILE_ORDER = 3): workgroup slot i runs on XCD
+        // i % 8, so deal 64x64-pixel supertiles over the XCDs (each XCD's L2 then
+        // holds the nodes of its own neighbouring tiles) and keep the costliest-
+        // first order within each XCD's list.
+        const uint32_t block = (uint32_t)(which ? std::max(och::kBounceBlock, p->opt_block) : p->opt_block);
+        const uint32_t tiles_x = (uint32_t)(W + 7) / 8, tiles_y = (uint32_t)(rows + 7) / 8;
+        const uint32_t stx = (tiles_x + 7) / 8, sty = (tiles_y + 7) / 8;
+        std::vector<std::vector<uint32_t>> lists(8);
+        for (uint32_t b : order) {
+            const uint32_t tile = b * (block / 64), view = tile / (tiles_x * tiles_y), t = tile % (tiles_x * tiles_y);
+            const uint32_t st = (view * sty + (t / tiles_x) / 8) * stx + (t % tiles_x) / 8;
+            lists[st % 8].push_back(b);
+        }
+        std::vector<uint32_t> grouped;
+        grouped.reserve(n_blocks);
+        std::vector<size_t> at(8, 0);
+        while (grouped.size() < n_blocks)
+            for (uint32_t x = 0; x < 8 && grouped.size() < n_blocks; ++x) {
+                uint32_t from = x;
+                if (at[x] == lists[x].size())       // this XCD's list ran dry: the fullest other list
+                    for (uint32_t y = 0; y < 8; ++y)
+                        if (lists[y].size() - at[y] > lists[from].size() - at[from]) from = y;
+                grouped.push_back(lists[from][at[from]++]);
+            }
         if (p->order_blocks[which] < n_blocks) {
-            if (p->d_order[which]) OCH_HIP(hipFree(p->d_order[which]));
-            p->d_order[which] = nullptr;
+            for (uint32_t **o : {&p->d_order[which], &p->d_order_xcd[which]}) {
+                if (*o) OCH_HIP(hipFree(*o));
+                *o = nullptr;
+            }
             p->order_blocks[which] = 0;
             OCH_HIP(hipMalloc(&p->d_order[which], (size_t)n_blocks * 4));
+            OCH_HIP(hipMalloc(&p->d_order_xcd[which], (size_t)n_blocks * 4));
             p->order_blocks[which] = n_blocks;
         }
         OCH_HIP(hipMemcpy(p->d_order[which], order.data(), (size_t)n_blocks * 4, hipMemcpyHostToDevice));
+        OCH_HIP(hipMemcpy(p->d_order_xcd[which], grouped.data(), (size_t)n_blocks * 4, hipMemcpyHostToDevice));
         const int64_t key[8] = {W, H, n_views, row_chunk, shard, n_shards, p->opt_block,
                                 which ? p->opt_bounce_compact : 0};
         std::memcpy(p->plan_key[which], key, sizeof key);

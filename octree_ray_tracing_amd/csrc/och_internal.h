@@ -95,6 +95,10 @@ struct DevFrame {
     int32_t row_chunk, shard, n_shards, slice_rows;
 };
 
+// Threads per workgroup of the config-5 (bounce) kernels: compaction spans
+// the block's 4 waves.
+constexpr int kBounceBlock = 256;
+
 // How trace/render launches are scheduled (och_gpu_set_option).
 struct Schedule {
     int kind;               // 0 grid, 1 persistent (resident waves pulling rays from *counter),

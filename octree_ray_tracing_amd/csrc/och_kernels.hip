@@ -1171,7 +1171,6 @@ hipError_t launch(const DevPool &p, const Src &s, const Sink &k, uint32_t n, con
                     : launch_as<Src, Sink, false, kCount>(p, s, k, n, sc, stream, supertile_rays);
 }
 
-constexpr int kBounceBlock = 256;   // compaction spans the block's 4 waves
 
 template <class Src, class Sink, bool kCount>
 hipError_t launch_bounce(const DevPool &p, const Src &s, const Sink &k, uint32_t n, const Schedule &sc, hipStream_t stream)

@@ -537,9 +537,10 @@ def test_refill_schedule_variants(ort, O, gpu_device, chunk, refill):
     pool.close()
 
 
-def test_planned_launch_order(ort, O, gpu_device):
+@pytest.mark.parametrize("order", [2, 3])
+def test_planned_launch_order(ort, O, gpu_device, order):
     """OCH_OPT_TILE_ORDER = 2: the costliest tiles of a planning frame go first
-    (och_gpu_plan_views).  Dispatch order only: frames of the planned geometry,
+    (och_gpu_plan_views); 3: the same, 64x64-pixel supertiles dealt over the XCDs.  Dispatch order only: frames of the planned geometry,
     of another geometry (natural order) and after the camera moved are all
     the oracle's."""
     import torch
@@ -552,7 +553,7 @@ def test_planned_launch_order(ort, O, gpu_device):
     W, H = 803, 451
     cams = [ort.camera((1.5, 1.5, 1.5), 0.3, p, 1.25, W, H) for p in (0.0, -0.6)]
     pool.plan_views(cams, 8, 0, 1)
-    pool.set_option("tile_order", 2)
+    pool.set_option("tile_order", order)
     for yaw in (0.3, 0.9):                   # the planned views, then a moved camera
         cams = [ort.camera((1.5, 1.5, 1.5), yaw, p, 1.25, W, H) for p in (0.0, -0.6)]
         want = []
