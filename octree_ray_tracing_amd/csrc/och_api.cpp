@@ -208,15 +208,11 @@ struct och_gpu_pool {
         for (int t = 0; t < 5; ++t) p.top_ids[t] = pk && !packed_by_slot ? packed_top_ids[t] : 1u;
         p.dim_lo = 1u << (23 - depth);
         p.dim_span = (1u << 22) - p.dim_lo;
-        // 1 + k / 2^depth and 3 - that are exact floats for depth <= 22
+        // 1 + k / 2^depth is an exact float for depth <= 22
         p.cull = box_any ? opt_cull : 0;
         for (int a = 0; a < 3; ++a) {
-            const float lo = 1.0F + std::ldexp((float)box_lo[a], -depth);
-            const float hi = 1.0F + std::ldexp((float)box_hi[a], -depth);
-            p.cull_lo[0][a] = lo;
-            p.cull_hi[0][a] = hi;
-            p.cull_lo[1][a] = 3.0F - hi;
-            p.cull_hi[1][a] = 3.0F - lo;
+            p.cull_lo[a] = 1.0F + std::ldexp((float)box_lo[a], -depth);
+            p.cull_hi[a] = 1.0F + std::ldexp((float)box_hi[a], -depth);
         }
         return p;
     }

@@ -31,10 +31,9 @@ struct DevPool {
     uint32_t dim_lo;        // child-size bit at the leaf level, 1 << (23 - depth)
     uint32_t dim_span;      // (1 << 22) - dim_lo: a walk is active while dim - dim_lo <= dim_span
     // Occupied-box cull (OCH_OPT_CULL, och_kernels.hip ray_cull): the bounding
-    // box of the pool's voxels in the reflected frame of each direction sign,
-    // [sign][axis]: sign 0 (d <= 0) = world coordinates, sign 1 = 3 - them.
+    // box of the pool's voxels, world coordinates (1 + voxel / 2^depth).
     int32_t cull;           // 0 off, 1 launches without PUSH counts, 2 all launches
-    float cull_lo[2][3], cull_hi[2][3];
+    float cull_lo[3], cull_hi[3];
 };
 
 // Bounding box of the reachable non-empty leaf voxels, voxel units, [lo, hi)

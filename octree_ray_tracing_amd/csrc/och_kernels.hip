@@ -42,14 +42,16 @@ __device__ __forceinline__ float ffrom(uint32_t u) { return __uint_as_float(u); 
 
 // RCPPS model (ORT/och_h_octree.h:316): the table holds RCPPS(-(1 + m/2^k))
 // for exponent-127 inputs; other exponents move the result exponent.
-__device__ __forceinline__ uint32_t rcpps(uint32_t x, const uint32_t *__restrict__ lut, int shift)
+// ent = lut[(x & 0x7FFFFF) >> shift], read by the caller for every input (the
+// index is in range for any x), so a ray's three lookups are in flight together.
+__device__ __forceinline__ uint32_t rcpps(uint32_t x, uint32_t ent)
 {
     const uint32_t sign = x & 0x80000000u, e = (x >> 23) & 0xFFu;
-    if (e == 0) return sign | 0x7F800000u;                          // +-0, denormal -> inf
-    if (e == 0xFFu) return (x & 0x7FFFFFu) ? (x | 0x400000u) : sign;
-    const uint32_t ent = lut[(x & 0x7FFFFFu) >> shift];
     const int ne = (int)((ent >> 23) & 0xFFu) + 127 - (int)e;
-    return ne <= 0 ? sign : (sign | ((uint32_t)ne << 23) | (ent & 0x7FFFFFu));
+    uint32_t r = ne <= 0 ? sign : (sign | ((uint32_t)ne << 23) | (ent & 0x7FFFFFu));
+    r = e == 0 ? (sign | 0x7F800000u) : r;                              // +-0, denormal -> inf
+    r = e == 0xFFu ? ((x & 0x7FFFFFu) ? (x | 0x400000u) : sign) : r;    // NaN (quietened), inf -> 0
+    return r;
 }
 
 struct Hit {
@@ -166,11 +168,13 @@ __device__ __forceinline__ bool ray_cull(const Ray &r, const DevPool &P, const f
         const uint32_t e = (fbits(r.c[a]) >> 23) & 0xFFu;
         ok &= e - 1u < 251u;                                                // 1..251
         ok &= o[a] > 1.0F && o[a] < 2.0F;
-        const bool pos = (r.inv >> a) & 1u;
-        const float lo = pos ? P.cull_lo[1][a] : P.cull_lo[0][a];
-        const float hi = pos ? P.cull_hi[1][a] : P.cull_hi[0][a];
-        enter = fmaxf(enter, __builtin_fmaf(hi, r.c[a], r.b[a]));
-        leave = fminf(leave, __builtin_fmaf(lo, r.c[a], r.b[a]));
+        // the box's two planes in the reflected frame, |K - Q| as setup reflects
+        // the origin (:314): exact, K - Q lies in [1, 2] or is -Q
+        const float k = (r.inv >> a) & 1u ? 3.0F : 0.0F;
+        const float t1 = __builtin_fmaf(fabsf(__fsub_rn(k, P.cull_lo[a])), r.c[a], r.b[a]);
+        const float t2 = __builtin_fmaf(fabsf(__fsub_rn(k, P.cull_hi[a])), r.c[a], r.b[a]);
+        enter = fmaxf(enter, fminf(t1, t2));        // t of the far plane (the larger q)
+        leave = fminf(leave, fmaxf(t1, t2));
     }
     return ok && (enter > leave || leave < 0.0F);
 }
@@ -188,13 +192,17 @@ __device__ __forceinline__ void ray_init(Ray &r, const DevPool &P, const float *
 {
     r.inv = 24;
     r.idx = 0;
+    uint32_t ent[3];
+#pragma unroll
+    for (int a = 0; a < 3; ++a) ent[a] = P.lut[(fbits(d[a]) & 0x7FFFFFu) >> P.lut_shift];
+    asm volatile("" : "+v"(ent[0]), "+v"(ent[1]), "+v"(ent[2]));   // three loads issued, then one wait
 #pragma unroll
     for (int a = 0; a < 3; ++a) {
         const uint32_t db = fbits(d[a]);
         const bool positive = (int32_t)db > 0 && db <= 0x7F800000u;          // 0 < d, :310
         r.inv |= (uint32_t)positive << a;
         const float refl = fabsf(__fsub_rn(positive ? 3.0F : 0.0F, o[a]));   // :314
-        const uint32_t cb = rcpps(db | 0x80000000u, P.lut, P.lut_shift);     // :312, :316
+        const uint32_t cb = rcpps(db | 0x80000000u, ent[a]);                 // :312, :316
         r.c[a] = ffrom(cb);
         r.b[a] = ffrom(fbits(__fmul_rn(r.c[a], refl)) ^ 0x80000000u);       // :318
         // A zero or denormal d gives c = -inf, b = +inf and t = fma(p, -inf,
