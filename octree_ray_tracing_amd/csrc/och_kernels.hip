@@ -71,6 +71,7 @@ struct Ray {
     uint32_t dim;         // mantissa bit of the current child size
     uint32_t cur;         // the current node: packed slot word (id | child mask << 24), or raw index
     uint32_t *sp;         // this lane's LDS stack slot for the current level (parents below it)
+    uint32_t *sp23;       // sp at dim = 1 (slot 23): sp = sp23 - ctz(dim) * stride (OCH_POP_CHAIN)
     uint32_t t_min;       // bits of the entry t of the current cell
     uint32_t min_axis;    // 1, 2, 4 (last STEP axis) or 8 (none yet)
     uint32_t child;       // slot word loaded by the last PUSH (pending); the voxel id after a hit
@@ -140,6 +141,11 @@ __device__ __forceinline__ void ray_push(Ray &r, const DevPool &P)
 // the stack), so the next PUSH needs no "pending" select.
 #ifndef OCH_LOAD_INTO_CUR
 #define OCH_LOAD_INTO_CUR 1
+#endif
+// OCH_POP_CHAIN: a POP and the POPs and the advance that follow it in one step
+// (merged loop; ray_phase_step has the proof).
+#ifndef OCH_POP_CHAIN
+#define OCH_POP_CHAIN 1
 #endif
 // OCH_DUAL: the grid kernel walks two rays per lane (two tiles per wave).
 #ifndef OCH_DUAL
@@ -221,6 +227,7 @@ __device__ __forceinline__ void ray_init(Ray &r, const DevPool &P, const float *
     r.dim = 1u << 22;                                                       // :326
     r.cur = P.root;
     r.sp = stack + stride;                                                  // slot 0: the miss POP's dummy read
+    r.sp23 = stack + 23u * stride;                                          // slot 23 - ctz(dim)
     r.t_min = 0;                                                            // +0.0F
     if (!OCH_DIM_LEVEL) r.level = 1;
     r.min_axis = 8;
@@ -274,7 +281,53 @@ __device__ __forceinline__ void ray_phase_step(Ray &r, uint32_t stride)
     const uint32_t axis = sx ? 1u : (sy ? 2u : 4u);
     r.min_axis = axis;
     r.t_min = tm;
-    const uint32_t adv = r.idx & axis;
+    uint32_t adv = r.idx & axis;
+#if OCH_POP_CHAIN
+    if (kPacked && OCH_MERGED_DESCEND) {
+        // POP chain.  After a POP (:421-446) the next STEP sees the parent's
+        // lower planes: on the exit axis a the same plane (the child was the
+        // lower half there), on every other axis the same or a lower one, whose
+        // t is the same or larger.  When all three t are non-negative floats
+        // (so the unsigned compare of :384-406 is the float order) that STEP
+        // picks axis a again with the same t_min, and it POPs again while the
+        // position bit of axis a is clear at that level.  So the walk POPs to
+        // the level of the lowest set bit of p_a above the current one and
+        // advances there on axis a -- or, with no such bit, POPs past the root
+        // (the MISS).  Nothing
+        // in between is counted or recorded; the chain lands in the state the
+        // POP-by-POP walk reaches, one STEP of it later.  Rays with a negative
+        // or NaN t (zero / denormal direction components, origins outside the
+        // root) take one POP as before.
+        if (!adv) {
+            const bool chain = max(max(tx, ty), tz) < 0x80000000u;
+            const uint32_t pa = sx ? r.p[0] : (sy ? r.p[1] : r.p[2]);
+            // bit 23 stands for "past the root": the MISS, also when p_a has no
+            // bit at 23 (an origin outside the root reflects to p = 0 or below 1)
+            const uint32_t up = chain ? ((pa & (0u - (r.dim << 1))) | (1u << 23)) : (r.dim << 1);
+            const uint32_t nd = up & (0u - up);                             // new child-size bit
+            const uint32_t k = __builtin_ctz(nd);
+            r.sp = r.sp23 - k * stride;
+            r.cur = *r.sp;                                                  // :434 (slot 0 after the MISS)
+            const uint32_t keep = 0u - nd;                                  // clears the levels popped, :436
+            r.p[0] &= keep;
+            r.p[1] &= keep;
+            r.p[2] &= keep;
+            r.dim = nd;
+            uint32_t zy = (__builtin_amdgcn_ubfe(r.p[2], k, 1) << 1) | __builtin_amdgcn_ubfe(r.p[1], k, 1);
+            asm volatile("" : "+v"(zy));
+            r.idx = (zy << 1) | __builtin_amdgcn_ubfe(r.p[0], k, 1);        // :440-444
+            adv = chain && nd <= (1u << 22) ? axis : 0u;                    // the advance at that level
+        }
+        r.mode = adv;
+        if (adv) {                                                          // advance :413-419
+            r.p[0] ^= sx ? r.dim : 0u;
+            r.p[1] ^= sy ? r.dim : 0u;
+            r.p[2] ^= sz ? r.dim : 0u;
+            r.idx ^= axis;
+        }
+        return;
+    }
+#endif
     // merged loop: the phase is the advance test itself -- nonzero (a PUSH is
     // due) after an advance, kStepping (0) after a POP; no write per branch
     if (kPacked && OCH_MERGED_DESCEND) r.mode = adv;
