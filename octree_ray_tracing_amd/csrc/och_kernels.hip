@@ -401,6 +401,31 @@ __device__ __forceinline__ bool ray_active(const Ray &r, const DevPool &P)
 // node of the next PUSH, or the voxel id of a HIT -- is loaded, and the next
 // PUSH takes it (mode kPending) after the other lanes' STEP phase has hidden
 // the load.  Two phases per iteration instead of three.
+// The descent of a PUSH that found its child (packed, merged loop): the
+// parent to the stack, the child's slot word loaded into cur, the child
+// cell chosen (:357-373); at the leaf level this is the HIT.
+template <bool kCount>
+__device__ __forceinline__ void ray_descend(Ray &r, const DevPool &P, uint32_t stride)
+{
+    const uint32_t c24 = r.idx ^ r.inv;
+    const uint32_t off = ((r.cur & kIdMask) << 5) + (c24 << 2);
+    const uint32_t *src = reinterpret_cast<const uint32_t *>(reinterpret_cast<const char *>(P.nodes) - 96 + off);
+    *r.sp = r.cur;
+    r.sp += stride;
+    r.cur = *src;
+    r.dim >>= 1;
+    const float tm = ffrom(r.t_min);
+    uint32_t nidx = 0;
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        const uint32_t mid = r.p[a] | r.dim;
+        const bool upper = __builtin_fmaf(ffrom(mid), r.c[a], r.b[a]) >= tm;
+        nidx |= (uint32_t)upper << a;
+        r.p[a] = upper ? mid : r.p[a];
+    }
+    r.idx = nidx;
+}
+
 template <bool kCount>
 __device__ __forceinline__ void ray_push_descend(Ray &r, const DevPool &P, uint32_t stride, const uint32_t *top)
 {
@@ -465,6 +490,52 @@ __device__ __forceinline__ void ray_iterate(Ray &r, const DevPool &P, uint32_t s
     if (in_mode(r, kStepping)) ray_phase_step<kPacked>(r, stride);
     if (kPacked && in_mode(r, kPending)) ray_phase_descend<kPacked>(r, P, stride);
     if (in_mode(r, kAtPush) && ray_active(r, P)) ray_push<kPacked, kCount>(r, P);   // PUSH :342-344
+}
+
+// OCH_STEP_RUN: the packed walk as one descent per iteration -- every lane
+// STEPs (advancing, or POP-chaining then advancing) until it stands at a
+// present child, then all lanes descend together.  The same PUSH / STEP / POP
+// sequence per ray as ray_iterate, in half the iterations (a lane that finds an
+// empty child steps on at once instead of waiting for the next iteration).
+#ifndef OCH_STEP_RUN
+#define OCH_STEP_RUN 0
+#endif
+__device__ __forceinline__ bool child_present(const Ray &r)
+{
+    return __builtin_amdgcn_ubfe(r.cur, r.idx ^ r.inv, 1u) != 0;
+}
+
+template <bool kCount>
+__device__ __forceinline__ void ray_walk_packed(Ray &r, const DevPool &P, uint32_t stride)
+{
+    while (ray_active(r, P)) {
+        // the child of the node the last descent loaded (or ray_init's root PUSH)
+        if (r.mode != kStepping) {
+            if (kCount) ++r.push;
+            if (!child_present(r)) r.mode = kStepping;
+        }
+        while (r.mode == kStepping && ray_active(r, P)) {
+            ray_phase_step<true>(r, stride);                    // advance, or POP chain + advance
+            if (r.mode != kStepping) {
+                if (kCount) ++r.push;                           // PUSH :342-344
+                if (!child_present(r)) r.mode = kStepping;
+            }
+        }
+        if (r.mode != kStepping) ray_descend<kCount>(r, P, stride);
+    }
+}
+
+// Walk an initialised ray to its HIT or MISS.
+template <bool kPacked, bool kCount>
+__device__ __forceinline__ void ray_run(Ray &r, const DevPool &P, uint32_t stride, const uint32_t *top = nullptr)
+{
+    if (kPacked && OCH_STEP_RUN && OCH_MERGED_DESCEND && OCH_LOAD_INTO_CUR && OCH_POP_CHAIN && !OCH_LDS_TOP) {
+        ray_walk_packed<kCount>(r, P, stride);
+        return;
+    }
+    if (ray_active(r, P)) do {
+        ray_iterate<kPacked, kCount>(r, P, stride, top);
+    } while (ray_active(r, P));
 }
 
 // The hit record of a finished ray (:346-355 hit, :423-431 miss).  The
@@ -895,9 +966,7 @@ __global__ void k_trace_grid(DevPool P, Src S, Sink K, uint32_t xcd_group, const
     if (wave_base + lane < S.count() && S.get_wave(wave_base, lane, o, d, out)) {
         Ray r;
         ray_init<kPacked, kCount, true>(r, P, o, d, lds_stack + threadIdx.x, blockDim.x);
-        if (ray_active(r, P)) do {
-            ray_iterate<kPacked, kCount>(r, P, blockDim.x, top);
-        } while (ray_active(r, P));
+        ray_run<kPacked, kCount>(r, P, blockDim.x, top);
         K.put(out, ray_result<kPacked>(r, P));
     }
 #endif
@@ -930,18 +999,14 @@ __global__ void k_trace_bounce(DevPool P, Src S, Sink K, int compact, const uint
     if (wave_base + (threadIdx.x & 63u) < S.count() && S.get_wave(wave_base, threadIdx.x & 63u, o, d, out)) {
         Ray r;
         ray_init<kPacked, kCount, true>(r, P, o, d, stack, nb);
-        if (ray_active(r, P)) do {
-            ray_iterate<kPacked, kCount>(r, P, nb);
-        } while (ray_active(r, P));
+        ray_run<kPacked, kCount>(r, P, nb);
         const Hit h1 = ray_result<kPacked>(r, P);
         want = h1.dir < OCH_EXIT;
         if (want) bounce_ray(o, d, h1, P.half_voxel, o2, d2);
         payload = K.put_primary(out, h1, want);
         if (want && !compact) {                                             // in place, no compaction
             ray_init<kPacked, kCount, true>(r, P, o2, d2, stack, nb);
-            if (ray_active(r, P)) do {
-                ray_iterate<kPacked, kCount>(r, P, nb);
-            } while (ray_active(r, P));
+            ray_run<kPacked, kCount>(r, P, nb);
             K.put_secondary(out, payload, ray_result<kPacked>(r, P));
         }
     }
@@ -986,9 +1051,7 @@ __global__ void k_trace_bounce(DevPool P, Src S, Sink K, int compact, const uint
     if (has) {
         Ray r;
         ray_init<kPacked, kCount, true>(r, P, so, sd, stack, nb);
-        if (ray_active(r, P)) do {
-            ray_iterate<kPacked, kCount>(r, P, nb);
-        } while (ray_active(r, P));
+        ray_run<kPacked, kCount>(r, P, nb);
         K.put_secondary(sout, spay, ray_result<kPacked>(r, P));
     }
     if (cost && threadIdx.x == 0) cost[blk] = (uint32_t)(__builtin_amdgcn_s_memtime() - c0);
