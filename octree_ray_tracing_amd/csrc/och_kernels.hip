@@ -281,9 +281,11 @@ __device__ __forceinline__ void ray_phase_step(Ray &r, uint32_t stride)
     const uint32_t axis = sx ? 1u : (sy ? 2u : 4u);
     r.min_axis = axis;
     r.t_min = tm;
-    uint32_t adv = r.idx & axis;
 #if OCH_POP_CHAIN
     if (kPacked && OCH_MERGED_DESCEND) {
+        // the phase register holds the advance test itself: nonzero (a PUSH is
+        // due) after an advance, kStepping (0) while POPs are left to do
+        r.mode = r.idx & axis;
         // POP chain.  After a POP (:421-446) the next STEP sees the parent's
         // lower planes: on the exit axis a the same plane (the child was the
         // lower half there), on every other axis the same or a lower one, whose
@@ -298,7 +300,7 @@ __device__ __forceinline__ void ray_phase_step(Ray &r, uint32_t stride)
         // POP-by-POP walk reaches, one STEP of it later.  Rays with a negative
         // or NaN t (zero / denormal direction components, origins outside the
         // root) take one POP as before.
-        if (!adv) {
+        if (!r.mode) {
             const bool chain = max(max(tx, ty), tz) < 0x80000000u;
             const uint32_t pa = sx ? r.p[0] : (sy ? r.p[1] : r.p[2]);
             // bit 23 stands for "past the root": the MISS, also when p_a has no
@@ -306,7 +308,8 @@ __device__ __forceinline__ void ray_phase_step(Ray &r, uint32_t stride)
             const uint32_t up = chain ? ((pa & (0u - (r.dim << 1))) | (1u << 23)) : (r.dim << 1);
             const uint32_t nd = up & (0u - up);                             // new child-size bit
             const uint32_t k = __builtin_ctz(nd);
-            r.sp = r.sp23 - k * stride;
+            // one 24-bit multiply-add: k < 32, stride <= 1024 words
+            r.sp = reinterpret_cast<uint32_t *>(reinterpret_cast<char *>(r.sp23) - __mul24((int)k, 4 * (int)stride));
             r.cur = *r.sp;                                                  // :434 (slot 0 after the MISS)
             const uint32_t keep = 0u - nd;                                  // clears the levels popped, :436
             r.p[0] &= keep;
@@ -316,10 +319,9 @@ __device__ __forceinline__ void ray_phase_step(Ray &r, uint32_t stride)
             uint32_t zy = (__builtin_amdgcn_ubfe(r.p[2], k, 1) << 1) | __builtin_amdgcn_ubfe(r.p[1], k, 1);
             asm volatile("" : "+v"(zy));
             r.idx = (zy << 1) | __builtin_amdgcn_ubfe(r.p[0], k, 1);        // :440-444
-            adv = chain && nd <= (1u << 22) ? axis : 0u;                    // the advance at that level
+            r.mode = chain && nd <= (1u << 22) ? axis : 0u;                 // the advance at that level
         }
-        r.mode = adv;
-        if (adv) {                                                          // advance :413-419
+        if (r.mode) {                                                       // advance :413-419
             r.p[0] ^= sx ? r.dim : 0u;
             r.p[1] ^= sy ? r.dim : 0u;
             r.p[2] ^= sz ? r.dim : 0u;
@@ -328,6 +330,7 @@ __device__ __forceinline__ void ray_phase_step(Ray &r, uint32_t stride)
         return;
     }
 #endif
+    const uint32_t adv = r.idx & axis;
     // merged loop: the phase is the advance test itself -- nonzero (a PUSH is
     // due) after an advance, kStepping (0) after a POP; no write per branch
     if (kPacked && OCH_MERGED_DESCEND) r.mode = adv;
