@@ -503,11 +503,16 @@ def main():
     bounce_host = None
     if not a.no_bounce:
         def bounce_run(n):
-            for k in range(2):
+            # warmup as for the primary line, then the median of three timed runs
+            # (one 20-step window alone swings by +-10 %)
+            for k in range(max(a.warmup, 2)):
                 step(k, None, True)
-            bev = []
-            el = timed(n, bounce=True, ev=bev)
-            return el, float(np.mean([x.elapsed_time(y) for x, y in bev]))
+            els, kms_ = [], []
+            for _ in range(3):
+                bev = []
+                els.append(timed(n, bounce=True, ev=bev))
+                kms_.append(float(np.mean([x.elapsed_time(y) for x, y in bev])))
+            return statistics.median(els), statistics.median(kms_)
         b_el, b_kms = bounce_run(a.steps)
         if rank == 0:
             bounce_host = sfs[(a.steps - 1) % len(sfs)].frames.cpu().numpy()
