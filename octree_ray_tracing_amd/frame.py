@@ -51,7 +51,7 @@ class ShardedFrame:
     """
 
     def __init__(self, pool: GpuPool, width: int, height: int, row_chunk: int = 8, n_views: int = 1, group=None,
-                 indexed: bool = False):
+                 indexed: bool = False, shard: tuple[int, int] | None = None):
         import torch
         import torch.distributed as dist
 
@@ -59,6 +59,13 @@ class ShardedFrame:
         self.n_views, self.group = n_views, group
         self.rank = dist.get_rank(group) if dist.is_initialized() else 0
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        # shard=(rank, world) without a process group: one rank's share of an
+        # N-rank frame on this GPU alone (tools/proxy_rank.py); exchange() then
+        # shades the gathered buffer without a collective
+        self.proxy = shard is not None and not dist.is_initialized()
+        if self.proxy:
+            self.rank, self.world = shard
+            assert 0 <= self.rank < self.world
         self.rows = shard_rows(height, row_chunk, self.world)
         # indexed=True: ranks render and exchange 1-byte colour codes (OCH_CODE_*)
         # and shade after the gather -- a quarter of the RGBA8 bytes on xGMI,
@@ -88,7 +95,12 @@ class ShardedFrame:
         import torch.distributed as dist
 
         src = self.slice
-        if self.world > 1:
+        if self.proxy:
+            # the bytes a gather lands in this rank's buffer, written on the
+            # device (every slot gets this rank's slice; no xGMI time)
+            self.gathered.copy_(self.slice.unsqueeze(0).expand_as(self.gathered))
+            src = self.gathered
+        elif self.world > 1:
             if dist.get_backend(self.group) == "gloo":      # host-staged (CPU tests, rehearsal runs)
                 host = self.gathered.new_empty(self.gathered.shape, device="cpu")
                 dist.all_gather(list(host.unbind(0)), self.slice.cpu(), group=self.group)

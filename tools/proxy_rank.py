@@ -1,0 +1,116 @@
+"""One rank's share of an N-rank bench step, on this one GPU (no collective).
+
+At N > 1 bench.py renders configs[3] (3840x2160, two views) split over the
+ranks; each rank renders its row chunks, all-gathers the 1-byte codes and
+shades the whole frame.  This tool times exactly that per-rank GPU work --
+the render of shard 0 of N and the shade of the full frame, with the
+gathered buffer written on the device instead of over xGMI -- for several
+frames-in-flight settings, so the N = 2/4/8 per-rank step can be measured
+on a 1-GPU box.  The xGMI receive time is not in it (estimated separately in
+DESIGN.md §5).
+
+python tools/proxy_rank.py --worlds 8 --inflight 3
+
+Run one (world, inflight) arm per process: HIP maps streams onto its hardware
+queues in creation order, and which streams share a queue moves the result by
+20 %, so every arm must create its streams as bench.py does --
+the current stream plus inflight - 1 new ones -- in a fresh process.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import statistics
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+
+sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--depth", type=int, default=12)
+    ap.add_argument("--worlds", default="1,2,4,8")
+    ap.add_argument("--inflight", default="2,3,4,6")
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--windows", type=int, default=7, help="20-step windows per arm (median)")
+    ap.add_argument("--sustain-steps", type=int, default=400)
+    ap.add_argument("--cache", default="/tmp/och_terrain_cache.npz")
+    ap.add_argument("--out", default="gpurun_out/proxy_rank.json")
+    ap.add_argument("--no-exchange", action="store_true", help="render only: no gather copy, no shade")
+    ap.add_argument("--opt", action="append", default=[], metavar="NAME=VALUE", help="pool option, e.g. chain=1")
+    a = ap.parse_args()
+
+    import torch
+    import octree_ray_tracing_amd as ort
+    from octree_ray_tracing_amd.frame import ShardedFrame
+
+    torch.cuda.set_device(0)
+    cache = Path(a.cache)
+    if cache.exists() and int(np.load(cache)["depth"]) == a.depth:
+        z = np.load(cache)
+        nodes, root = z["nodes"], int(z["root"])
+    else:
+        tree = ort.build_terrain(a.depth, use_gpu=True)
+        nodes, root = tree.nodes, tree.root
+        np.savez(cache, nodes=nodes, root=root, depth=a.depth)
+    pool = ort.HOctree(nodes, root, a.depth, device=0)
+    pool.set_palette(ort.VoxelData().get_colours())
+    base = torch.cuda.current_stream()
+    pool.set_stream(base)
+    pool.set_option("tile_order", 2)
+    opts = dict(kv.split("=") for kv in a.opt)
+    for k, v in opts.items():
+        pool.set_option(k, int(v))
+    res = []
+    for world in [int(x) for x in a.worlds.split(",")]:
+        W, H = (1920, 1080) if world == 1 else (3840, 2160)     # configs[2] / configs[3]
+        cams = [ort.camera((1.5, 1.5, 1.5), 0.3, p, 1.25, W, H) for p in (0.0, -0.6)]
+        pool.plan_views(cams, 8, 0, world)
+        rays_rank = None
+        for nf in [int(x) for x in a.inflight.split(",")]:
+            streams = [base] + [torch.cuda.Stream() for _ in range(nf - 1)]
+            sfs = []
+            for s_ in streams:
+                with torch.cuda.stream(s_):
+                    sfs.append(ShardedFrame(pool, W, H, 8, n_views=2, indexed=True, shard=(0, world)))
+            rows = sfs[0].rows
+            from octree_ray_tracing_amd.frame import slice_row_map
+            rays_rank = int((slice_row_map(H, 8, world, 0) >= 0).sum()) * W * 2
+
+            def run(n):
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                for k in range(n):
+                    s_, f_ = streams[k % nf], sfs[k % nf]
+                    pool.set_stream(s_)
+                    with torch.cuda.stream(s_):
+                        f_.render_local(cams)
+                        if not a.no_exchange:
+                            f_.exchange()
+                torch.cuda.synchronize()
+                return time.perf_counter() - t0
+
+            run(5)
+            wins = [run(a.steps) for _ in range(a.windows)]
+            sus = [run(a.sustain_steps) for _ in range(3)]
+            row = {"world": world, "frame": f"{W}x{H}", "inflight": nf, "opts": opts, "exchange": not a.no_exchange, "rays_per_step_rank": rays_rank,
+                   "slice_rows": rows,
+                   "ms_per_step_20": round(statistics.median(wins) / a.steps * 1e3, 4),
+                   "mrays_s_rank_20": round(rays_rank * a.steps / statistics.median(wins) / 1e6, 1),
+                   "ms_per_step_sustained": round(statistics.median(sus) / a.sustain_steps * 1e3, 4),
+                   "mrays_s_rank_sustained": round(rays_rank * a.sustain_steps / statistics.median(sus) / 1e6, 1)}
+            print(json.dumps(row), flush=True)
+            res.append(row)
+            pool.set_stream(base)
+            del sfs
+    Path(a.out).parent.mkdir(parents=True, exist_ok=True)
+    Path(a.out).write_text(json.dumps(res, indent=1))
+    pool.close()
+
+
+if __name__ == "__main__":
+    main()
