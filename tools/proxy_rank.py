@@ -41,6 +41,7 @@ def main():
     ap.add_argument("--cache", default="/tmp/och_terrain_cache.npz")
     ap.add_argument("--out", default="gpurun_out/proxy_rank.json")
     ap.add_argument("--no-exchange", action="store_true", help="render only: no gather copy, no shade")
+    ap.add_argument("--events", action="store_true", help="record timing events around every render, as bench.py")
     ap.add_argument("--opt", action="append", default=[], metavar="NAME=VALUE", help="pool option, e.g. chain=1")
     a = ap.parse_args()
 
@@ -88,7 +89,12 @@ def main():
                     s_, f_ = streams[k % nf], sfs[k % nf]
                     pool.set_stream(s_)
                     with torch.cuda.stream(s_):
+                        if a.events:
+                            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                            e0.record(s_)
                         f_.render_local(cams)
+                        if a.events:
+                            e1.record(s_)
                         if not a.no_exchange:
                             f_.exchange()
                 torch.cuda.synchronize()
@@ -97,7 +103,7 @@ def main():
             run(5)
             wins = [run(a.steps) for _ in range(a.windows)]
             sus = [run(a.sustain_steps) for _ in range(3)]
-            row = {"world": world, "frame": f"{W}x{H}", "inflight": nf, "opts": opts, "exchange": not a.no_exchange, "rays_per_step_rank": rays_rank,
+            row = {"world": world, "frame": f"{W}x{H}", "inflight": nf, "opts": opts, "exchange": not a.no_exchange, "events": a.events, "rays_per_step_rank": rays_rank,
                    "slice_rows": rows,
                    "ms_per_step_20": round(statistics.median(wins) / a.steps * 1e3, 4),
                    "mrays_s_rank_20": round(rays_rank * a.steps / statistics.median(wins) / 1e6, 1),
