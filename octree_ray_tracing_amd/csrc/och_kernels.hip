@@ -601,6 +601,13 @@ struct ArraySource {
     {
         return get(wave_base + lane, o, d, out);
     }
+    // Arbitrary rays: no shortcut (see CameraSource::get_wave_culled).
+    __device__ __forceinline__ bool get_wave_culled(uint32_t wave_base, uint32_t lane, const DevPool &, bool,
+                                                    float *o, float *d, uint32_t &out, bool &miss) const
+    {
+        miss = false;
+        return get(wave_base + lane, o, d, out);
+    }
     // Refill: ray base + k, base wave-uniform, k < 64.
     __device__ __forceinline__ bool get_refill(uint32_t base, uint32_t k, float *o, float *d, uint32_t &out) const
     {
@@ -610,21 +617,65 @@ struct ArraySource {
 
 // tree_camera::update_position per pixel (ORT/test_och_h_octree.cpp:119-136):
 // products rounded, sums left to right, correctly rounded sqrt and divide.
-__device__ __forceinline__ void camera_ray(const och_camera &C, int col, int row, float *d)
+__device__ __forceinline__ void camera_rot(const och_camera &C, int col, int row, float &ru, float &rv, float &rw)
 {
     const float u = __fmul_rn(C.aspect, __fsub_rn(__fmul_rn(C.view_x, (float)col), 1.0F));
     const float v = __fsub_rn(__fmul_rn(C.view_y, (float)row), 1.0F);
     const float f = C.fov_factor;
     const float *m = C.rot;
-    const float ru = __fadd_rn(__fadd_rn(__fmul_rn(u, m[0]), __fmul_rn(v, m[1])), __fmul_rn(f, m[2]));
-    const float rv = __fadd_rn(__fadd_rn(__fmul_rn(u, m[3]), __fmul_rn(v, m[4])), __fmul_rn(f, m[5]));
-    const float rw = __fadd_rn(__fadd_rn(__fmul_rn(u, m[6]), __fmul_rn(v, m[7])), __fmul_rn(f, m[8]));
+    ru = __fadd_rn(__fadd_rn(__fmul_rn(u, m[0]), __fmul_rn(v, m[1])), __fmul_rn(f, m[2]));
+    rv = __fadd_rn(__fadd_rn(__fmul_rn(u, m[3]), __fmul_rn(v, m[4])), __fmul_rn(f, m[5]));
+    rw = __fadd_rn(__fadd_rn(__fmul_rn(u, m[6]), __fmul_rn(v, m[7])), __fmul_rn(f, m[8]));
+}
+
+// Proven sky before the ray is set up (OCH_OPT_CULL).  The
+// camera ray's direction is D * R per component, D = (rw, ru, -rv) and R the
+// rounded 1 / |D|, each product rounded.  The walk's t of a plane q on axis a
+// (ray_cull) is then (q - o_a) / D_a times a common factor 1 / R, times a
+// per-axis factor within 2^-11 of 1 (RCPPS's relative error 1.5 * 2^-12, the
+// roundings of d, b and the fma), plus a shift worth less than 2^-21 world
+// units of plane position (the roundings of b and of the reflected origin).
+// So with the box grown by 2^-16 on every side: if the ray leaves the grown
+// box behind it (far t < 0), or enters it after leaving it by a relative
+// margin of 2^-7, ray_cull's exact test is true for the real box and the ray
+// ends as the MISS -- decided here with an approximate reciprocal and no
+// correctly rounded divide or square root.  Same preconditions as ray_cull:
+// origin inside (1, 2)^3, no component below 2^-60 of the largest (so every
+// c_a is a normal float below 2^61).  Rays that fail the test take the full
+// setup and ray_cull decides them exactly.
+__device__ __forceinline__ bool camera_proven_miss(const och_camera &C, float ru, float rv, float rw, const DevPool &P)
+{
+    const float D[3] = {rw, ru, -rv};
+    const float dmax = fmaxf(fmaxf(fabsf(D[0]), fabsf(D[1])), fabsf(D[2]));
+    bool ok = dmax > 0x1p-100F;
+    float tn = -INFINITY, tf = INFINITY;
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        const float o = C.pos[a];
+        ok &= o > 1.0F && o < 2.0F && fabsf(D[a]) >= dmax * 0x1p-60F;
+        const float inv = __builtin_amdgcn_rcpf(D[a]);
+        const float t1 = (P.cull_lo[a] - 0x1p-16F - o) * inv, t2 = (P.cull_hi[a] + 0x1p-16F - o) * inv;
+        tn = fmaxf(tn, fminf(t1, t2));
+        tf = fminf(tf, fmaxf(t1, t2));
+    }
+    return ok && (tf < 0.0F || tn > tf * (1.0F + 0x1p-7F));
+}
+
+__device__ __forceinline__ void camera_ray_from(float ru, float rv, float rw, float *d)
+{
     const float mag2 = __fadd_rn(__fadd_rn(__fmul_rn(ru, ru), __fmul_rn(rv, rv)), __fmul_rn(rw, rw));
     // __builtin_sqrtf lowers to the correctly rounded expansion; __fsqrt_rn is a bare v_sqrt_f32 (1 ulp).
     const float rmag = __fdiv_rn(1.0F, __builtin_sqrtf(mag2));
     d[0] = __fmul_rn(rw, rmag);
     d[1] = __fmul_rn(ru, rmag);
     d[2] = __fmul_rn(-rv, rmag);
+}
+
+__device__ __forceinline__ void camera_ray(const och_camera &C, int col, int row, float *d)
+{
+    float ru, rv, rw;
+    camera_rot(C, col, row, ru, rv, rw);
+    camera_ray_from(ru, rv, rw, d);
 }
 
 // Pixel tile of one wave: kTileW x kTileH = 64 pixels.
@@ -705,15 +756,44 @@ struct CameraSource {
     // tile arithmetic, divisions included, to the scalar unit.
     __device__ __forceinline__ bool get_wave(uint32_t wave_base, uint32_t lane, float *o, float *d, uint32_t &out) const
     {
-        uint32_t view, tx, ty;
+        uint32_t view;
+        int col, srow, row;
+        if (!locate_wave(wave_base, lane, view, col, srow, row)) return false;
+        return finish(view, col, srow, row, o, d, out);
+    }
+    // get_wave, or miss = true without a ray when camera_proven_miss shows
+    // the ray ends as the MISS (cull: the launch may cull, OCH_OPT_CULL).
+    __device__ __forceinline__ bool get_wave_culled(uint32_t wave_base, uint32_t lane, const DevPool &P, bool cull,
+                                                    float *o, float *d, uint32_t &out, bool &miss) const
+    {
+        uint32_t view;
+        int col, srow, row;
+        miss = false;
+        if (!locate_wave(wave_base, lane, view, col, srow, row)) return false;
+        const och_camera &C = cam[view];
+        out = view * slice_pixels + (uint32_t)srow * (uint32_t)width + (uint32_t)col;
+        float ru, rv, rw;
+        camera_rot(C, col, row, ru, rv, rw);
+        if (cull && camera_proven_miss(C, ru, rv, rw, P)) {
+            miss = true;
+            return true;
+        }
+        o[0] = C.pos[0]; o[1] = C.pos[1]; o[2] = C.pos[2];
+        camera_ray_from(ru, rv, rw, d);
+        return true;
+    }
+    __device__ __forceinline__ bool locate_wave(uint32_t wave_base, uint32_t lane, uint32_t &view, int &col, int &srow,
+                                                int &row) const
+    {
+        uint32_t tx, ty;
         tile_of(__builtin_amdgcn_readfirstlane(wave_base), view, tx, ty);
         view = __builtin_amdgcn_readfirstlane(view);
         tx = __builtin_amdgcn_readfirstlane(tx);
         ty = __builtin_amdgcn_readfirstlane(ty);
-        const int col = (int)(tx * kTileW + lane % kTileW);
-        const int srow0 = (int)(ty * kTileH), srow = srow0 + (int)(lane / kTileW);
+        col = (int)(tx * kTileW + lane % kTileW);
+        const int srow0 = (int)(ty * kTileH);
+        srow = srow0 + (int)(lane / kTileW);
         if (col >= width || srow >= slice_rows) return false;
-        int row;
         if (row_chunk % (int)kTileH == 0) {                // the tile lies inside one row chunk
             const int chunk = __builtin_amdgcn_readfirstlane((int)by_row_chunk.div((uint32_t)srow0));
             row = (chunk * n_shards + shard) * row_chunk + (srow - chunk * row_chunk);
@@ -721,7 +801,7 @@ struct CameraSource {
             const int chunk = (int)by_row_chunk.div((uint32_t)srow);
             row = (chunk * n_shards + shard) * row_chunk + (srow - chunk * row_chunk);
         }
-        return finish(view, col, srow, row, o, d, out);
+        return row < height;
     }
     // Refill (k_trace_refill): ray base + k, base wave-uniform, k < 64.  The
     // rays span at most two tiles, A = base / 64 and A + 1, whose coordinates
@@ -966,11 +1046,17 @@ __global__ void k_trace_grid(DevPool P, Src S, Sink K, uint32_t xcd_group, const
     const uint32_t wave_base = blk * blockDim.x + (threadIdx.x & ~63u);
     float o[3], d[3];
     uint32_t out;
-    if (wave_base + lane < S.count() && S.get_wave(wave_base, lane, o, d, out)) {
-        Ray r;
-        ray_init<kPacked, kCount, true>(r, P, o, d, lds_stack + threadIdx.x, blockDim.x);
-        ray_run<kPacked, kCount>(r, P, blockDim.x, top);
-        K.put(out, ray_result<kPacked>(r, P));
+    bool miss;
+    if (wave_base + lane < S.count() &&
+        S.get_wave_culled(wave_base, lane, P, kCount ? P.cull == 2 : P.cull != 0, o, d, out, miss)) {
+        if (miss) {                                 // proven before setup: the MISS record, 0 PUSHes
+            K.put(out, Hit{OCH_EXIT, 0u, P.miss_bits, 0u});
+        } else {
+            Ray r;
+            ray_init<kPacked, kCount, true>(r, P, o, d, lds_stack + threadIdx.x, blockDim.x);
+            ray_run<kPacked, kCount>(r, P, blockDim.x, top);
+            K.put(out, ray_result<kPacked>(r, P));
+        }
     }
 #endif
     if (cost && threadIdx.x == 0) cost[blk] = (uint32_t)(__builtin_amdgcn_s_memtime() - c0);
@@ -999,18 +1085,24 @@ __global__ void k_trace_bounce(DevPool P, Src S, Sink K, int compact, const uint
     float o[3], d[3], o2[3], d2[3];
     uint32_t out = 0, payload = 0;
     bool want = false;
-    if (wave_base + (threadIdx.x & 63u) < S.count() && S.get_wave(wave_base, threadIdx.x & 63u, o, d, out)) {
-        Ray r;
-        ray_init<kPacked, kCount, true>(r, P, o, d, stack, nb);
-        ray_run<kPacked, kCount>(r, P, nb);
-        const Hit h1 = ray_result<kPacked>(r, P);
-        want = h1.dir < OCH_EXIT;
-        if (want) bounce_ray(o, d, h1, P.half_voxel, o2, d2);
-        payload = K.put_primary(out, h1, want);
-        if (want && !compact) {                                             // in place, no compaction
-            ray_init<kPacked, kCount, true>(r, P, o2, d2, stack, nb);
+    bool miss;
+    if (wave_base + (threadIdx.x & 63u) < S.count() &&
+        S.get_wave_culled(wave_base, threadIdx.x & 63u, P, kCount ? P.cull == 2 : P.cull != 0, o, d, out, miss)) {
+        if (miss) {                                 // proven before setup: the MISS, no secondary ray
+            K.put_primary(out, Hit{OCH_EXIT, 0u, P.miss_bits, 0u}, false);
+        } else {
+            Ray r;
+            ray_init<kPacked, kCount, true>(r, P, o, d, stack, nb);
             ray_run<kPacked, kCount>(r, P, nb);
-            K.put_secondary(out, payload, ray_result<kPacked>(r, P));
+            const Hit h1 = ray_result<kPacked>(r, P);
+            want = h1.dir < OCH_EXIT;
+            if (want) bounce_ray(o, d, h1, P.half_voxel, o2, d2);
+            payload = K.put_primary(out, h1, want);
+            if (want && !compact) {                                         // in place, no compaction
+                ray_init<kPacked, kCount, true>(r, P, o2, d2, stack, nb);
+                ray_run<kPacked, kCount>(r, P, nb);
+                K.put_secondary(out, payload, ray_result<kPacked>(r, P));
+            }
         }
     }
     if (!compact) {

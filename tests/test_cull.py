@@ -210,3 +210,49 @@ def test_cull_frames_identical(ort, O, gpu_device):
                 torch.cuda.synchronize()
                 assert_frames(sf.frames, want)
     pool.close()
+
+
+@pytest.mark.gpu
+def test_cull_camera_shortcut_grazing(ort, gpu_device):
+    """Camera frames skip ray setup for rays camera_proven_miss shows to miss
+    the voxels' box (och_kernels.hip).  Around a tight box,
+    from origins near it, in every direction, with wide and narrow fields of
+    view, the box's silhouette is full of rays that graze its faces, edges and
+    corners: frames with the cull on (shortcut + exact cull) equal the frames
+    of the full walk (cull off, itself pinned to the oracle above) code for
+    code, primary and config 5."""
+    import torch
+    depth = 8
+    rng = np.random.default_rng(11)
+    vox = [(int(x), int(y), int(z), int(rng.integers(1, 7)))
+           for x, y, z in rng.integers((100, 50, 200), (110, 53, 230), (120, 3))]
+    nodes, root = sparse_dag(depth, vox)
+    blo, bhi = ort.occupied_box(nodes, root, depth)
+    lo = 1 + np.array(blo) / 2.0 ** depth
+    hi = 1 + np.array(bhi) / 2.0 ** depth
+    pool = ort.HOctree(nodes, root, depth, device=0)
+    pool.set_palette(ort.VoxelData().get_colours())
+    pool.set_stream(torch.cuda.current_stream())
+    W, H = 192, 108
+    yaws = np.linspace(0, 2 * np.pi, 8, endpoint=False)
+    centre, size = (lo + hi) / 2, hi - lo
+    frames = {c: [] for c in (1, 0)}
+    for _ in range(6):
+        pos = np.clip(centre + size * rng.uniform(0.6, 3.0, 3) * rng.choice([-1, 1], 3), 1.001, 1.999)
+        for fov in (1.25, 0.3):
+            cams = [ort.camera(tuple(float(v) for v in pos), float(y), float(p), fov, W, H)
+                    for y in yaws for p in (-1.2, -0.4, 0.4, 1.2)]
+            for cull in (1, 0):
+                pool.set_option("cull", cull)
+                for bounce in (False, True):                # config 5 takes the shortcut too
+                    for i in range(0, len(cams), 8):
+                        out = torch.empty(8 * W * H, dtype=torch.uint8, device="cuda")
+                        pool.render_codes_views_dev(cams[i:i + 8], out, H, 0, 1, bounce)
+                        frames[cull].append(out)
+    torch.cuda.synchronize()
+    on, off = torch.cat(frames[1]), torch.cat(frames[0])
+    assert torch.equal(on, off)
+    # the box is in view: some of these rays hit it, most miss it
+    hit = ((off.cpu().numpy() & 0x7F) < 120).mean()
+    assert 0.001 < hit < 0.9
+    pool.close()
