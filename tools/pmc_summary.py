@@ -25,8 +25,10 @@ from pathlib import Path
 def family(name: str) -> str:
     if "CameraSource" in name and "Bounce" in name:
         return "k_render_bounce"
+    if "CameraSource" in name and "FrameSink" in name:
+        return "k_render_rgba"          # RGBA8 frames: the planning launch, render_views
     if "CameraSource" in name:
-        return "k_render"
+        return "k_render"               # indexed-colour codes: the bench's timed launches
     if "ArraySource" in name and "Bounce" in name:
         return "k_trace_bounce"
     if "ArraySource" in name:
