@@ -1324,9 +1324,12 @@ __global__ __launch_bounds__(256) void k_shade_unshard4(const uint8_t *__restric
     const int gchunk = row / row_chunk, within = row - gchunk * row_chunk;
     const int shard = gchunk % n_shards, lchunk = gchunk / n_shards;
     const size_t src = (((size_t)shard * n_views + view) * slice_rows + (size_t)lchunk * row_chunk + within) * width + col;
-    const uint32_t c = *reinterpret_cast<const uint32_t *>(gathered + src);
-    const uint4 px = make_uint4(lut[c & 0xFFu], lut[(c >> 8) & 0xFFu], lut[(c >> 16) & 0xFFu], lut[c >> 24]);
-    *reinterpret_cast<uint4 *>(frames + ((size_t)view * height + row) * width + col) = px;
+    // streaming accesses: the codes are read once and the frame is not read
+    // back here, so neither should evict the DAG's lines from L2 / MALL
+    const uint32_t c = __builtin_nontemporal_load(reinterpret_cast<const uint32_t *>(gathered + src));
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    const u32x4 px = {lut[c & 0xFFu], lut[(c >> 8) & 0xFFu], lut[(c >> 16) & 0xFFu], lut[c >> 24]};
+    __builtin_nontemporal_store(px, reinterpret_cast<u32x4 *>(frames + ((size_t)view * height + row) * width + col));
 }
 
 // Editor flush: `count` staged slots (8 words each, raw and optionally packed)
