@@ -35,6 +35,7 @@ of the last timed step -- primary and config 5 -- pixel for pixel (`parity`).
 from __future__ import annotations
 
 import argparse
+import gc
 import hashlib
 import json
 import math
@@ -325,6 +326,8 @@ def main():
                     help="render and exchange RGBA8 slices instead of 1-byte indexed-colour codes")
     ap.add_argument("--fresh-streams", action="store_true",
                     help="put every frame in flight on a new stream, none on the current stream")
+    ap.add_argument("--extra-windows", type=int, default=0,
+                    help="diagnostic: this many more warmup + timed windows after the first (reported, not value)")
     ap.add_argument("--inflight", type=int, default=3,
                     help="frames in flight: steps alternate over this many HIP streams, so one step's "
                          "slowest rays overlap the next step's bulk (1 = serialised)")
@@ -435,6 +438,10 @@ def main():
                       "bytes_per_ray": 12 + 12 + 4 * push_total / (n_px * len(cams))}
     del hd, hv, ht, hp, dirs
 
+    # timing events for every step of a window, created once, outside the timed region
+    ev_pool = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+               for _ in range(max(a.steps, 1))]
+
     def step(k, ev=None, bounce=False):
         """One step: render both views of this rank's rows, all-gather, unshard --
         on stream k % inflight, into that stream's own frame buffers."""
@@ -442,7 +449,8 @@ def main():
         pool.set_stream(s_)
         with torch.cuda.stream(s_):
             if ev is not None:
-                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                # event pairs are made before the timed region (ev_pool); recorded here
+                e0, e1 = ev_pool[len(ev) % len(ev_pool)]
                 e0.record(s_)
             f_.render_local(cams, bounce)
             if ev is not None:
@@ -450,20 +458,27 @@ def main():
                 ev.append((e0, e1))
             f_.exchange()
 
+    issue_s = []                           # host time to issue each timed window's steps
+
     def timed(n, bounce=False, ev=None):
         """n steps between barrier + synchronize; max over ranks of the wall time."""
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize()
+        gc_was = gc.isenabled()
+        gc.disable()                       # no collector pause inside the timed region (as timeit)
         t0 = time.perf_counter()
         for k in range(n):
             step(k, ev, bounce)
+        issue_s.append(time.perf_counter() - t0)
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize()
         el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
+        if gc_was:
+            gc.enable()
         if world > 1:
             coll(dist.all_reduce, el, op=dist.ReduceOp.MAX)
         return float(el.item())
@@ -486,6 +501,12 @@ def main():
     frames = a.steps * len(cams)
     total_rays = W * H * frames
     value = total_rays / elapsed / 1e6
+    host_issue_ms = round(issue_s[-1] * 1e3, 4)
+    extra = []
+    for _ in range(a.extra_windows):
+        for k in range(a.warmup):
+            step(k)
+        extra.append(round(total_rays / timed(a.steps, ev=[]) / 1e6, 1))
 
     # Sustained: >= a.sustain seconds of steps, three runs, median.
     sustained = None
@@ -557,6 +578,7 @@ def main():
     pmc, pmc_src = load_pmc("k_render", f"d{a.depth}_{W}x{H}_n{world}")
     roof = {"kernel": f"k_trace_grid<CameraSource,{'CodeSink' if indexed else 'FrameSink'}> (2 views per launch)",
             "kernel_ms": round(k_avg_ms, 4), "kernel_ms_serial": round(latency_ms, 4),
+            "host_issue_ms": host_issue_ms,
             "ms_per_step": round(step_s * 1e3, 4), "frames_in_flight": len(streams),
             "push_per_ray": round(push_total / rays_rank, 3), "rays_per_launch": rays_rank,
             "walked_push_per_ray": round(walk_push / rays_rank, 3), "culled_frac": round(culled / rays_rank, 4),
@@ -625,6 +647,7 @@ def main():
             "cpu_baseline": cpu,
             "parity": parity,
             "sustained": sustained,
+            **({"extra_windows": extra} if extra else {}),
             "trace_batch": trace_only,
             "bounce": bounce,
             "other_configs": others,
