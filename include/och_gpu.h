@@ -158,7 +158,8 @@ typedef enum och_option {
     OCH_OPT_CHUNK_TILES = 7,   /* schedule 2: 64-ray tiles per wave, a power of two in 1..64 (default 4) */
     OCH_OPT_CULL = 8           /* 1 (default) = a ray whose walk provably never enters the bounding box of the
                                   pool's voxels (och_pool_occupied_box) is recorded as the miss it would end in,
-                                  without walking; exact, for launches that do not count
+                                  without walking (camera rays: a cheaper conservative test first, before the
+                                  ray's setup); exact, for launches that do not count
                                   PUSHes.  0 = every ray walks.  2 = diagnostic: launches that count PUSHes
                                   cull too, a culled ray counting 0 (the PUSHes the culled launch walks) */
 } och_option;
