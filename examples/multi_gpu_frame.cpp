@@ -19,9 +19,10 @@ int main(int argc, char **argv)
     const int depth = argc > 1 ? std::atoi(argv[1]) : 12;
     const int W = argc > 2 ? std::atoi(argv[2]) : 3840, H = argc > 3 ? std::atoi(argv[3]) : 2160;
     const char *path = argc > 4 ? argv[4] : "multi_gpu_frame.ppm";
-    int n = 0;
-    och_device_count(&n);
-    if (argc > 5) n = std::atoi(argv[5]);
+    // the gfx950 devices by HIP index: a node may list other devices too
+    const std::vector<int> gfx950 = och::gpu::devices();
+    int n = (int)gfx950.size();
+    if (argc > 5 && std::atoi(argv[5]) < n) n = std::atoi(argv[5]);
     const int frames = argc > 6 ? std::atoi(argv[6]) : 10;
     const int view = argc > 7 ? std::atoi(argv[7]) : 1;
     if (n < 1) {
@@ -33,8 +34,7 @@ int main(int argc, char **argv)
     och::gpu::check(och_build_terrain(&tp, &hp), "och_build_terrain");
     int rc = 0;
     try {
-        std::vector<int> devices(n);
-        for (int i = 0; i < n; ++i) devices[i] = i;
+        const std::vector<int> devices(gfx950.begin(), gfx950.begin() + n);
         och::gpu::frame_group group(devices, hp.nodes, hp.n_nodes, hp.root, hp.depth);
         group.set_palette(examples::reference_palette());
         std::vector<och_camera> cams;

@@ -97,6 +97,9 @@ typedef struct och_pool_info {
 OCH_API int och_abi_version(void);
 OCH_API const char *och_last_error(void);      /* thread-local message of the last failure */
 OCH_API int och_device_count(int *count);       /* visible gfx950 devices */
+/* HIP indices of the visible gfx950 devices, in HIP order: up to capacity of
+ * them into devices[], their total into *count. */
+OCH_API int och_device_list(int *devices, int capacity, int *count);
 
 /* ------------------------------------------------------------ RCPPS model */
 /* Capture this host CPU's _mm_rcp_ps (the reference's reciprocal,
@@ -108,6 +111,11 @@ OCH_API int och_device_count(int *count);       /* visible gfx950 devices */
 OCH_API int och_host_rcp_lut(uint32_t *lut, int *log2_entries);
 /* Same model evaluated on the host, for a single input bit pattern. */
 OCH_API uint32_t och_rcp_from_lut(uint32_t xbits, const uint32_t *lut, int log2_entries);
+/* Largest relative error |r * x - 1| of a table over x in [-2, -1).  A pool
+ * whose table exceeds 2^-10 (x86 RCPPS: within 1.5 * 2^-12) does not use the
+ * cull's approximate camera test, only its exact per-ray test (OCH_OPT_CULL),
+ * so records stay the reference's under any table. */
+OCH_API int och_rcp_lut_error(const uint32_t *lut, int log2_entries, double *max_rel_error);
 
 /* ------------------------------------------------------------ node pools */
 /* Upload a node pool.  nodes = n_nodes x 8 uint32 child slots exactly as the
@@ -276,7 +284,7 @@ OCH_API int och_gpu_shade_unshard_views_dev(och_gpu_pool *pool, const uint8_t *g
  * would write, bit for bit.  Slices travel as 1-byte colour codes when the
  * palette has at most OCH_CODE_MAX_VOXELS ids, as RGBA8 otherwise.  RCCL is
  * loaded on first use (dlopen; an RCCL already in the process is reused);
- * OCH_E_NODEV when it cannot be.  devices = NULL means 0..n_devices-1.
+ * OCH_E_NODEV when it cannot be.  devices = NULL means the first n_devices gfx950 devices (och_device_list).
  * Replaces the per-pixel loop of ORT/test_och_h_octree.cpp:437-457 across GPUs. */
 typedef struct och_frame_group och_frame_group;
 OCH_API int och_frame_group_create(const int *devices, int n_devices, const uint32_t *nodes, uint32_t n_nodes,
@@ -391,8 +399,10 @@ OCH_API int och_editor_nodes(const och_editor *editor, const uint32_t **nodes, u
  * windowed upload; any other pool (a new one, one another editor or
  * och_gpu_pool_update wrote, or one a failed flush left behind) is written
  * whole, its packed layout replaced by one numbered like the slots.  The root
- * is published after every slot it reaches, so a failed flush leaves the pool
- * tracing its previous tree. */
+ * is published after every slot it reaches.  A flush that fails after it
+ * began writing leaves slots half written (slots are reused in place), so it
+ * marks the pool torn: traces, renders and och_gpu_pool_update on it return
+ * OCH_E_INVALID until a later flush of this editor succeeds. */
 OCH_API int och_editor_flush(och_editor *editor, och_gpu_pool *pool);
 
 #ifdef __cplusplus

@@ -32,6 +32,16 @@ inline void check(int status, const char *what)
     if (status != OCH_OK) throw error(status, std::string(what) + ": " + och_last_error());
 }
 
+// HIP indices of the visible gfx950 devices (och_device_list).
+inline std::vector<int> devices()
+{
+    int n = 0;
+    check(och_device_list(nullptr, 0, &n), "och_device_list");
+    std::vector<int> d(n);
+    if (n) check(och_device_list(d.data(), n, &n), "och_device_list");
+    return d;
+}
+
 struct float3 {
     float x, y, z;
 };

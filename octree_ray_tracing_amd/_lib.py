@@ -62,8 +62,10 @@ PROTOTYPES = {
     "och_abi_version": (C.c_int, []),
     "och_last_error": (C.c_char_p, []),
     "och_device_count": (C.c_int, [C.POINTER(C.c_int)]),
+    "och_device_list": (C.c_int, [_P, C.c_int, C.POINTER(C.c_int)]),
     "och_host_rcp_lut": (C.c_int, [_P, C.POINTER(C.c_int)]),
     "och_rcp_from_lut": (_u32, [_u32, _P, C.c_int]),
+    "och_rcp_lut_error": (C.c_int, [_P, C.c_int, C.POINTER(C.c_double)]),
     "och_gpu_pool_create": (C.c_int, [_P, _u32, _u32, C.c_int, C.c_int, _f32, C.c_int, C.POINTER(_P)]),
     "och_gpu_pool_destroy": (C.c_int, [_P]),
     "och_gpu_pool_info": (C.c_int, [_P, C.POINTER(PoolInfo)]),

@@ -126,6 +126,7 @@ struct och_gpu_pool {
     float miss_t = INFINITY;
     uint32_t *d_lut = nullptr;
     int lut_log2 = 0;
+    double lut_error = INFINITY;    // maximum relative error of the table (lut_max_rel_error)
     uint32_t *d_palette = nullptr;
     uint32_t n_voxels = 0;
     uint32_t *d_code_table = nullptr;   // OCH_CODE_* -> RGBA8 (256 words), when n_voxels <= OCH_CODE_MAX_VOXELS
@@ -150,6 +151,7 @@ struct och_gpu_pool {
     bool packed_by_slot = false;    // d_packed numbered like d_nodes (editor flushes)
     uint64_t serial = 0;            // process-unique, never reused (och::pool_serial)
     uint64_t last_writer = 0;       // editor id of the last och::pool_commit, 0 otherwise
+    bool torn = false;              // a failed editor flush left the slots half written (och::pool_mark_torn)
     int opt_layout = 1;
     int opt_tile_order = 0;
     int opt_bounce_compact = 1;
@@ -210,6 +212,7 @@ struct och_gpu_pool {
         p.dim_span = (1u << 22) - p.dim_lo;
         // 1 + k / 2^depth is an exact float for depth <= 22
         p.cull = box_any ? opt_cull : 0;
+        p.cam_cull = lut_error <= och::kCameraCullRcpError ? 1 : 0;
         for (int a = 0; a < 3; ++a) {
             p.cull_lo[a] = 1.0F + std::ldexp((float)box_lo[a], -depth);
             p.cull_hi[a] = 1.0F + std::ldexp((float)box_hi[a], -depth);
@@ -228,6 +231,16 @@ int ensure_scratch(och_gpu_pool *p, size_t bytes)
     p->scratch_bytes = 0;
     OCH_HIP(hipMalloc(&p->d_scratch, bytes));
     p->scratch_bytes = bytes;
+    return OCH_OK;
+}
+
+// Launches refuse a pool that a failed editor flush left half written: its
+// slots may name nodes that were never uploaded.
+int check_ready(const och_gpu_pool *p)
+{
+    if (p->torn)
+        return fail(OCH_E_INVALID, "pool left half written by a failed och_editor_flush: flush the editor again");
+    if (!p->d_lut) return fail(OCH_E_RCP_MODEL, "no RCPPS table on this pool (call och_gpu_set_rcp_lut)");
     return OCH_OK;
 }
 
@@ -424,6 +437,23 @@ int upload_packed(och_gpu_pool *p, const uint32_t *nodes, uint32_t n_nodes)
     return OCH_OK;
 }
 
+// Largest relative error |r * x - 1| of the table model over x in [-2, -1):
+// entry k serves the mantissa bin [k, k + 1) / 2^L, so the extremes are at
+// the bin's ends.  Non-finite or zero entries count as an infinite error.
+double lut_max_rel_error(const uint32_t *lut, int log2_entries)
+{
+    const uint32_t n = 1u << log2_entries;
+    double worst = 0.0;
+    for (uint32_t k = 0; k < n; ++k) {
+        float r;
+        std::memcpy(&r, &lut[k], 4);
+        if (!std::isfinite(r) || r == 0.0F) return INFINITY;
+        const double lo = -(1.0 + (double)k / n), hi = -(1.0 + (double)(k + 1) / n);
+        worst = std::max({worst, std::fabs((double)r * lo - 1.0), std::fabs((double)r * hi - 1.0)});
+    }
+    return worst;
+}
+
 int upload_lut(och_gpu_pool *p, const uint32_t *lut, int log2_entries)
 {
     if (!lut || log2_entries < 1 || log2_entries > 23) return fail(OCH_E_INVALID, "bad RCPPS table");
@@ -433,6 +463,9 @@ int upload_lut(och_gpu_pool *p, const uint32_t *lut, int log2_entries)
     OCH_HIP(hipMalloc(&p->d_lut, bytes));
     OCH_HIP(hipMemcpy(p->d_lut, lut, bytes, hipMemcpyHostToDevice));
     p->lut_log2 = log2_entries;
+    // camera_proven_miss budgets the table's error; a coarser table leaves
+    // every camera ray to the exact ray_cull
+    p->lut_error = lut_max_rel_error(lut, log2_entries);
     return OCH_OK;
 }
 
@@ -444,19 +477,27 @@ OCH_API int och_abi_version(void) { return OCH_GPU_ABI_VERSION; }
 
 OCH_API const char *och_last_error(void) { return g_error.c_str(); }
 
-OCH_API int och_device_count(int *count)
+OCH_API int och_device_list(int *devices, int capacity, int *count)
 {
-    if (!count) return fail(OCH_E_INVALID, "count is NULL");
+    if (!count || (capacity > 0 && !devices)) return fail(OCH_E_INVALID, "NULL argument");
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess) n = 0;
     int gfx950 = 0;
     for (int i = 0; i < n; ++i) {
         hipDeviceProp_t prop;
-        if (hipGetDeviceProperties(&prop, i) == hipSuccess && std::strncmp(prop.gcnArchName, "gfx950", 6) == 0)
+        if (hipGetDeviceProperties(&prop, i) == hipSuccess && std::strncmp(prop.gcnArchName, "gfx950", 6) == 0) {
+            if (gfx950 < capacity) devices[gfx950] = i;
             ++gfx950;
+        }
     }
     *count = gfx950;
     return OCH_OK;
+}
+
+OCH_API int och_device_count(int *count)
+{
+    if (!count) return fail(OCH_E_INVALID, "count is NULL");
+    return och_device_list(nullptr, 0, count);
 }
 
 OCH_API uint32_t och_rcp_from_lut(uint32_t x, const uint32_t *lut, int log2_entries)
@@ -467,6 +508,13 @@ OCH_API uint32_t och_rcp_from_lut(uint32_t x, const uint32_t *lut, int log2_entr
     const uint32_t ent = lut[(x & 0x7FFFFFu) >> (23 - log2_entries)];
     const int ne = (int)((ent >> 23) & 0xFFu) + 127 - (int)e;
     return ne <= 0 ? sign : (sign | ((uint32_t)ne << 23) | (ent & 0x7FFFFFu));
+}
+
+OCH_API int och_rcp_lut_error(const uint32_t *lut, int log2_entries, double *max_rel_error)
+{
+    if (!lut || !max_rel_error || log2_entries < 1 || log2_entries > 23) return fail(OCH_E_INVALID, "bad RCPPS table");
+    *max_rel_error = lut_max_rel_error(lut, log2_entries);
+    return OCH_OK;
 }
 
 OCH_API int och_host_rcp_lut(uint32_t *lut, int *log2_entries)
@@ -573,6 +621,7 @@ OCH_API int och_gpu_pool_info(const och_gpu_pool *p, och_pool_info *info)
 OCH_API int och_gpu_pool_update(och_gpu_pool *p, uint32_t first, uint32_t count, const uint32_t *nodes, uint32_t root)
 {
     if (!p || (count && !nodes)) return fail(OCH_E_INVALID, "pool/nodes is NULL");
+    if (p->torn) return fail(OCH_E_INVALID, "pool left half written by a failed och_editor_flush: flush the editor again");
     const uint32_t n_user = p->n_nodes - (uint32_t)p->index_base;
     const uint32_t lo = p->index_base == 1 ? 1u : 0u;
     if (count && (first < lo || (uint64_t)first - lo + count > n_user))
@@ -588,6 +637,10 @@ OCH_API int och_gpu_pool_update(och_gpu_pool *p, uint32_t first, uint32_t count,
         std::memcpy(p->mirror.data() + off, saved.data(), saved.size() * 4);
         return st;
     }
+    // slots are rewritten in place: kernels of frames in flight on any stream
+    // may still walk them (as the editor's flush)
+    int ds = och::pool_drain(p);
+    if (ds != OCH_OK) return ds;
     DeviceGuard g(p->device);
     if (count)
         OCH_HIP(hipMemcpyAsync(p->d_nodes + 8 * (size_t)(first - lo + p->index_base), p->mirror.data() + off,
@@ -715,6 +768,24 @@ int och::pool_commit(och_gpu_pool *p, uint32_t root, uint32_t packed_root, bool 
         p->box_hi[a] = p->box_any ? box_hi[a] : 0;
     }
     p->last_writer = writer;
+    p->torn = false;
+    return OCH_OK;
+}
+
+int och::pool_mark_torn(och_gpu_pool *p)
+{
+    if (!p) return OCH_E_INVALID;
+    DeviceGuard g(p->device);
+    (void)hipDeviceSynchronize();
+    if (p->d_packed) (void)hipFree(p->d_packed);
+    p->d_packed = nullptr;
+    p->packed_nodes = 0;
+    p->packed_by_slot = false;
+    p->packed_root = 0;
+    p->root = 0;
+    p->box_any = false;
+    p->last_writer = 0;
+    p->torn = true;
     return OCH_OK;
 }
 
@@ -870,7 +941,7 @@ OCH_API int och_gpu_trace_batch_dev(och_gpu_pool *p, const float *origin, int or
     if (!p || (n && (!origin || !dirs || !hit_dir || !hit_voxel || !hit_time)))
         return fail(OCH_E_INVALID, "NULL argument");
     if (origin_stride != 0 && origin_stride != 3) return fail(OCH_E_INVALID, "origin_stride must be 0 or 3");
-    if (!p->d_lut) return fail(OCH_E_RCP_MODEL, "no RCPPS table on this pool (call och_gpu_set_rcp_lut)");
+    if (int rs = check_ready(p)) return rs;
     DeviceGuard g(p->device);
     OCH_HIP(hipEventRecord(p->ev_start, p->stream()));
     OCH_HIP(och::launch_trace_batch(p->dev(), origin, origin_stride, dirs, n, hit_dir, hit_voxel,
@@ -889,7 +960,7 @@ OCH_API int och_gpu_trace_bounce_batch_dev(och_gpu_pool *p, const float *origin,
                      !bounce_time)))
         return fail(OCH_E_INVALID, "NULL argument");
     if (origin_stride != 0 && origin_stride != 3) return fail(OCH_E_INVALID, "origin_stride must be 0 or 3");
-    if (!p->d_lut) return fail(OCH_E_RCP_MODEL, "no RCPPS table on this pool (call och_gpu_set_rcp_lut)");
+    if (int rs = check_ready(p)) return rs;
     DeviceGuard g(p->device);
     OCH_HIP(hipEventRecord(p->ev_start, p->stream()));
     OCH_HIP(och::launch_trace_bounce_batch(p->dev(), origin, origin_stride, dirs, n, hit_dir, hit_voxel,
@@ -1002,7 +1073,7 @@ int render_views(och_gpu_pool *p, const och_camera *cams, int n_views, uint32_t 
             return fail(OCH_E_INVALID, "views must share one positive width and height");
     if ((uint64_t)cams[0].width * cams[0].height * n_views >= (1ull << 32))
         return fail(OCH_E_INVALID, "frame too large");
-    if (!p->d_lut) return fail(OCH_E_RCP_MODEL, "no RCPPS table on this pool (call och_gpu_set_rcp_lut)");
+    if (int rs = check_ready(p)) return rs;
     DeviceGuard g(p->device);
     och::DevFrame f;
     for (int v = 0; v < n_views; ++v) f.cams[v] = cams[v];
@@ -1043,7 +1114,7 @@ OCH_API int och_gpu_plan_views(och_gpu_pool *p, const och_camera *cams, int n_vi
     if (!p || !cams) return fail(OCH_E_INVALID, "NULL argument");
     if (n_views < 1 || n_views > OCH_MAX_VIEWS || row_chunk <= 0 || n_shards <= 0 || shard < 0 || shard >= n_shards)
         return fail(OCH_E_INVALID, "bad plan arguments");
-    if (!p->d_lut) return fail(OCH_E_RCP_MODEL, "no RCPPS table on this pool (call och_gpu_set_rcp_lut)");
+    if (int rs = check_ready(p)) return rs;
     DeviceGuard g(p->device);
     // One planning render per kernel (primary grid, config-5 bounce) into
     // scratch in natural order, timing every workgroup.

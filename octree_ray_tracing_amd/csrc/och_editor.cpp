@@ -471,6 +471,7 @@ OCH_API int och_editor_flush(och_editor *e, och_gpu_pool *pool)
     const bool windowed = e->synced == och::pool_serial(pool) && och::pool_last_writer(pool) == e->id;
     if (windowed && e->dirty.empty() && !e->root_dirty) return OCH_OK;
     st = och::pool_drain(pool);
+    const bool drained = st == OCH_OK;
     if (st == OCH_OK && !windowed) {
         // both layouts whole, packed in slot numbering
         std::vector<uint32_t> raw((size_t)(e->capacity + 1) * 8, 0u);
@@ -495,6 +496,8 @@ OCH_API int och_editor_flush(och_editor *e, och_gpu_pool *pool)
                               e->box_any ? e->box_hi : nullptr);
     if (st != OCH_OK) {
         e->synced = 0;   // the next flush rewrites the pool whole
+        // slots may be half written: no launch may walk the pool until then
+        if (drained) (void)och::pool_mark_torn(pool);
         return st;
     }
     e->synced = och::pool_serial(pool);

@@ -156,8 +156,16 @@ OCH_API int och_frame_group_create(const int *devices, int n_devices, const uint
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return group_fail(OCH_E_NODEV, "no HIP device visible");
     std::vector<int> devs(n_devices);
+    if (!devices) {                          // the first n_devices gfx950 devices, in HIP order
+        std::vector<int> all(ndev);
+        int n950 = 0;
+        if (och_device_list(all.data(), ndev, &n950) != OCH_OK || n950 < n_devices)
+            return group_fail(OCH_E_NODEV, std::to_string(n_devices) + " gfx950 devices asked, " +
+                                               std::to_string(n950) + " visible");
+        for (int r = 0; r < n_devices; ++r) devs[r] = all[r];
+    }
     for (int r = 0; r < n_devices; ++r) {
-        devs[r] = devices ? devices[r] : r;
+        if (devices) devs[r] = devices[r];
         if (devs[r] < 0 || devs[r] >= ndev) return group_fail(OCH_E_NODEV, "device " + std::to_string(devs[r]) + " not visible");
         for (int q = 0; q < r; ++q)
             if (devs[q] == devs[r]) return group_fail(OCH_E_INVALID, "a device appears twice in the group");

@@ -34,7 +34,16 @@ struct DevPool {
     // box of the pool's voxels, world coordinates (1 + voxel / 2^depth).
     int32_t cull;           // 0 off, 1 launches without PUSH counts, 2 all launches
     float cull_lo[3], cull_hi[3];
+    // camera_proven_miss (the cull's cheaper test before a camera ray's setup)
+    // budgets the RCPPS table's relative error: 1 only when the uploaded
+    // table's maximum error is within kCameraCullRcpError (och_api.cpp).
+    int32_t cam_cull;
 };
+
+// Largest RCPPS-table relative error for which camera_proven_miss is sound
+// (och_kernels.hip has the budget: per-axis factors within 2^-9 of 1 against
+// its 2^-7 margin); x86 RCPPS is specified within 1.5 * 2^-12.
+constexpr double kCameraCullRcpError = 0x1p-10;
 
 // Bounding box of the reachable non-empty leaf voxels, voxel units, [lo, hi)
 // per axis; false when there are none (och_pool_occupied_box).
@@ -50,8 +59,9 @@ bool occupied_box(const uint32_t *nodes, uint32_t n_nodes, uint32_t root, int de
 //                       one level per slot and ids below 2^24).  `full`
 //                       replaces the packed buffer (count must then cover
 //                       slots 0..n_nodes-1 and raw/packed start at slot 0).
-//                       Roots are not touched, so a failed flush leaves the
-//                       pool tracing its old tree;
+//                       Roots are not touched; a failed write may leave
+//                       slots half written, so the flush then marks the
+//                       pool torn (pool_mark_torn);
 //   pool_commit      -- publishes both roots (packed == false drops the packed
 //                       layout) and the editor's voxel bounding box (the cull
 //                       box, OCH_OPT_CULL), and records `writer` as the pool's
@@ -70,6 +80,12 @@ int pool_write_slots(och_gpu_pool *pool, uint32_t first, uint32_t count, const u
 // nullptr when it holds none.
 int pool_commit(och_gpu_pool *pool, uint32_t root, uint32_t packed_root, bool packed, uint64_t writer,
                 const int32_t *box_lo, const int32_t *box_hi);
+// After a failed pool_write_slots / pool_scatter_slots: the slots may be half
+// written (a freed-and-reused slot rewritten in place, or the packed buffer
+// reallocated before its copy failed).  Drops the packed layout, sets root 0,
+// clears the cull box and marks the pool torn: trace / render launches and
+// och_gpu_pool_update refuse it until a pool_commit (a successful flush).
+int pool_mark_torn(och_gpu_pool *pool);
 // pool_write_slots for scattered slots: ids[count] (1..n_nodes-1, distinct),
 // raw / packed = count x 8 words; one staged copy and one scatter kernel,
 // complete on return.

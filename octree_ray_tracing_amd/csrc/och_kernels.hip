@@ -632,17 +632,21 @@ __device__ __forceinline__ void camera_rot(const och_camera &C, int col, int row
 // camera ray's direction is D * R per component, D = (rw, ru, -rv) and R the
 // rounded 1 / |D|, each product rounded.  The walk's t of a plane q on axis a
 // (ray_cull) is then (q - o_a) / D_a times a common factor 1 / R, times a
-// per-axis factor within 2^-11 of 1 (RCPPS's relative error 1.5 * 2^-12, the
-// roundings of d, b and the fma), plus a shift worth less than 2^-21 world
-// units of plane position (the roundings of b and of the reflected origin).
-// So with the box grown by 2^-16 on every side: if the ray leaves the grown
-// box behind it (far t < 0), or enters it after leaving it by a relative
-// margin of 2^-7, ray_cull's exact test is true for the real box and the ray
-// ends as the MISS -- decided here with an approximate reciprocal and no
-// correctly rounded divide or square root.  Same preconditions as ray_cull:
-// origin inside (1, 2)^3, no component below 2^-60 of the largest (so every
-// c_a is a normal float below 2^61).  Rays that fail the test take the full
-// setup and ray_cull decides them exactly.
+// per-axis factor within 2^-9 of 1 (the RCPPS table's relative error, at
+// most kCameraCullRcpError = 2^-10 -- x86 RCPPS: 1.5 * 2^-12 -- plus the
+// roundings of d, b and the fma, a few 2^-24), plus a shift worth less than
+// 2^-21 world units of plane position (the roundings of b and of the
+// reflected origin).  So with the box grown by 2^-16 on every side: if the
+// ray leaves the grown box behind it (far t < 0), or enters it after leaving
+// it by a relative margin of 2^-7 (> (1 + 2^-9) / (1 - 2^-9) - 1 with room for
+// this test's own roundings), ray_cull's exact test is true for the real box
+// and the ray ends as the MISS -- decided here with an approximate
+// reciprocal and no correctly rounded divide or square root.  A pool whose
+// table exceeds the bound (P.cam_cull = 0, och_api.cpp upload_lut) skips
+// this test and leaves every ray to ray_cull.  Same preconditions as
+// ray_cull: origin inside (1, 2)^3, no component below 2^-60 of the largest
+// (so every c_a is a normal float below 2^61).  Rays that fail the test take
+// the full setup and ray_cull decides them exactly.
 __device__ __forceinline__ bool camera_proven_miss(const och_camera &C, float ru, float rv, float rw, const DevPool &P)
 {
     const float D[3] = {rw, ru, -rv};
@@ -774,7 +778,7 @@ struct CameraSource {
         out = view * slice_pixels + (uint32_t)srow * (uint32_t)width + (uint32_t)col;
         float ru, rv, rw;
         camera_rot(C, col, row, ru, rv, rw);
-        if (cull && camera_proven_miss(C, ru, rv, rw, P)) {
+        if (cull && P.cam_cull && camera_proven_miss(C, ru, rv, rw, P)) {
             miss = true;
             return true;
         }

@@ -155,6 +155,8 @@ class FrameGroup:
 
     def set_palette(self, rgba: np.ndarray):
         rgba = np.ascontiguousarray(rgba, np.uint32).reshape(-1)
+        if rgba.size % 6:
+            raise ValueError("palette must hold 6 colours per voxel id")
         call("och_frame_group_set_palette", self._h, rgba.ctypes.data, rgba.size // 6)
 
     def set_option(self, name: str, value: int):

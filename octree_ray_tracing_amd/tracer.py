@@ -63,6 +63,14 @@ def rcp_from_lut(xbits: int, lut: np.ndarray) -> int:
     return call("och_rcp_from_lut", xbits, _np_ptr(lut), int(round(math.log2(lut.size))))
 
 
+def rcp_lut_error(lut: np.ndarray) -> float:
+    """Largest relative error of an RCPPS table over [-2, -1) (och_rcp_lut_error)."""
+    lut = np.ascontiguousarray(lut, np.uint32)
+    e = C.c_double()
+    call("och_rcp_lut_error", _np_ptr(lut), int(round(math.log2(lut.size))), C.byref(e))
+    return e.value
+
+
 def device_count() -> int:
     n = C.c_int()
     call("och_device_count", C.byref(n))

@@ -791,6 +791,162 @@ ORA_API void ora_href_fill_terrain(ora_href *T, int tunnels)
     free(h);
 }
 
+/* ------------------------------------- och::octree's table, restated exactly */
+
+/* och::octree (ORT/och_octree.h:10-69, ORT/och_octree.cpp:14-160): a
+ * capacity-sized table of 8 x u32 nodes, the root fixed at index 0, children
+ * 0-based (0 = empty), a free list threaded through children[0] of the free
+ * nodes (create_table :21-34, alloc :46-63, dealloc :65-72).  set() allocates
+ * the missing path and writes the voxel, 0 included (:74-91), so set(..., 0)
+ * leaves allocated empty nodes reachable; unset() clears the voxel and
+ * deallocates the nodes it empties, bottom-up (:93-139) -- the root too,
+ * which then gets the free list's head written into its children[0] and
+ * leaves head = 0.  The reference exit(0)s when alloc() finds head == 0
+ * (:50-54); here that sets `overflow` and the edit stops. */
+typedef struct ora_oref {
+    int depth, dim;
+    uint32_t cap;
+    uint32_t *nodes;                 /* cap x 8 */
+    uint32_t head;                   /* och_octree.h:27 */
+    int node_cnt;                    /* och_octree.h:28, OCH_IF_DEBUG counter */
+    int overflow;
+} ora_oref;
+
+ORA_API ora_oref *ora_oref_new(int depth, uint32_t capacity)          /* :14, create_table :21-34 */
+{
+    if (capacity < 2) return NULL;
+    ora_oref *T = (ora_oref *)calloc(1, sizeof *T);
+    T->depth = depth; T->dim = 1 << depth; T->cap = capacity;
+    T->nodes = (uint32_t *)calloc((size_t)capacity * 8, 4);
+    for (uint32_t i = 1; i != capacity; ++i) T->nodes[(size_t)i * 8] = i + 1;
+    T->nodes[(size_t)(capacity - 1) * 8] = 0;
+    T->head = 1;
+    T->node_cnt = 1;
+    return T;
+}
+
+ORA_API void ora_oref_free(ora_oref *T)
+{
+    if (!T) return;
+    free(T->nodes); free(T);
+}
+
+static uint32_t oref_alloc(ora_oref *T)                               /* :46-63 */
+{
+    ++T->node_cnt;
+    if (!T->head) { T->overflow = 1; return 0; }                     /* "Too many allocations", exit(0) */
+    const uint32_t old = T->head;
+    T->head = T->nodes[(size_t)old * 8];
+    memset(T->nodes + (size_t)old * 8, 0, 32);
+    return old;
+}
+
+static void oref_dealloc(ora_oref *T, uint32_t idx)                   /* :65-72 */
+{
+    --T->node_cnt;
+    T->nodes[(size_t)idx * 8] = T->head;
+    T->head = idx;
+}
+
+static int oref_is_empty(const ora_oref *T, uint32_t idx)             /* :41-44 */
+{
+    const uint32_t *c = T->nodes + (size_t)idx * 8;
+    for (int k = 0; k < 8; ++k) if (c[k]) return 0;
+    return 1;
+}
+
+/* The child digit of level i of z_encode_16(x, y, z) (ORT/och_z_order.cpp:191-196). */
+static inline int oref_digit(int x, int y, int z, int i)
+{
+    return ((x >> i) & 1) | (((y >> i) & 1) << 1) | (((z >> i) & 1) << 2);
+}
+
+ORA_API void ora_oref_set(ora_oref *T, int x, int y, int z, uint32_t vx)   /* :74-91 */
+{
+    if (T->overflow) return;
+    uint32_t curr = 0;                                                /* root */
+    for (int i = T->depth - 1; i != 0; --i) {
+        const int k = oref_digit(x, y, z, i);
+        if (!T->nodes[(size_t)curr * 8 + k]) {
+            const uint32_t n = oref_alloc(T);
+            if (T->overflow) return;
+            T->nodes[(size_t)curr * 8 + k] = n;
+        }
+        curr = T->nodes[(size_t)curr * 8 + k];
+    }
+    T->nodes[(size_t)curr * 8 + oref_digit(x, y, z, 0)] = vx;
+}
+
+ORA_API void ora_oref_unset(ora_oref *T, int x, int y, int z)         /* :93-139 */
+{
+    if (T->overflow) return;
+    uint32_t curr = 0, stack[32];
+    int sptr = 0;
+    for (int i = T->depth - 1; i != 0; --i) {
+        const uint32_t child = T->nodes[(size_t)curr * 8 + oref_digit(x, y, z, i)];
+        if (!child) return;
+        stack[sptr++] = curr;
+        curr = child;
+    }
+    T->nodes[(size_t)curr * 8 + oref_digit(x, y, z, 0)] = 0;
+    if (oref_is_empty(T, curr)) oref_dealloc(T, curr);
+    else return;
+    for (int i = 1; i != T->depth; ++i) {
+        --sptr;
+        T->nodes[(size_t)stack[sptr] * 8 + oref_digit(x, y, z, i)] = 0;
+        if (oref_is_empty(T, stack[sptr])) oref_dealloc(T, stack[sptr]);   /* the root too: dealloc(0) */
+        else return;
+    }
+}
+
+ORA_API uint32_t ora_oref_at(const ora_oref *T, int x, int y, int z)  /* :141-160 */
+{
+    uint32_t curr = 0;
+    for (int i = T->depth - 1; i > 0; --i) {
+        const uint32_t c = T->nodes[(size_t)curr * 8 + oref_digit(x, y, z, i)];
+        if (!c) return 0;
+        curr = c;
+    }
+    return T->nodes[(size_t)curr * 8 + oref_digit(x, y, z, 0)];
+}
+
+/* Config 1's och::octree, filled the reference's way: the demo
+ * terrain's columns with non-zero set() calls (y outer, x inner, z upward;
+ * one rand() per column for the top voxel, ORT/test_och_h_octree.cpp:776-783),
+ * then remove()'s pass over every voxel, z outer, x inner (:735-743), for the
+ * tunnel voxels (:745-765, :786): tunnel_mode 0 unset()s them, tunnel_mode 1
+ * set()s them to 0 as remove() does on the h_octree (leaving allocated empty
+ * nodes reachable, air voxels included), tunnel_mode -1 skips the pass. */
+ORA_API void ora_oref_fill_terrain(ora_oref *T, int tunnel_mode)
+{
+    const int dim = T->dim;
+    int *h = (int *)malloc(sizeof(int) * (size_t)dim * dim);
+    for (int y = 0; y < dim; ++y)
+        for (int x = 0; x < dim; ++x) h[(size_t)y * dim + x] = ora_height(x, y, dim);
+    srand(1);
+    for (int y = 0; y < dim && !T->overflow; ++y)
+        for (int x = 0; x < dim; ++x) {
+            const int hh = h[(size_t)y * dim + x];
+            const int top = 2 + (rand() > RAND_MAX / 2);
+            for (int z = 0; z <= hh && z < dim; ++z) ora_oref_set(T, x, y, z, ora_voxel(x, y, z, hh, top, 0));
+        }
+    if (tunnel_mode >= 0)
+        for (int z = 0; z < dim; ++z)
+            for (int y = 0; y < dim; ++y)
+                for (int x = 0; x < dim; ++x)
+                    if (ora_is_tunnel(x, y, z)) {
+                        if (tunnel_mode == 0) ora_oref_unset(T, x, y, z);
+                        else ora_oref_set(T, x, y, z, 0);
+                    }
+    free(h);
+}
+
+ORA_API const uint32_t *ora_oref_nodes(const ora_oref *T) { return T->nodes; }
+ORA_API uint32_t ora_oref_capacity(const ora_oref *T) { return T->cap; }
+ORA_API uint32_t ora_oref_head(const ora_oref *T) { return T->head; }
+ORA_API int ora_oref_node_cnt(const ora_oref *T) { return T->node_cnt; }
+ORA_API int ora_oref_overflow(const ora_oref *T) { return T->overflow; }
+
 ORA_API const uint32_t *ora_href_nodes(const ora_href *T) { return T->nodes; }
 ORA_API uint32_t ora_href_capacity(const ora_href *T) { return T->cap; }
 ORA_API uint32_t ora_href_root(const ora_href *T) { return T->root; }

@@ -352,3 +352,77 @@ class HRef:
 
     def pool(self) -> OraclePool:
         return OraclePool(self.nodes(), self.root, self.depth, index_base=1)
+
+
+class ORef:
+    """Exact restatement of och::octree's table and edits (ORT/och_octree.cpp:14-160):
+    capacity-sized, root at 0, free list threaded through children[0], set() /
+    unset() / at() as the reference performs them.  nodes() is the reference's
+    _table, slot for slot (what a reference user hands to the GPU)."""
+
+    def __init__(self, depth: int, capacity: int):
+        L = lib()
+        if not hasattr(L, "_oref_ready"):
+            L.ora_oref_new.restype = C.c_void_p
+            L.ora_oref_new.argtypes = [C.c_int, C.c_uint32]
+            L.ora_oref_free.argtypes = [C.c_void_p]
+            L.ora_oref_set.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_uint32]
+            L.ora_oref_unset.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int]
+            L.ora_oref_at.restype = C.c_uint32
+            L.ora_oref_at.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int]
+            L.ora_oref_fill_terrain.argtypes = [C.c_void_p, C.c_int]
+            L.ora_oref_nodes.restype = C.c_void_p
+            L.ora_oref_nodes.argtypes = [C.c_void_p]
+            for f in ("capacity", "head"):
+                getattr(L, "ora_oref_" + f).restype = C.c_uint32
+                getattr(L, "ora_oref_" + f).argtypes = [C.c_void_p]
+            for f in ("node_cnt", "overflow"):
+                getattr(L, "ora_oref_" + f).restype = C.c_int
+                getattr(L, "ora_oref_" + f).argtypes = [C.c_void_p]
+            L._oref_ready = True
+        if capacity < 2:
+            raise ValueError("capacity must be at least 2")
+        self.depth, self.capacity = int(depth), int(capacity)
+        self._t = L.ora_oref_new(self.depth, self.capacity)
+
+    def __del__(self):
+        if getattr(self, "_t", None):
+            lib().ora_oref_free(self._t)
+            self._t = None
+
+    def _check(self):
+        if lib().ora_oref_overflow(self._t):
+            raise RuntimeError("octree table exhausted (reference: 'Too many allocations', exit(0))")
+
+    def set(self, x, y, z, v):
+        lib().ora_oref_set(self._t, x, y, z, v)
+        self._check()
+
+    def unset(self, x, y, z):
+        lib().ora_oref_unset(self._t, x, y, z)
+
+    def at(self, x, y, z):
+        return lib().ora_oref_at(self._t, x, y, z)
+
+    def fill_terrain(self, tunnels: str | None = "unset"):
+        """Config 1's fill: non-zero set() per column, then the tunnel voxels
+        unset() ("unset"), set to 0 ("set0", as remove() does), or kept (None)."""
+        mode = {"unset": 0, "set0": 1, None: -1}[tunnels]
+        lib().ora_oref_fill_terrain(self._t, mode)
+        self._check()
+
+    @property
+    def head(self):
+        return lib().ora_oref_head(self._t)
+
+    @property
+    def node_cnt(self):
+        return lib().ora_oref_node_cnt(self._t)
+
+    def nodes(self) -> np.ndarray:
+        p = lib().ora_oref_nodes(self._t)
+        return np.ctypeslib.as_array(C.cast(p, C.POINTER(C.c_uint32)),
+                                     shape=(self.capacity * 8,)).reshape(self.capacity, 8).copy()
+
+    def pool(self) -> OraclePool:
+        return OraclePool(self.nodes(), 0, self.depth, index_base=0)

@@ -212,15 +212,65 @@ def test_cull_frames_identical(ort, O, gpu_device):
     pool.close()
 
 
+def oracle_codes(O, ref_pool, rcp, pos, yaw, pitch, fov, W, H, nvox, bounce):
+    """The indexed-colour frame (OCH_CODE_*, include/och_gpu.h) of one camera
+    at any position, from the oracle's raygen (ORT/test_och_h_octree.cpp:
+    87-138) and full walk: 6 * (voxel - 1) + dir, 125 magenta, 126 inside,
+    127 sky, | 128 when config 5's secondary ray is blocked."""
+    rays = O.raygen(yaw, pitch, fov, W, H)
+    o = np.asarray(pos, np.float32)
+    if bounce:
+        r = O.trace_bounce_batch(ref_pool, rcp, o, rays, nthreads=16)
+    else:
+        r = O.trace_batch(ref_pool, rcp, o, rays, nthreads=16)
+    d, v = r["dir"].astype(np.int64), r["voxel"].astype(np.int64)
+    code = np.where((v >= 1) & (v <= nvox), 6 * (v - 1) + d, 125)
+    code = np.where(d == 7, 126, np.where(d == 6, 127, code))
+    if bounce:
+        code |= np.where((d < 6) & (r["dir2"] != 6), 128, 0)
+    return code.astype(np.uint8)
+
+
+def _render_codes_vs_oracle(ort, O, pool, ref_pool, cams, W, H, rcp=None, culls=(1, 0)):
+    """Render every camera's codes (8 views a launch), primary and config 5,
+    at each cull setting; compare each frame with the oracle's.  Returns the
+    oracle frames (for statistics)."""
+    import torch
+    rcp = O.Rcp(None) if rcp is None else rcp
+    nvox = len(ort.VoxelData().get_colours()) // 6
+    wants = {}
+    for bounce in (False, True):                            # config 5 takes the shortcut too
+        wants[bounce] = [oracle_codes(O, ref_pool, rcp, tuple(c.pos), *c._args, W, H, nvox, bounce)
+                         for c in cams]
+        for cull in culls:
+            pool.set_option("cull", cull)
+            for i in range(0, len(cams), 8):
+                group = cams[i:i + 8]
+                out = torch.empty(len(group) * W * H, dtype=torch.uint8, device="cuda")
+                pool.render_codes_views_dev(group, out, H, 0, 1, bounce)
+                got = out.cpu().numpy().reshape(len(group), H * W)
+                for k, c in enumerate(group):
+                    bad = np.nonzero(got[k] != wants[bounce][i + k])[0]
+                    assert bad.size == 0, (f"cull {cull} bounce {bounce} camera pos {tuple(c.pos)} "
+                                           f"yaw/pitch/fov {c._args}: {bad.size} pixels differ, first {bad[:4]}")
+    return wants
+
+
+def _camera(ort, pos, yaw, pitch, fov, W, H):
+    c = ort.camera(tuple(float(v) for v in pos), float(yaw), float(pitch), float(fov), W, H)
+    c._args = (float(yaw), float(pitch), float(fov))
+    return c
+
+
 @pytest.mark.gpu
-def test_cull_camera_shortcut_grazing(ort, gpu_device):
+def test_cull_camera_shortcut_grazing(ort, O, gpu_device):
     """Camera frames skip ray setup for rays camera_proven_miss shows to miss
     the voxels' box (och_kernels.hip).  Around a tight box,
     from origins near it, in every direction, with wide and narrow fields of
     view, the box's silhouette is full of rays that graze its faces, edges and
-    corners: frames with the cull on (shortcut + exact cull) equal the frames
-    of the full walk (cull off, itself pinned to the oracle above) code for
-    code, primary and config 5."""
+    corners: frames with the cull on (shortcut + exact cull) and off (the
+    full walk) both equal the oracle's code for code, at every one of the 384
+    cameras, primary and config 5."""
     import torch
     depth = 8
     rng = np.random.default_rng(11)
@@ -233,26 +283,73 @@ def test_cull_camera_shortcut_grazing(ort, gpu_device):
     pool = ort.HOctree(nodes, root, depth, device=0)
     pool.set_palette(ort.VoxelData().get_colours())
     pool.set_stream(torch.cuda.current_stream())
+    ref_pool = O.OraclePool(nodes, root, depth, 1)
     W, H = 192, 108
     yaws = np.linspace(0, 2 * np.pi, 8, endpoint=False)
     centre, size = (lo + hi) / 2, hi - lo
-    frames = {c: [] for c in (1, 0)}
+    cams = []
     for _ in range(6):
         pos = np.clip(centre + size * rng.uniform(0.6, 3.0, 3) * rng.choice([-1, 1], 3), 1.001, 1.999)
         for fov in (1.25, 0.3):
-            cams = [ort.camera(tuple(float(v) for v in pos), float(y), float(p), fov, W, H)
-                    for y in yaws for p in (-1.2, -0.4, 0.4, 1.2)]
-            for cull in (1, 0):
-                pool.set_option("cull", cull)
-                for bounce in (False, True):                # config 5 takes the shortcut too
-                    for i in range(0, len(cams), 8):
-                        out = torch.empty(8 * W * H, dtype=torch.uint8, device="cuda")
-                        pool.render_codes_views_dev(cams[i:i + 8], out, H, 0, 1, bounce)
-                        frames[cull].append(out)
-    torch.cuda.synchronize()
-    on, off = torch.cat(frames[1]), torch.cat(frames[0])
-    assert torch.equal(on, off)
+            cams += [_camera(ort, pos, y, p, fov, W, H) for y in yaws for p in (-1.2, -0.4, 0.4, 1.2)]
+    assert len(cams) == 384
+    wants = _render_codes_vs_oracle(ort, O, pool, ref_pool, cams, W, H)
     # the box is in view: some of these rays hit it, most miss it
-    hit = ((off.cpu().numpy() & 0x7F) < 120).mean()
+    hit = np.mean([((w & 0x7F) < 120).mean() for w in wants[False]])
     assert 0.001 < hit < 0.9
+    pool.close()
+
+
+@pytest.mark.gpu
+def test_cull_camera_shortcut_grazing_d12(ort, O, gpu_device):
+    """The bench's depth-12 terrain, whose voxels fill [0, 4096)^2 x [0, 1264):
+    cameras just above the box's top face, z = 1 + 1264/4096 + a few voxels or
+    less, looking along it (pitch within +-0.02 rad) in eight directions.  The
+    rays that graze the top face are where camera_proven_miss's error budget
+    is tightest; cull on and off equal the oracle pixel for pixel."""
+    import torch
+    t = ort.build_terrain(12, use_gpu=True)
+    pool = ort.HOctree(t.nodes, t.root, 12, device=0)
+    pool.set_palette(ort.VoxelData().get_colours())
+    pool.set_stream(torch.cuda.current_stream())
+    ref_pool = O.OraclePool(t.nodes, t.root, 12, 1)
+    assert ort.occupied_box(t.nodes, t.root, 12)[1][2] == 1264
+    top = 1.0 + 1264 / 4096
+    W, H = 320, 180
+    rng = np.random.default_rng(12)
+    cams = []
+    for dz in (2.0 ** -23, 2.0 ** -16, 0.5 / 4096, 3.0 / 4096):
+        for yaw in np.linspace(0, 2 * np.pi, 8, endpoint=False) + 0.05:
+            pos = (float(rng.uniform(1.2, 1.8)), float(rng.uniform(1.2, 1.8)), float(np.float32(top + dz)))
+            for pitch, fov in ((0.0, 1.25), (-0.02, 0.3), (0.02, 0.3)):
+                cams.append(_camera(ort, pos, yaw, pitch, fov, W, H))
+    assert all(c.pos[2] > top for c in cams)
+    wants = _render_codes_vs_oracle(ort, O, pool, ref_pool, cams, W, H)
+    sky = np.mean([(w == 127).mean() for w in wants[False]])
+    assert 0.2 < sky < 0.95                    # half the view is sky, much of it grazing the top face
+    pool.close()
+
+
+@pytest.mark.gpu
+def test_cull_coarse_rcp_table(ort, O, gpu_device, intel_lut):
+    """camera_proven_miss budgets the RCPPS table's error.  A coarse
+    table (2^6 entries, relative error ~2^-6, above the 2^-10 bound) switches
+    the shortcut off for its pool, so only the exact per-ray cull runs:
+    frames stay the oracle's under the same table, cull on and off."""
+    import torch
+    coarse = np.ascontiguousarray(intel_lut[::32])
+    assert coarse.size == 64 and ort.rcp_lut_error(coarse) > 2.0 ** -10
+    assert ort.rcp_lut_error(intel_lut) < 1.5 * 2.0 ** -12
+    t = ort.build_terrain(9)
+    pool = ort.HOctree(t.nodes, t.root, 9, device=0)
+    pool.set_palette(ort.VoxelData().get_colours())
+    pool.set_stream(torch.cuda.current_stream())
+    pool.set_rcp_lut(coarse)
+    ref_pool = O.OraclePool(t.nodes, t.root, 9, 1)
+    W, H = 320, 180
+    top = 1.0 + ort.occupied_box(t.nodes, t.root, 9)[1][2] / 512
+    cams = [_camera(ort, (1.5, 1.5, 1.5), 0.3, p, 1.25, W, H) for p in (0.0, -0.6, 0.4)]
+    cams += [_camera(ort, (1.4, 1.6, top + dz), y, 0.0, 1.25, W, H)
+             for dz in (2.0 ** -20, 1.0 / 1024) for y in (0.3, 1.9, 3.5, 5.1)]
+    _render_codes_vs_oracle(ort, O, pool, ref_pool, cams, W, H, rcp=O.Rcp(coarse))
     pool.close()
