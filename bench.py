@@ -58,6 +58,7 @@ PITCHES = (0.0, -0.6)
 YAW, FOV = 0.3, 1.25
 ORIGIN = (1.5, 1.5, 1.5)
 PMC_PATH = ROOT / "profiles" / "pmc_summary.json"
+WINDOW_PATH = ROOT / "profiles" / "window_summary.json"
 
 
 def log(*a):
@@ -302,6 +303,23 @@ def load_pmc(kernel: str, config_key: str):
     return d.get("kernels", {}).get(kernel), "profiles/pmc_summary.json"
 
 
+def load_window():
+    """The committed rocprofv3 kernel-trace summary of the bench's pipelined
+    window (profiles/window_summary.json, written by tools/window_trace.py),
+    if it was taken of the kernel source in this tree."""
+    if not WINDOW_PATH.exists():
+        return None
+    try:
+        d = json.loads(WINDOW_PATH.read_text())
+    except Exception:
+        return None
+    if d.get("kernel_source_sha") != kernel_source_digest():
+        return {"source": "profiles/window_summary.json", "stale": True}
+    keep = ("config", "steps", "ms_per_step_trace", "busy_union_ms_per_step", "kernel_ms_sum_per_step",
+            "mean_concurrency", "concurrency_hist_ms", "render_mean_ms")
+    return {"source": "profiles/window_summary.json", **{k: d.get(k) for k in keep}}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -328,6 +346,10 @@ def main():
                     help="put every frame in flight on a new stream, none on the current stream")
     ap.add_argument("--extra-windows", type=int, default=0,
                     help="diagnostic: this many more warmup + timed windows after the first (reported, not value)")
+    ap.add_argument("--shade", choices=("display", "all"), default="display",
+                    help="N > 1: every rank all-gathers the frame's codes; 'display' = only rank 0 (the display) "
+                         "expands them to RGBA8 frames, 'all' = every rank does")
+    ap.add_argument("--no-cull-off", action="store_true", help="skip the cull-off window (value_cull_off)")
     ap.add_argument("--inflight", type=int, default=3,
                     help="frames in flight: steps alternate over this many HIP streams, so one step's "
                          "slowest rays overlap the next step's bulk (1 = serialised)")
@@ -379,7 +401,7 @@ def main():
     sfs = []
     for s_ in streams:
         with torch.cuda.stream(s_):
-            sfs.append(ShardedFrame(pool, W, H, a.row_chunk, n_views=len(PITCHES), indexed=indexed))
+            sfs.append(ShardedFrame(pool, W, H, a.row_chunk, n_views=len(PITCHES), indexed=indexed, shade=a.shade))
     pool.set_stream(stream)
     # Launch order: one planning render of these views times every tile, and
     # the costliest tiles go first (och_gpu_plan_views; dispatch order only,
@@ -435,7 +457,29 @@ def main():
         torch.cuda.synchronize()
         ms = np.array([x.elapsed_time(y) for x, y in tms])
         trace_only = {"mrays_s": n_px * len(cams) * 10 / ms.sum() / 1e3, "ms_per_frame": float(ms.mean()),
-                      "bytes_per_ray": 12 + 12 + 4 * push_total / (n_px * len(cams))}
+                      "bytes_per_ray": 12 + 12 + 4 * push_total / (n_px * len(cams)),
+                      "path": "och_gpu_trace_batch_dev: resident rays, 64 consecutive rays per wave"}
+        # the same rays through och_gpu_trace_batch_tiled_dev (8x8 tiles of the W-wide
+        # ray image per wave), launch order planned from the pitch-0 view's rays
+        pool.raygen_dev(cams[0], dirs)
+        pool.plan_batch_tiled(o_t, dirs, W)
+        tms = []
+        for cam in cams:
+            pool.raygen_dev(cam, dirs)
+            for _ in range(5):
+                pool.trace_batch_tiled_dev(o_t, dirs, W, hd, hv, ht)
+            for _ in range(10):
+                s0, s1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                s0.record(stream)
+                pool.trace_batch_tiled_dev(o_t, dirs, W, hd, hv, ht)
+                s1.record(stream)
+                tms.append((s0, s1))
+        torch.cuda.synchronize()
+        ms = np.array([x.elapsed_time(y) for x, y in tms])
+        trace_only["tiled"] = {"mrays_s": n_px * len(cams) * 10 / ms.sum() / 1e3, "ms_per_frame": float(ms.mean()),
+                               "path": f"och_gpu_trace_batch_tiled_dev: the same resident rays as a {W}-wide image, "
+                                       "one 8x8 tile per wave, launch order planned from the pitch-0 view's rays "
+                                       "(och_gpu_plan_batch_tiled), one launch per view"}
     del hd, hv, ht, hp, dirs
 
     # timing events for every step of a window, created once, outside the timed region
@@ -459,9 +503,18 @@ def main():
             f_.exchange()
 
     issue_s = []                           # host time to issue each timed window's steps
+    rank_s = []                            # every rank's wall time of each timed window
+    marker = torch.zeros(1, dtype=torch.int64, device=dev)
 
-    def timed(n, bounce=False, ev=None):
+    def mark():
+        """A one-element bitwise_not kernel: brackets the headline window in a
+        rocprofv3 kernel trace (tools/window_trace.py), outside the timed region."""
+        torch.bitwise_not(marker, out=marker)
+
+    def timed(n, bounce=False, ev=None, marked=False):
         """n steps between barrier + synchronize; max over ranks of the wall time."""
+        if marked:
+            mark()
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
@@ -479,8 +532,14 @@ def main():
         el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
         if gc_was:
             gc.enable()
+        if marked:
+            mark()
         if world > 1:
-            coll(dist.all_reduce, el, op=dist.ReduceOp.MAX)
+            every = torch.zeros(world, dtype=torch.float64, device=dev)
+            coll(dist.all_gather_into_tensor, every, el)
+            rank_s.append(every.tolist())
+            return float(every.max().item())
+        rank_s.append([float(el.item())])
         return float(el.item())
 
     # Frame latency: the render launch alone on an otherwise idle GPU.
@@ -493,7 +552,8 @@ def main():
     for k in range(a.warmup):
         step(k)
     ev = []
-    elapsed = timed(a.steps, ev=ev)
+    elapsed = timed(a.steps, ev=ev, marked=True)
+    per_rank_ms = [round(t / a.steps * 1e3, 4) for t in rank_s[-1]]
     last = (a.steps - 1) % len(sfs)
     frames_host = sfs[last].frames.cpu().numpy() if rank == 0 else None
     pool.set_stream(stream)
@@ -516,6 +576,24 @@ def main():
         vals = [W * H * len(cams) * n_s / r / 1e6 for r in runs]
         sustained = {"value": round(statistics.median(vals), 2), "unit": "Mrays/s", "steps_per_run": n_s,
                      "runs_s": [round(r, 4) for r in runs], "values": [round(v, 2) for v in vals]}
+
+    # The same window with the occupied-box cull off (every ray walks): the
+    # traversal speed like-for-like with round 1 and with the CPU baseline.
+    cull_off = None
+    if not a.no_cull_off and pool.get_option("cull"):
+        c_prev = pool.get_option("cull")
+        pool.set_option("cull", 0)
+        if pool.get_option("tile_order") >= 2:
+            pool.plan_views(cams, a.row_chunk, rank, world)       # the plan is per cull setting
+        for k in range(a.warmup):
+            step(k)
+        el_off = timed(a.steps)
+        cull_off = {"value": round(total_rays / el_off / 1e6, 2), "ms_per_step": round(el_off / a.steps * 1e3, 4),
+                    "note": "same warmup and window, OCH_OPT_CULL = 0: every ray walks from the root"}
+        pool.set_option("cull", c_prev)
+        if pool.get_option("tile_order") >= 2:
+            pool.plan_views(cams, a.row_chunk, rank, world)
+        pool.set_stream(stream)
 
     # Config 5 (BASELINE configs[4]): the same frames with one mirrored
     # secondary ray per hit pixel, in-block wavefront compaction on; same
@@ -584,17 +662,25 @@ def main():
             "walked_push_per_ray": round(walk_push / rays_rank, 3), "culled_frac": round(culled / rays_rank, 4),
             "traffic": None if pmc is None else pmc.get("hbm_bytes_per_launch"),
             "traffic_note": "PMC 2*FETCH_SIZE + WRITE_SIZE per render launch (MI355X_MICROARCH.md HBM): bytes "
-                            "leaving L2, Infinity-Cache hits included", "pmc_source": pmc_src, "hbm": hbm}
+                            "leaving L2, Infinity-Cache hits included", "pmc_source": pmc_src, "hbm": hbm,
+            "window_profile": load_window()}
     if pmc and "SQ_INSTS_VALU" in pmc:
         insts = float(pmc["SQ_INSTS_VALU"])
         ach = insts / step_s / 1e9
+        prof_ms = float(pmc.get("mean_ms") or 0.0)
         roof.update({"bound": "valu-issue", "achieved": round(ach, 1), "peak": VALU_PEAK_GINST_S,
                      "unit": "G VALU wave-instructions/s", "frac": round(ach / VALU_PEAK_GINST_S, 4),
                      "valu_insts_per_launch": int(insts), "valu_insts_per_wave": pmc.get("valu_insts_per_wave"),
                      "valu_lane_utilization": pmc.get("valu_lane_utilization"),
                      "achieved_per_launch": round(insts / (k_avg_ms * 1e-3) / 1e9, 1),
-                     "note": "issue rate over the pipelined step (frames overlap, so per-launch durations overlap "
-                             "too); the DAG is L2/MALL-resident, so HBM is far from binding (see hbm)"})
+                     # per launch, from the profile alone: SQ_INSTS_VALU / that profile's mean launch duration
+                     "frac_profile": round(insts / (prof_ms * 1e-3) / 1e9 / VALU_PEAK_GINST_S, 4) if prof_ms else None,
+                     "profile_mean_ms": prof_ms or None,
+                     "effective_clock_ghz": pmc.get("effective_clock_ghz"),
+                     "note": "frac = issue rate over the pipelined step (three frames overlap, so a launch lasts "
+                             "longer than a step: window_profile shows the overlap); frac_profile = the same "
+                             "instructions over one launch's mean duration under the profiler; the DAG is "
+                             "L2/MALL-resident, so HBM is far from binding (see hbm)"})
     else:
         roof.update({k: hbm[k] for k in ("bound", "achieved", "peak", "unit", "frac")})
 
@@ -641,12 +727,21 @@ def main():
                        "pool_mb": round(nodes.nbytes / 2**20, 1), "build_s": round(build_s, 2),
                        "build": "och_build_terrain, use_gpu=1: 32^3 bricks voxelised, hash-consed and renumbered on the GPU",
                        "parallelism": f"rows{world}",
+                       "shade": ("every rank all-gathers the frame's codes; " +
+                                 ("rank 0 (the display) shades them to RGBA8" if a.shade == "display" and world > 1
+                                  else "every rank shades them to RGBA8")),
                        "frames": "indexed-colour codes, shaded after the exchange" if indexed else "rgba8",
                        "options": {k: pool.get_option(k) for k in pool.OPTIONS}},
             "roofline": roof,
             "cpu_baseline": cpu,
             "parity": parity,
             "sustained": sustained,
+            "value_cull_off": None if cull_off is None else cull_off["value"],
+            "cull_off": cull_off,
+            "walked_rays_per_s": round(value * (1 - culled / rays_rank), 2),
+            "walked_rays_note": "Mrays/s of the rays that walk the DAG (value x (1 - culled_frac)); the "
+                                "occupied-box cull ends the rest as proven misses",
+            "per_rank_ms_per_step": per_rank_ms,
             **({"extra_windows": extra} if extra else {}),
             "trace_batch": trace_only,
             "bounce": bounce,

@@ -203,6 +203,26 @@ OCH_API int och_gpu_trace_batch_dev(och_gpu_pool *pool, const float *origin, int
                                     int32_t *hit_direction, uint32_t *hit_voxel, float *hit_time,
                                     uint32_t *push_count);
 
+/* och_gpu_trace_batch_dev for rays laid out as a row-major image `width`
+ * rays wide (a camera's rays as update_position stores them, x + y * W,
+ * ORT/test_och_h_octree.cpp:135): each wavefront walks an 8x8 tile of
+ * neighbouring rays instead of 64 consecutive rays of one row, so its lanes
+ * share the DAG's top nodes and finish after similar walks.  n need not be a
+ * multiple of width (the last row is partial).  Records in the caller's
+ * order, bit-identical to och_gpu_trace_batch_dev.  With OCH_OPT_TILE_ORDER
+ * >= 2, batches of the geometry planned by och_gpu_plan_batch_tiled dispatch
+ * their costliest tiles first. */
+OCH_API int och_gpu_trace_batch_tiled_dev(och_gpu_pool *pool, const float *origin, int origin_stride,
+                                          const float *dirs, uint32_t n, uint32_t width,
+                                          int32_t *hit_direction, uint32_t *hit_voxel, float *hit_time,
+                                          uint32_t *push_count);
+/* Plan the launch order of tiled batches of n rays `width` wide (block size
+ * and schedule included in the key): one timed trace of these rays, then
+ * costliest tiles first.  Synchronous; a plan stays valid while the rays
+ * change (it orders dispatch only). */
+OCH_API int och_gpu_plan_batch_tiled(och_gpu_pool *pool, const float *origin, int origin_stride,
+                                     const float *dirs, uint32_t n, uint32_t width);
+
 /* Config 5 (BASELINE configs[4]): each primary ray that hits a voxel face
  * spawns one secondary ray -- from o + d*t - offset, the point half a voxel in
  * front of the hit face (get_directional_hit_offset, ORT/test_och_h_octree.cpp:

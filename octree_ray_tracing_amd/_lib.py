@@ -82,6 +82,8 @@ PROTOTYPES = {
     "och_gpu_trace": (C.c_int, [_P] + [_f32] * 6 + [C.POINTER(_i32), C.POINTER(_u32), C.POINTER(_f32)]),
     "och_gpu_trace_batch": (C.c_int, [_P, _P, C.c_int, _P, _u32, _P, _P, _P]),
     "och_gpu_trace_batch_dev": (C.c_int, [_P, _P, C.c_int, _P, _u32, _P, _P, _P, _P]),
+    "och_gpu_trace_batch_tiled_dev": (C.c_int, [_P, _P, C.c_int, _P, _u32, _u32, _P, _P, _P, _P]),
+    "och_gpu_plan_batch_tiled": (C.c_int, [_P, _P, C.c_int, _P, _u32, _u32]),
     "och_gpu_trace_bounce_batch_dev": (C.c_int, [_P, _P, C.c_int, _P, _u32, _P, _P, _P, _P, _P, _P, _P]),
     "och_camera_setup": (C.c_int, [_f32] * 6 + [C.c_int, C.c_int, C.POINTER(Camera)]),
     "och_gpu_raygen_dev": (C.c_int, [_P, C.POINTER(Camera), _P]),

@@ -166,11 +166,12 @@ struct och_gpu_pool {
     uint32_t *h_stage = nullptr, *d_stage = nullptr;
     size_t stage_words = 0;
     // cost-planned launch order (och_gpu_plan_views, OCH_OPT_TILE_ORDER = 2)
-    // [0] primary frames (grid kernel), [1] config-5 frames (bounce kernel)
-    uint32_t *d_order[2] = {nullptr, nullptr};
-    uint32_t *d_order_xcd[2] = {nullptr, nullptr};   // OCH_OPT_TILE_ORDER = 3: the same, grouped per XCD
-    uint32_t order_blocks[2] = {0, 0};
-    int64_t plan_key[2][8] = {};
+    // [0] primary frames (grid kernel), [1] config-5 frames (bounce kernel),
+    // [2] tiled trace batches (och_gpu_plan_batch_tiled)
+    uint32_t *d_order[3] = {nullptr, nullptr, nullptr};
+    uint32_t *d_order_xcd[3] = {nullptr, nullptr, nullptr};   // OCH_OPT_TILE_ORDER = 3: grouped per XCD
+    uint32_t order_blocks[3] = {0, 0, 0};
+    int64_t plan_key[3][8] = {};
 
     hipStream_t stream() const { return use_ext ? ext_stream : own_stream; }
 
@@ -969,6 +970,91 @@ OCH_API int och_gpu_trace_bounce_batch_dev(och_gpu_pool *p, const float *origin,
                                            p->stream()));
     OCH_HIP(hipEventRecord(p->ev_stop, p->stream()));
     p->timed = true;
+    return OCH_OK;
+}
+
+namespace {
+
+int tiled_args(const och_gpu_pool *p, const float *origin, int origin_stride, const float *dirs, uint32_t n,
+               uint32_t width)
+{
+    if (!p || (n && (!origin || !dirs))) return fail(OCH_E_INVALID, "NULL argument");
+    if (origin_stride != 0 && origin_stride != 3) return fail(OCH_E_INVALID, "origin_stride must be 0 or 3");
+    if (width == 0) return fail(OCH_E_INVALID, "width must be positive");
+    const uint64_t rows = ((uint64_t)n + width - 1) / width;
+    if ((uint64_t)((width + 7) / 8) * ((rows + 7) / 8) * 64 >= (1ull << 32))
+        return fail(OCH_E_INVALID, "batch of %u rays %u wide too large", n, width);
+    return check_ready(p);
+}
+
+// The key of a tiled batch's launch plan: the geometry and the block size.
+void batch_key(const och_gpu_pool *p, uint32_t n, uint32_t width, int64_t key[8])
+{
+    const int64_t k[8] = {n, width, p->opt_block, p->opt_schedule, 0, 0, 0, 0};
+    std::memcpy(key, k, sizeof k);
+}
+
+}  // namespace
+
+OCH_API int och_gpu_trace_batch_tiled_dev(och_gpu_pool *p, const float *origin, int origin_stride, const float *dirs,
+                                          uint32_t n, uint32_t width, int32_t *hit_dir, uint32_t *hit_voxel,
+                                          float *hit_time, uint32_t *push_count)
+{
+    if (int st = tiled_args(p, origin, origin_stride, dirs, n, width)) return st;
+    if (n && (!hit_dir || !hit_voxel || !hit_time)) return fail(OCH_E_INVALID, "NULL argument");
+    DeviceGuard g(p->device);
+    och::Schedule sc = p->schedule();
+    if (p->opt_tile_order >= 2 && p->opt_schedule == 0 && p->d_order[2]) {
+        int64_t key[8];
+        batch_key(p, n, width, key);
+        if (std::memcmp(key, p->plan_key[2], sizeof key) == 0) sc.order = p->d_order[2];
+    }
+    OCH_HIP(hipEventRecord(p->ev_start, p->stream()));
+    OCH_HIP(och::launch_trace_batch_tiled(p->dev(), origin, origin_stride, dirs, n, width, hit_dir, hit_voxel,
+                                          reinterpret_cast<uint32_t *>(hit_time), push_count, sc, p->stream()));
+    OCH_HIP(hipEventRecord(p->ev_stop, p->stream()));
+    p->timed = true;
+    return OCH_OK;
+}
+
+OCH_API int och_gpu_plan_batch_tiled(och_gpu_pool *p, const float *origin, int origin_stride, const float *dirs,
+                                     uint32_t n, uint32_t width)
+{
+    if (int st = tiled_args(p, origin, origin_stride, dirs, n, width)) return st;
+    if (n == 0) return OCH_OK;
+    DeviceGuard g(p->device);
+    const uint32_t tiles = ((width + 7) / 8) * (uint32_t)(((n + width - 1) / width + 7) / 8);
+    const uint32_t max_blocks = (uint32_t)(((uint64_t)tiles * 64 + p->opt_block - 1) / p->opt_block);
+    const size_t out_bytes = (((size_t)n * 4 + 255) & ~(size_t)255);
+    int st = ensure_scratch(p, 3 * out_bytes + (size_t)max_blocks * 4);
+    if (st != OCH_OK) return st;
+    char *base = static_cast<char *>(p->d_scratch);
+    uint32_t *cost = reinterpret_cast<uint32_t *>(base + 3 * out_bytes);
+    OCH_HIP(hipMemsetAsync(cost, 0xFF, (size_t)max_blocks * 4, p->stream()));
+    och::Schedule sc = p->schedule();
+    sc.kind = 0;
+    sc.tile_order = 0;
+    sc.cost = cost;
+    OCH_HIP(och::launch_trace_batch_tiled(p->dev(), origin, origin_stride, dirs, n, width,
+                                          reinterpret_cast<int32_t *>(base), reinterpret_cast<uint32_t *>(base + out_bytes),
+                                          reinterpret_cast<uint32_t *>(base + 2 * out_bytes), nullptr, sc, p->stream()));
+    std::vector<uint32_t> c(max_blocks);
+    OCH_HIP(hipMemcpyAsync(c.data(), cost, (size_t)max_blocks * 4, hipMemcpyDeviceToHost, p->stream()));
+    OCH_HIP(hipStreamSynchronize(p->stream()));
+    std::vector<uint32_t> order(max_blocks);
+    for (uint32_t i = 0; i < max_blocks; ++i) order[i] = i;
+    std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return c[a] > c[b]; });
+    if (p->order_blocks[2] < max_blocks) {
+        for (uint32_t **o : {&p->d_order[2], &p->d_order_xcd[2]}) {
+            if (*o) OCH_HIP(hipFree(*o));
+            *o = nullptr;
+        }
+        p->order_blocks[2] = 0;
+        OCH_HIP(hipMalloc(&p->d_order[2], (size_t)max_blocks * 4));
+        p->order_blocks[2] = max_blocks;
+    }
+    OCH_HIP(hipMemcpy(p->d_order[2], order.data(), (size_t)max_blocks * 4, hipMemcpyHostToDevice));
+    batch_key(p, n, width, p->plan_key[2]);
     return OCH_OK;
 }
 

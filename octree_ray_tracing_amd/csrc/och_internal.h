@@ -135,6 +135,11 @@ struct Schedule {
 hipError_t launch_trace_batch(const DevPool &p, const float *origin, int origin_stride, const float *dirs,
                               uint32_t n, int32_t *hit_dir, uint32_t *hit_voxel, uint32_t *hit_time,
                               uint32_t *push_count, const Schedule &sc, hipStream_t stream);
+// The same rays as a row-major image `width` rays wide, one 8x8 tile per
+// wave (TiledArraySource); records in the caller's order.
+hipError_t launch_trace_batch_tiled(const DevPool &p, const float *origin, int origin_stride, const float *dirs,
+                                    uint32_t n, uint32_t width, int32_t *hit_dir, uint32_t *hit_voxel,
+                                    uint32_t *hit_time, uint32_t *push_count, const Schedule &sc, hipStream_t stream);
 // hipOccupancyMaxActiveBlocksPerMultiprocessor of kind 0 render-grid,
 // 1 render-persistent, 2 trace-grid, at this block size and stack depth.
 hipError_t occupancy_blocks_per_cu(int kind, int block, int depth, int *blocks);

@@ -688,12 +688,6 @@ __device__ __forceinline__ void camera_ray(const och_camera &C, int col, int row
 #endif
 constexpr uint32_t kTileW = OCH_TILE_W, kTileH = 64 / OCH_TILE_W;
 
-// Camera rays of one shard's slice for up to kMaxViews cameras of equal size,
-// enumerated view after view, 8x8 pixel tile after tile, so a wave's 64 rays
-// are one tile of one view (ray i -> tile i / 64, pixel i % 64).  Tiles run
-// row-major (order 0) or in 64x64-pixel supertiles of 8x8 tiles (order 1),
-// which the grid kernel hands to one XCD as a unit (see xcd_block).  The
-// output token is view * slice_pixels + slice pixel.
 // Division by a launch constant: n / d = (mulhi(n, m) + n) >> s for every
 // 32-bit n, with m, s from the host (round-up multiplier; checked against
 // plain division over all 32-bit edge cases).  A wave-uniform n stays on the
@@ -714,6 +708,61 @@ struct FastDiv {
     }
 };
 
+// Resident rays of a row-major image `width` rays wide (a camera's rays as
+// update_position lays them out, ORT/test_och_h_octree.cpp:135, x + y * W),
+// walked one 8x8 tile per wave as CameraSource walks pixels: neighbouring
+// rays share the DAG's top nodes and finish after similar walks, where a
+// wave of 64 consecutive rays of one row spreads over a 64 x 1 strip.  Ray
+// i = row * width + col, records in the caller's order.  The tile arithmetic
+// of a wave runs on the scalar unit.
+struct TiledArraySource {
+    const float *origin;
+    const float *dirs;
+    int origin_stride;
+    uint32_t n, width, tiles_x, tiles;
+    FastDiv by_tiles_x;
+    __host__ __device__ __forceinline__ uint32_t count() const { return tiles * 64u; }
+    __device__ __forceinline__ bool at(uint32_t tile, uint32_t lane, float *o, float *d, uint32_t &out) const
+    {
+        const uint32_t ty = by_tiles_x.div(tile), tx = tile - ty * tiles_x;
+        const uint32_t col = tx * 8u + (lane & 7u), row = ty * 8u + (lane >> 3);
+        if (col >= width) return false;
+        const uint32_t i = row * width + col;
+        if (i >= n) return false;
+        const float *po = origin + (size_t)origin_stride * i;
+        const float *pd = dirs + 3 * (size_t)i;
+        o[0] = po[0]; o[1] = po[1]; o[2] = po[2];
+        d[0] = pd[0]; d[1] = pd[1]; d[2] = pd[2];
+        out = i;
+        return true;
+    }
+    __device__ __forceinline__ bool get(uint32_t i, float *o, float *d, uint32_t &out) const
+    {
+        return at(i >> 6, i & 63u, o, d, out);
+    }
+    __device__ __forceinline__ bool get_wave(uint32_t wave_base, uint32_t lane, float *o, float *d, uint32_t &out) const
+    {
+        return at(__builtin_amdgcn_readfirstlane(wave_base >> 6), lane, o, d, out);
+    }
+    // Arbitrary rays: no camera shortcut; ray_init's exact cull still applies.
+    __device__ __forceinline__ bool get_wave_culled(uint32_t wave_base, uint32_t lane, const DevPool &, bool,
+                                                    float *o, float *d, uint32_t &out, bool &miss) const
+    {
+        miss = false;
+        return get_wave(wave_base, lane, o, d, out);
+    }
+    __device__ __forceinline__ bool get_refill(uint32_t base, uint32_t k, float *o, float *d, uint32_t &out) const
+    {
+        return get(base + k, o, d, out);
+    }
+};
+
+// Camera rays of one shard's slice for up to kMaxViews cameras of equal size,
+// enumerated view after view, 8x8 pixel tile after tile, so a wave's 64 rays
+// are one tile of one view (ray i -> tile i / 64, pixel i % 64).  Tiles run
+// row-major (order 0) or in 64x64-pixel supertiles of 8x8 tiles (order 1),
+// which the grid kernel hands to one XCD as a unit (see xcd_block).  The
+// output token is view * slice_pixels + slice pixel.
 struct CameraSource {
     och_camera cam[kMaxViews];
     int32_t n_views, row_chunk, shard, n_shards, slice_rows, width, height, order;
@@ -1472,6 +1521,27 @@ hipError_t launch_trace_batch(const DevPool &p, const float *origin, int origin_
                                                         n, sc, stream);
     return launch<ArraySource, HitSink<false>, false>(p, src, HitSink<false>{hit_dir, hit_voxel, hit_time, nullptr}, n,
                                                       sc, stream);
+}
+
+hipError_t launch_trace_batch_tiled(const DevPool &p, const float *origin, int origin_stride, const float *dirs,
+                                    uint32_t n, uint32_t width, int32_t *hit_dir, uint32_t *hit_voxel,
+                                    uint32_t *hit_time, uint32_t *push_count, const Schedule &sc, hipStream_t stream)
+{
+    if (n == 0) return hipSuccess;
+    TiledArraySource src;
+    src.origin = origin;
+    src.dirs = dirs;
+    src.origin_stride = origin_stride;
+    src.n = n;
+    src.width = width;
+    src.tiles_x = (width + 7) / 8;
+    src.tiles = src.tiles_x * ((((n + width - 1) / width) + 7) / 8);
+    src.by_tiles_x.init(src.tiles_x);
+    if (push_count)
+        return launch<TiledArraySource, HitSink<true>, true>(
+            p, src, HitSink<true>{hit_dir, hit_voxel, hit_time, push_count}, src.count(), sc, stream);
+    return launch<TiledArraySource, HitSink<false>, false>(p, src, HitSink<false>{hit_dir, hit_voxel, hit_time, nullptr},
+                                                           src.count(), sc, stream);
 }
 
 hipError_t launch_raygen(const och_camera &cam, float *dirs, hipStream_t stream)

@@ -51,7 +51,7 @@ class ShardedFrame:
     """
 
     def __init__(self, pool: GpuPool, width: int, height: int, row_chunk: int = 8, n_views: int = 1, group=None,
-                 indexed: bool = False, shard: tuple[int, int] | None = None):
+                 indexed: bool = False, shard: tuple[int, int] | None = None, shade: str = "all"):
         import torch
         import torch.distributed as dist
 
@@ -71,6 +71,14 @@ class ShardedFrame:
         # and shade after the gather -- a quarter of the RGBA8 bytes on xGMI,
         # the same frames (needs a palette of <= CODE_MAX_VOXELS ids).
         self.indexed = indexed
+        # shade="display": every rank all-gathers the frame (as codes or RGBA8
+        # slices), and only rank 0 -- the one that displays it, as the
+        # reference's single window does (ORT/test_och_h_octree.cpp:437-457) --
+        # turns it into the [views][H][W] RGBA8 frames; the other ranks'
+        # `frames` stay unwritten and `gathered` holds their copy of the frame.
+        if shade not in ("all", "display"):
+            raise ValueError("shade must be 'all' or 'display'")
+        self.shade = shade
         dev = torch.device("cuda", torch.cuda.current_device())
         dt = torch.uint8 if indexed else torch.int32
         self.slice = torch.empty((n_views, self.rows, width), dtype=dt, device=dev)
@@ -108,6 +116,8 @@ class ShardedFrame:
             else:
                 dist.all_gather_into_tensor(self.gathered, self.slice, group=self.group)
             src = self.gathered
+        if self.shade == "display" and self.rank != 0:
+            return None
         if self.indexed:
             self.pool.shade_unshard_dev(src, self.frames, self.width, self.height, self.row_chunk, self.world,
                                         self.n_views)
@@ -131,8 +141,8 @@ class FrameGroup:
                  miss_t: float | None = None):
         nodes = np.ascontiguousarray(nodes, np.uint32).reshape(-1, 8)
         if devices is None:
-            from .tracer import device_count
-            devices = list(range(device_count()))
+            from .tracer import device_list
+            devices = device_list()
         devs = (C.c_int * len(devices))(*devices)
         if miss_t is None:
             miss_t = math.inf if index_base == 1 else 0.0

@@ -71,6 +71,15 @@ def rcp_lut_error(lut: np.ndarray) -> float:
     return e.value
 
 
+def device_list() -> list[int]:
+    """HIP indices of the visible gfx950 devices (och_device_list)."""
+    n = C.c_int()
+    call("och_device_list", None, 0, C.byref(n))
+    arr = (C.c_int * max(n.value, 1))()
+    call("och_device_list", C.cast(arr, C.c_void_p), n.value, C.byref(n))
+    return list(arr[:n.value])
+
+
 def device_count() -> int:
     n = C.c_int()
     call("och_device_count", C.byref(n))
@@ -209,6 +218,23 @@ class GpuPool:
         call("och_gpu_trace_batch_dev", self._h, _dev_ptr(origins), stride, _dev_ptr(dirs), int(n),
              _dev_ptr(hit_dir), _dev_ptr(hit_voxel), _dev_ptr(hit_time),
              None if push is None else _dev_ptr(push))
+
+    def trace_batch_tiled_dev(self, origins, dirs, width: int, hit_dir, hit_voxel, hit_time, push=None, n=None):
+        """trace_batch_dev for rays laid out as a row-major image `width` wide: one 8x8 tile of
+        neighbouring rays per wavefront (och_gpu_trace_batch_tiled_dev); records in the caller's order."""
+        if n is None:
+            n = dirs.numel() // 3
+        stride = 0 if origins.numel() == 3 else 3
+        call("och_gpu_trace_batch_tiled_dev", self._h, _dev_ptr(origins), stride, _dev_ptr(dirs), int(n), int(width),
+             _dev_ptr(hit_dir), _dev_ptr(hit_voxel), _dev_ptr(hit_time), None if push is None else _dev_ptr(push))
+
+    def plan_batch_tiled(self, origins, dirs, width: int, n=None):
+        """Plan the launch order of tiled batches of this geometry (och_gpu_plan_batch_tiled); used with
+        set_option("tile_order", 2).  Synchronous."""
+        if n is None:
+            n = dirs.numel() // 3
+        stride = 0 if origins.numel() == 3 else 3
+        call("och_gpu_plan_batch_tiled", self._h, _dev_ptr(origins), stride, _dev_ptr(dirs), int(n), int(width))
 
     def trace_bounce_batch_dev(self, origins, dirs, hit_dir, hit_voxel, hit_time, bounce_dir, bounce_voxel,
                                bounce_time, push=None, n=None):

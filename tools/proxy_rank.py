@@ -1,13 +1,15 @@
-"""One rank's share of an N-rank bench step, on this one GPU (no collective).
+"""Every rank's share of an N-rank bench step, on this one GPU (no collective).
 
 At N > 1 bench.py renders configs[3] (3840x2160, two views) split over the
-ranks; each rank renders its row chunks, all-gathers the 1-byte codes and
-shades the whole frame.  This tool times exactly that per-rank GPU work --
-the render of shard 0 of N and the shade of the full frame, with the
-gathered buffer written on the device instead of over xGMI -- for several
-frames-in-flight settings, so the N = 2/4/8 per-rank step can be measured
-on a 1-GPU box.  The xGMI receive time is not in it (estimated separately in
-DESIGN.md §5).
+ranks; each rank renders its row chunks, all-gathers the 1-byte codes, and
+the display rank (or, with --shade all, every rank) shades the whole frame.
+This tool times exactly that per-rank GPU work -- the render of shard s of N
+and the shade of the full frame where that rank shades, with the gathered
+buffer written on the device instead of over xGMI -- for every shard s
+(--shards all) and several frames-in-flight settings, so the N = 2/4/8
+per-rank steps, and their maximum (the driver's value takes the max over
+ranks), can be measured on a 1-GPU box.  The xGMI receive time is not in it
+(estimated separately in DESIGN.md §5).
 
 python tools/proxy_rank.py --worlds 8 --inflight 3
 
@@ -43,6 +45,9 @@ def main():
     ap.add_argument("--no-exchange", action="store_true", help="render only: no gather copy, no shade")
     ap.add_argument("--events", action="store_true", help="record timing events around every render, as bench.py")
     ap.add_argument("--opt", action="append", default=[], metavar="NAME=VALUE", help="pool option, e.g. chain=1")
+    ap.add_argument("--shards", default="0", help="'all', or a comma list of shards to time")
+    ap.add_argument("--shade", choices=("display", "all"), default="display",
+                    help="as bench.py: 'display' = only rank 0 shades the gathered frame")
     a = ap.parse_args()
 
     import torch
@@ -70,52 +75,82 @@ def main():
     for world in [int(x) for x in a.worlds.split(",")]:
         W, H = (1920, 1080) if world == 1 else (3840, 2160)     # configs[2] / configs[3]
         cams = [ort.camera((1.5, 1.5, 1.5), 0.3, p, 1.25, W, H) for p in (0.0, -0.6)]
-        pool.plan_views(cams, 8, 0, world)
-        rays_rank = None
+        shards = list(range(world)) if a.shards == "all" else [int(x) for x in a.shards.split(",") if int(x) < world]
         for nf in [int(x) for x in a.inflight.split(",")]:
             streams = [base] + [torch.cuda.Stream() for _ in range(nf - 1)]
-            sfs = []
-            for s_ in streams:
-                with torch.cuda.stream(s_):
-                    sfs.append(ShardedFrame(pool, W, H, 8, n_views=2, indexed=True, shard=(0, world)))
-            rows = sfs[0].rows
-            from octree_ray_tracing_amd.frame import slice_row_map
-            rays_rank = int((slice_row_map(H, 8, world, 0) >= 0).sum()) * W * 2
-
-            def run(n):
-                torch.cuda.synchronize()
-                t0 = time.perf_counter()
-                for k in range(n):
-                    s_, f_ = streams[k % nf], sfs[k % nf]
-                    pool.set_stream(s_)
-                    with torch.cuda.stream(s_):
-                        if a.events:
-                            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                            e0.record(s_)
-                        f_.render_local(cams)
-                        if a.events:
-                            e1.record(s_)
-                        if not a.no_exchange:
-                            f_.exchange()
-                torch.cuda.synchronize()
-                return time.perf_counter() - t0
-
-            run(5)
-            wins = [run(a.steps) for _ in range(a.windows)]
-            sus = [run(a.sustain_steps) for _ in range(3)]
-            row = {"world": world, "frame": f"{W}x{H}", "inflight": nf, "opts": opts, "exchange": not a.no_exchange, "events": a.events, "rays_per_step_rank": rays_rank,
-                   "slice_rows": rows,
-                   "ms_per_step_20": round(statistics.median(wins) / a.steps * 1e3, 4),
-                   "mrays_s_rank_20": round(rays_rank * a.steps / statistics.median(wins) / 1e6, 1),
-                   "ms_per_step_sustained": round(statistics.median(sus) / a.sustain_steps * 1e3, 4),
-                   "mrays_s_rank_sustained": round(rays_rank * a.sustain_steps / statistics.median(sus) / 1e6, 1)}
-            print(json.dumps(row), flush=True)
-            res.append(row)
+            per_shard = []
+            for shard in shards:
+                pool.set_stream(base)
+                pool.plan_views(cams, 8, shard, world)
+                row = arm(a, torch, pool, streams, cams, W, H, world, shard, nf, opts)
+                print(json.dumps(row), flush=True)
+                res.append(row)
+                per_shard.append(row)
+            if len(per_shard) > 1:
+                summ = {"world": world, "inflight": nf, "summary": True, "shade": a.shade,
+                        "shards": len(per_shard)}
+                for k in ("mrays_s_rank_20", "mrays_s_rank_sustained"):
+                    v = [r[k] for r in per_shard]
+                    summ[k.replace("mrays_s_rank", "min")] = min(v)
+                    summ[k.replace("mrays_s_rank", "max")] = max(v)
+                for k in ("ms_per_step_20", "ms_per_step_sustained"):
+                    v = [r[k] for r in per_shard]
+                    summ["slowest_" + k] = max(v)
+                    summ["spread_" + k] = round(max(v) / min(v) - 1, 4)
+                # the driver's value takes the max over ranks of the step time: the whole
+                # job's rays over the slowest rank's step
+                rays_all = sum(r["rays_per_step_rank"] for r in per_shard)
+                summ["job_mrays_s_20"] = round(rays_all / (summ["slowest_ms_per_step_20"] * 1e-3) / 1e6, 1)
+                summ["job_mrays_s_sustained"] = round(rays_all / (summ["slowest_ms_per_step_sustained"] * 1e-3) / 1e6, 1)
+                print(json.dumps(summ), flush=True)
+                res.append(summ)
             pool.set_stream(base)
-            del sfs
     Path(a.out).parent.mkdir(parents=True, exist_ok=True)
     Path(a.out).write_text(json.dumps(res, indent=1))
     pool.close()
+
+
+def arm(a, torch, pool, streams, cams, W, H, world, shard, nf, opts):
+    """One shard's pipelined steps: 20-step windows (median) and sustained runs."""
+    from octree_ray_tracing_amd.frame import ShardedFrame, slice_row_map
+    sfs = []
+    for s_ in streams:
+        with torch.cuda.stream(s_):
+            sfs.append(ShardedFrame(pool, W, H, 8, n_views=2, indexed=True, shard=(shard, world),
+                                    shade=a.shade))
+    rows = sfs[0].rows
+    rays_rank = int((slice_row_map(H, 8, world, shard) >= 0).sum()) * W * 2
+
+    def run(n):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for k in range(n):
+            s_, f_ = streams[k % nf], sfs[k % nf]
+            pool.set_stream(s_)
+            with torch.cuda.stream(s_):
+                if a.events:
+                    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    e0.record(s_)
+                f_.render_local(cams)
+                if a.events:
+                    e1.record(s_)
+                if not a.no_exchange:
+                    f_.exchange()
+        torch.cuda.synchronize()
+        return time.perf_counter() - t0
+
+    run(5)
+    wins = [run(a.steps) for _ in range(a.windows)]
+    sus = [run(a.sustain_steps) for _ in range(3)]
+    row = {"world": world, "shard": shard, "frame": f"{W}x{H}", "inflight": nf, "opts": opts,
+           "exchange": not a.no_exchange, "shade": a.shade, "shades": a.shade == "all" or shard == 0,
+           "events": a.events, "rays_per_step_rank": rays_rank, "slice_rows": rows,
+           "ms_per_step_20": round(statistics.median(wins) / a.steps * 1e3, 4),
+           "mrays_s_rank_20": round(rays_rank * a.steps / statistics.median(wins) / 1e6, 1),
+           "ms_per_step_sustained": round(statistics.median(sus) / a.sustain_steps * 1e3, 4),
+           "mrays_s_rank_sustained": round(rays_rank * a.sustain_steps / statistics.median(sus) / 1e6, 1)}
+    del sfs
+    return row
 
 
 if __name__ == "__main__":
