@@ -229,7 +229,7 @@ def other_configs(a, dev, stream):
     sfs = []
     for s_ in streams:
         with torch.cuda.stream(s_):
-            sfs.append(ShardedFrame(pool, 1920, 1080, a.row_chunk, n_views=2, indexed=True))
+            sfs.append(ShardedFrame(pool, 1920, 1080, a.row_chunk, n_views=2, indexed=True, direct=not a.no_direct))
 
     def run(n):
         torch.cuda.synchronize()
@@ -350,6 +350,9 @@ def main():
                     help="N > 1: every rank all-gathers the frame's codes; 'display' = only rank 0 (the display) "
                          "expands them to RGBA8 frames, 'all' = every rank does")
     ap.add_argument("--no-cull-off", action="store_true", help="skip the cull-off window (value_cull_off)")
+    ap.add_argument("--no-direct", action="store_true",
+                    help="N = 1: render codes and shade them in a second pass, as ranks do at N > 1, instead of "
+                         "the fused launch writing the RGBA8 frames directly")
     ap.add_argument("--inflight", type=int, default=3,
                     help="frames in flight: steps alternate over this many HIP streams, so one step's "
                          "slowest rays overlap the next step's bulk (1 = serialised)")
@@ -392,6 +395,7 @@ def main():
     # Frames travel between ranks as 1-byte colour codes and are shaded after
     # the gather (same RGBA8 frames, a quarter of the bytes on xGMI).
     indexed = not a.rgba_frames and ort.VoxelData().get_colours().size // 6 <= pool.CODE_MAX_VOXELS
+    direct = world == 1 and not a.no_direct
     cams = [ort.camera(ORIGIN, YAW, p, FOV, W, H) for p in PITCHES]
     # One frame buffer set and one HIP stream per frame in flight.
     if a.fresh_streams:      # every frame in flight on a new stream (none on the current one)
@@ -401,7 +405,8 @@ def main():
     sfs = []
     for s_ in streams:
         with torch.cuda.stream(s_):
-            sfs.append(ShardedFrame(pool, W, H, a.row_chunk, n_views=len(PITCHES), indexed=indexed, shade=a.shade))
+            sfs.append(ShardedFrame(pool, W, H, a.row_chunk, n_views=len(PITCHES), indexed=indexed, shade=a.shade,
+                                    direct=direct))
     pool.set_stream(stream)
     # Launch order: one planning render of these views times every tile, and
     # the costliest tiles go first (och_gpu_plan_views; dispatch order only,
@@ -460,26 +465,38 @@ def main():
                       "bytes_per_ray": 12 + 12 + 4 * push_total / (n_px * len(cams)),
                       "path": "och_gpu_trace_batch_dev: resident rays, 64 consecutive rays per wave"}
         # the same rays through och_gpu_trace_batch_tiled_dev (8x8 tiles of the W-wide
-        # ray image per wave), launch order planned from the pitch-0 view's rays
-        pool.raygen_dev(cams[0], dirs)
-        pool.plan_batch_tiled(o_t, dirs, W)
-        tms = []
-        for cam in cams:
-            pool.raygen_dev(cam, dirs)
-            for _ in range(5):
-                pool.trace_batch_tiled_dev(o_t, dirs, W, hd, hv, ht)
-            for _ in range(10):
-                s0, s1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                s0.record(stream)
-                pool.trace_batch_tiled_dev(o_t, dirs, W, hd, hv, ht)
-                s1.record(stream)
-                tms.append((s0, s1))
-        torch.cuda.synchronize()
-        ms = np.array([x.elapsed_time(y) for x, y in tms])
-        trace_only["tiled"] = {"mrays_s": n_px * len(cams) * 10 / ms.sum() / 1e3, "ms_per_frame": float(ms.mean()),
-                               "path": f"och_gpu_trace_batch_tiled_dev: the same resident rays as a {W}-wide image, "
-                                       "one 8x8 tile per wave, launch order planned from the pitch-0 view's rays "
-                                       "(och_gpu_plan_batch_tiled), one launch per view"}
+        # ray image per wave): one launch per view, and both views' rays in one
+        # launch (a W x 2H image, as the render launch takes both views), that
+        # geometry's launch order planned (och_gpu_plan_batch_tiled)
+        both = torch.empty(2 * n_px * 3, dtype=torch.float32, device=dev)
+        bd = torch.empty(2 * n_px, dtype=torch.int32, device=dev)
+        bv = torch.empty(2 * n_px, dtype=torch.int32, device=dev)
+        bt = torch.empty(2 * n_px, dtype=torch.float32, device=dev)
+        for v, cam in enumerate(cams):
+            pool.raygen_dev(cam, both[v * n_px * 3:(v + 1) * n_px * 3])
+        pool.plan_batch_tiled(o_t, both, W)      # the plan keys one geometry: the two-view batch
+        tiled = {}
+        for label, n_rays, buf in (("per_view", n_px, None), ("two_views", 2 * n_px, both)):
+            tms = []
+            for v in range(len(cams) if buf is None else 1):
+                src = both[v * n_px * 3:(v + 1) * n_px * 3] if buf is None else buf
+                for _ in range(5):
+                    pool.trace_batch_tiled_dev(o_t, src, W, bd, bv, bt, n=n_rays)
+                for _ in range(10):
+                    s0, s1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    s0.record(stream)
+                    pool.trace_batch_tiled_dev(o_t, src, W, bd, bv, bt, n=n_rays)
+                    s1.record(stream)
+                    tms.append((s0, s1))
+            torch.cuda.synchronize()
+            ms = np.array([x.elapsed_time(y) for x, y in tms])
+            tiled[label] = {"mrays_s": n_rays * len(tms) / ms.sum() / 1e3, "ms_per_launch": float(ms.mean()),
+                            "rays_per_launch": n_rays}
+        tiled["path"] = (f"och_gpu_trace_batch_tiled_dev: the same resident rays as a {W}-wide image, one 8x8 tile "
+                         "per wave; per_view = one launch per view, two_views = both views' rays in one launch "
+                         "(W x 2H, planned with och_gpu_plan_batch_tiled)")
+        trace_only["tiled"] = tiled
+        del both, bd, bv, bt
     del hd, hv, ht, hp, dirs
 
     # timing events for every step of a window, created once, outside the timed region
@@ -548,6 +565,12 @@ def main():
         step(0, lat if k >= max(a.warmup, 1) else None)
         torch.cuda.synchronize()
     latency_ms = float(np.median([x.elapsed_time(y) for x, y in lat]))
+    if trace_only is not None:
+        # per ray against a lone render launch (both views, raygen + trace + shade)
+        lone = latency_ms / (W * H * len(cams))
+        trace_only["vs_lone_render_per_ray"] = {
+            "untiled_per_view": round(trace_only["ms_per_frame"] / n_px / lone, 3),
+            "tiled_two_views": round(trace_only["tiled"]["two_views"]["ms_per_launch"] / (2 * n_px) / lone, 3)}
     # warmup, then the timed steps
     for k in range(a.warmup):
         step(k)
@@ -653,8 +676,9 @@ def main():
            "frac": round(canon_bytes / (k_avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 5),
            "achieved_per_step": round(canon_bytes / step_s / 1e9, 2),
            "frac_per_step": round(canon_bytes / step_s / 1e9 / HBM_PEAK_GBS, 5)}
-    pmc, pmc_src = load_pmc("k_render", f"d{a.depth}_{W}x{H}_n{world}")
-    roof = {"kernel": f"k_trace_grid<CameraSource,{'CodeSink' if indexed else 'FrameSink'}> (2 views per launch)",
+    rgba_launch = direct or not indexed
+    pmc, pmc_src = load_pmc("k_render_rgba" if rgba_launch else "k_render", f"d{a.depth}_{W}x{H}_n{world}")
+    roof = {"kernel": f"k_trace_grid<CameraSource,{'FrameSink' if rgba_launch else 'CodeSink'}> (2 views per launch)",
             "kernel_ms": round(k_avg_ms, 4), "kernel_ms_serial": round(latency_ms, 4),
             "host_issue_ms": host_issue_ms,
             "ms_per_step": round(step_s * 1e3, 4), "frames_in_flight": len(streams),
@@ -730,7 +754,8 @@ def main():
                        "shade": ("every rank all-gathers the frame's codes; " +
                                  ("rank 0 (the display) shades them to RGBA8" if a.shade == "display" and world > 1
                                   else "every rank shades them to RGBA8")),
-                       "frames": "indexed-colour codes, shaded after the exchange" if indexed else "rgba8",
+                       "frames": ("rgba8 frames written by the fused launch (no exchange at N = 1)" if direct else
+                                  "indexed-colour codes, shaded after the exchange" if indexed else "rgba8 slices"),
                        "options": {k: pool.get_option(k) for k in pool.OPTIONS}},
             "roofline": roof,
             "cpu_baseline": cpu,

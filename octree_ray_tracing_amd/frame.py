@@ -51,7 +51,8 @@ class ShardedFrame:
     """
 
     def __init__(self, pool: GpuPool, width: int, height: int, row_chunk: int = 8, n_views: int = 1, group=None,
-                 indexed: bool = False, shard: tuple[int, int] | None = None, shade: str = "all"):
+                 indexed: bool = False, shard: tuple[int, int] | None = None, shade: str = "all",
+                 direct: bool = False):
         import torch
         import torch.distributed as dist
 
@@ -79,6 +80,10 @@ class ShardedFrame:
         if shade not in ("all", "display"):
             raise ValueError("shade must be 'all' or 'display'")
         self.shade = shade
+        # direct=True on a single rank: the fused launch writes the RGBA8 frames
+        # themselves (update_image's framebuffer, ORT/test_och_h_octree.cpp:
+        # 448-450) -- no slice, no exchange, no shade pass
+        self.direct = bool(direct) and self.world == 1 and not self.proxy
         dev = torch.device("cuda", torch.cuda.current_device())
         dt = torch.uint8 if indexed else torch.int32
         self.slice = torch.empty((n_views, self.rows, width), dtype=dt, device=dev)
@@ -92,6 +97,10 @@ class ShardedFrame:
         if not isinstance(cams, (list, tuple)):
             cams = [cams]
         assert len(cams) == self.n_views
+        if self.direct:
+            render = self.pool.render_bounce_views_dev if bounce else self.pool.render_views_dev
+            render(list(cams), self.frames, self.row_chunk, 0, 1)
+            return self.frames
         if self.indexed:
             self.pool.render_codes_views_dev(list(cams), self.slice, self.row_chunk, self.rank, self.world, bounce)
             return self.slice
@@ -102,6 +111,8 @@ class ShardedFrame:
     def exchange(self):
         import torch.distributed as dist
 
+        if self.direct:
+            return self.frames
         src = self.slice
         if self.proxy:
             # the bytes a gather lands in this rank's buffer, written on the

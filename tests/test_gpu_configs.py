@@ -95,6 +95,23 @@ def test_bench_instance_d12_1080p(ort, O, gpu_device, d12, d12_ref, pal):
     sf.render(cams)
     torch.cuda.synchronize()
     assert_frames(sf.frames, want)
+    # the N = 1 bench instance: the fused launch writes the RGBA8 frames
+    # directly (k_trace_grid<CameraSource,FrameSink>), three frames in flight
+    pool.set_option("tile_order", 2)
+    sfs = []
+    for s in streams:
+        with torch.cuda.stream(s):
+            sfs.append(ShardedFrame(pool, W, H, 8, n_views=2, indexed=True, direct=True))
+    for k in range(6):
+        s, sf = streams[k % 3], sfs[k % 3]
+        pool.set_stream(s)
+        with torch.cuda.stream(s):
+            sf.render(cams)
+    torch.cuda.synchronize()
+    for sf in sfs:
+        assert sf.direct
+        assert_frames(sf.frames, want)
+    pool.set_stream(torch.cuda.current_stream())
     pool.close()
 
 
