@@ -429,9 +429,29 @@ __device__ __forceinline__ void ray_descend(Ray &r, const DevPool &P, uint32_t s
     r.idx = nidx;
 }
 
+// OCH_ASM_LOAD: the descent's slot-word load into cur is issued by inline asm,
+// so the compiler's waitcnt pass does not see it in flight.  Its only
+// readers are the next PUSH and ray_result, each behind an explicit
+// `s_waitcnt vmcnt(0)` that takes cur as an operand (so no read of cur is
+// scheduled above it).  What the compiler's view saves is the vmcnt(0) it
+// puts at the POP chain: the chain writes cur (the popped word, an LDS read)
+// in lanes that are STEPping, and a load into cur may still be in flight for
+// the lanes that descended.  Those lanes are disjoint (a lane that descended
+// is due to PUSH and skips the STEP phase), and a load writes only the lanes
+// active at its issue, so no lane sees the other's write; the wave no longer
+// waits for its descents' loads before popping.
+#ifndef OCH_ASM_LOAD
+#define OCH_ASM_LOAD 0
+#endif
+__device__ __forceinline__ void wait_cur(Ray &r)
+{
+    if (OCH_ASM_LOAD) asm volatile("s_waitcnt vmcnt(0)" : "+v"(r.cur) : : "memory");
+}
+
 template <bool kCount>
 __device__ __forceinline__ void ray_push_descend(Ray &r, const DevPool &P, uint32_t stride, const uint32_t *top)
 {
+    wait_cur(r);
     if (!OCH_LOAD_INTO_CUR) r.cur = in_mode(r, kPending) ? r.child : r.cur;
     if (kCount) ++r.push;
     const uint32_t c24 = r.idx ^ r.inv;                                     // 24 + child index
@@ -450,7 +470,12 @@ __device__ __forceinline__ void ray_push_descend(Ray &r, const DevPool &P, uint3
     if (!OCH_DIM_LEVEL) ++r.level;
     *r.sp = r.cur;                          // the parent, before its register takes the child's word
     r.sp += stride;
-    if (OCH_LOAD_INTO_CUR)
+    if (OCH_LOAD_INTO_CUR && OCH_ASM_LOAD && !OCH_LDS_TOP)
+        asm volatile("global_load_dword %0, %1, %2 offset:-96"     // src = P.nodes - 96 B + off
+                     : "+v"(r.cur)
+                     : "v"(off), "s"(P.nodes)
+                     : "memory");
+    else if (OCH_LOAD_INTO_CUR)
         r.cur = *src;                       // the next PUSH's node, or the voxel id of a HIT
     else
         r.child = *src;
@@ -547,13 +572,15 @@ template <bool kPacked>
 __device__ __forceinline__ Hit ray_result(const Ray &r, const DevPool &P)
 {
     Hit h;
+    uint32_t cur = r.cur;
+    if (OCH_ASM_LOAD) asm volatile("s_waitcnt vmcnt(0)" : "+v"(cur) : : "memory");   // a HIT's voxel id load
     if (OCH_DIM_LEVEL ? r.dim > (1u << 22) : r.level == 0) {
         h.dir = OCH_EXIT;
         h.voxel = 0;
         h.t = P.miss_bits;
     } else {
         h.dir = (int32_t)((r.min_axis >> 1) + 3u * ((r.inv & r.min_axis & 7u) == 0));
-        h.voxel = (kPacked && OCH_MERGED_DESCEND && OCH_LOAD_INTO_CUR) ? r.cur : r.child;
+        h.voxel = (kPacked && OCH_MERGED_DESCEND && OCH_LOAD_INTO_CUR) ? cur : r.child;
         h.t = r.t_min;
     }
     h.push = r.push;
