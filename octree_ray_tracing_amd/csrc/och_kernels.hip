@@ -151,7 +151,7 @@ __device__ __forceinline__ void ray_push(Ray &r, const DevPool &P)
 #ifndef OCH_DUAL
 #define OCH_DUAL 0
 #endif
-template <bool kCount>
+template <bool kCount, bool kAsm = false>
 __device__ __forceinline__ void ray_push_descend(Ray &r, const DevPool &P, uint32_t stride,
                                                  const uint32_t *top = nullptr);
 
@@ -192,7 +192,7 @@ __device__ __forceinline__ bool ray_cull(const Ray &r, const DevPool &P, const f
 // before iterating.  Launches that count PUSHes cull only at OCH_OPT_CULL = 2
 // (a diagnostic: how many PUSHes the culled launch walks), so their counts
 // stay the reference's.
-template <bool kPacked, bool kCount, bool kCull = false>
+template <bool kPacked, bool kCount, bool kCull = false, bool kAsm = false>
 __device__ __forceinline__ void ray_init(Ray &r, const DevPool &P, const float *o, const float *d, uint32_t *stack,
                                          uint32_t stride)
 {
@@ -241,7 +241,7 @@ __device__ __forceinline__ void ray_init(Ray &r, const DevPool &P, const float *
         return;
     }
     if (kPacked && OCH_MERGED_DESCEND)
-        ray_push_descend<true>(r, P, stride);
+        ray_push_descend<true, kAsm>(r, P, stride);
     else
         ray_push<kPacked, true>(r, P);
 }
@@ -443,15 +443,19 @@ __device__ __forceinline__ void ray_descend(Ray &r, const DevPool &P, uint32_t s
 #ifndef OCH_ASM_LOAD
 #define OCH_ASM_LOAD 0
 #endif
+// The grid and bounce kernels (one ray per lane, straight-line use of cur)
+// take it; the refill and persistent schedules keep the compiler's loads.
+constexpr bool kAsmLoad = OCH_ASM_LOAD != 0;
+template <bool kAsm>
 __device__ __forceinline__ void wait_cur(Ray &r)
 {
-    if (OCH_ASM_LOAD) asm volatile("s_waitcnt vmcnt(0)" : "+v"(r.cur) : : "memory");
+    if (kAsm) asm volatile("s_waitcnt vmcnt(0)" : "+v"(r.cur) : : "memory");
 }
 
-template <bool kCount>
+template <bool kCount, bool kAsm>
 __device__ __forceinline__ void ray_push_descend(Ray &r, const DevPool &P, uint32_t stride, const uint32_t *top)
 {
-    wait_cur(r);
+    wait_cur<kAsm>(r);
     if (!OCH_LOAD_INTO_CUR) r.cur = in_mode(r, kPending) ? r.child : r.cur;
     if (kCount) ++r.push;
     const uint32_t c24 = r.idx ^ r.inv;                                     // 24 + child index
@@ -470,7 +474,7 @@ __device__ __forceinline__ void ray_push_descend(Ray &r, const DevPool &P, uint3
     if (!OCH_DIM_LEVEL) ++r.level;
     *r.sp = r.cur;                          // the parent, before its register takes the child's word
     r.sp += stride;
-    if (OCH_LOAD_INTO_CUR && OCH_ASM_LOAD && !OCH_LDS_TOP)
+    if (OCH_LOAD_INTO_CUR && kAsm && !OCH_LDS_TOP)
         asm volatile("global_load_dword %0, %1, %2 offset:-96"     // src = P.nodes - 96 B + off
                      : "+v"(r.cur)
                      : "v"(off), "s"(P.nodes)
@@ -503,7 +507,7 @@ __device__ __forceinline__ void ray_push_descend(Ray &r, const DevPool &P, uint3
     r.idx = nidx;
 }
 
-template <bool kPacked, bool kCount>
+template <bool kPacked, bool kCount, bool kAsm = false>
 __device__ __forceinline__ void ray_iterate(Ray &r, const DevPool &P, uint32_t stride, const uint32_t *top = nullptr)
 {
     if (kPacked && OCH_MERGED_DESCEND) {
@@ -511,7 +515,7 @@ __device__ __forceinline__ void ray_iterate(Ray &r, const DevPool &P, uint32_t s
         // no activity test: a miss leaves the lane kStepping, a HIT ends in this phase
         uint32_t m = r.mode;                  // tested through an opaque copy, so the skipping
         asm volatile("" : "+v"(m));           // lanes' r.mode is not re-materialised as kStepping
-        if (m != kStepping) ray_push_descend<kCount>(r, P, stride, top);
+        if (m != kStepping) ray_push_descend<kCount, kAsm>(r, P, stride, top);
         return;
     }
     if (!kPacked && in_mode(r, kPending)) ray_phase_descend<kPacked>(r, P, stride);
@@ -554,7 +558,7 @@ __device__ __forceinline__ void ray_walk_packed(Ray &r, const DevPool &P, uint32
 }
 
 // Walk an initialised ray to its HIT or MISS.
-template <bool kPacked, bool kCount>
+template <bool kPacked, bool kCount, bool kAsm = false>
 __device__ __forceinline__ void ray_run(Ray &r, const DevPool &P, uint32_t stride, const uint32_t *top = nullptr)
 {
     if (kPacked && OCH_STEP_RUN && OCH_MERGED_DESCEND && OCH_LOAD_INTO_CUR && OCH_POP_CHAIN && !OCH_LDS_TOP) {
@@ -562,18 +566,18 @@ __device__ __forceinline__ void ray_run(Ray &r, const DevPool &P, uint32_t strid
         return;
     }
     if (ray_active(r, P)) do {
-        ray_iterate<kPacked, kCount>(r, P, stride, top);
+        ray_iterate<kPacked, kCount, kAsm>(r, P, stride, top);
     } while (ray_active(r, P));
 }
 
 // The hit record of a finished ray (:346-355 hit, :423-431 miss).  The
 // merged loop (OCH_LOAD_INTO_CUR) leaves a HIT's voxel id in cur.
-template <bool kPacked>
-__device__ __forceinline__ Hit ray_result(const Ray &r, const DevPool &P)
+template <bool kPacked, bool kAsm = false>
+__device__ __forceinline__ Hit ray_result(Ray &r, const DevPool &P)
 {
     Hit h;
-    uint32_t cur = r.cur;
-    if (OCH_ASM_LOAD) asm volatile("s_waitcnt vmcnt(0)" : "+v"(cur) : : "memory");   // a HIT's voxel id load
+    wait_cur<kAsm>(r);                      // a HIT's voxel id load (OCH_ASM_LOAD)
+    const uint32_t cur = r.cur;
     if (OCH_DIM_LEVEL ? r.dim > (1u << 22) : r.level == 0) {
         h.dir = OCH_EXIT;
         h.voxel = 0;
@@ -1133,9 +1137,9 @@ __global__ void k_trace_grid(DevPool P, Src S, Sink K, uint32_t xcd_group, const
             K.put(out, Hit{OCH_EXIT, 0u, P.miss_bits, 0u});
         } else {
             Ray r;
-            ray_init<kPacked, kCount, true>(r, P, o, d, lds_stack + threadIdx.x, blockDim.x);
-            ray_run<kPacked, kCount>(r, P, blockDim.x, top);
-            K.put(out, ray_result<kPacked>(r, P));
+            ray_init<kPacked, kCount, true, kAsmLoad>(r, P, o, d, lds_stack + threadIdx.x, blockDim.x);
+            ray_run<kPacked, kCount, kAsmLoad>(r, P, blockDim.x, top);
+            K.put(out, ray_result<kPacked, kAsmLoad>(r, P));
         }
     }
 #endif
@@ -1172,16 +1176,16 @@ __global__ void k_trace_bounce(DevPool P, Src S, Sink K, int compact, const uint
             K.put_primary(out, Hit{OCH_EXIT, 0u, P.miss_bits, 0u}, false);
         } else {
             Ray r;
-            ray_init<kPacked, kCount, true>(r, P, o, d, stack, nb);
-            ray_run<kPacked, kCount>(r, P, nb);
-            const Hit h1 = ray_result<kPacked>(r, P);
+            ray_init<kPacked, kCount, true, kAsmLoad>(r, P, o, d, stack, nb);
+            ray_run<kPacked, kCount, kAsmLoad>(r, P, nb);
+            const Hit h1 = ray_result<kPacked, kAsmLoad>(r, P);
             want = h1.dir < OCH_EXIT;
             if (want) bounce_ray(o, d, h1, P.half_voxel, o2, d2);
             payload = K.put_primary(out, h1, want);
             if (want && !compact) {                                         // in place, no compaction
-                ray_init<kPacked, kCount, true>(r, P, o2, d2, stack, nb);
-                ray_run<kPacked, kCount>(r, P, nb);
-                K.put_secondary(out, payload, ray_result<kPacked>(r, P));
+                ray_init<kPacked, kCount, true, kAsmLoad>(r, P, o2, d2, stack, nb);
+                ray_run<kPacked, kCount, kAsmLoad>(r, P, nb);
+                K.put_secondary(out, payload, ray_result<kPacked, kAsmLoad>(r, P));
             }
         }
     }
@@ -1225,9 +1229,9 @@ __global__ void k_trace_bounce(DevPool P, Src S, Sink K, int compact, const uint
     __syncthreads();                                  // the queue is read: its LDS becomes stacks again
     if (has) {
         Ray r;
-        ray_init<kPacked, kCount, true>(r, P, so, sd, stack, nb);
-        ray_run<kPacked, kCount>(r, P, nb);
-        K.put_secondary(sout, spay, ray_result<kPacked>(r, P));
+        ray_init<kPacked, kCount, true, kAsmLoad>(r, P, so, sd, stack, nb);
+        ray_run<kPacked, kCount, kAsmLoad>(r, P, nb);
+        K.put_secondary(sout, spay, ray_result<kPacked, kAsmLoad>(r, P));
     }
     if (cost && threadIdx.x == 0) cost[blk] = (uint32_t)(__builtin_amdgcn_s_memtime() - c0);
     if (stamps) stamp(stamps, stamp_cap, t0, total);
