@@ -441,7 +441,7 @@ __device__ __forceinline__ void ray_descend(Ray &r, const DevPool &P, uint32_t s
 // active at its issue, so no lane sees the other's write; the wave no longer
 // waits for its descents' loads before popping.
 #ifndef OCH_ASM_LOAD
-#define OCH_ASM_LOAD 0
+#define OCH_ASM_LOAD 1
 #endif
 // The grid and bounce kernels (one ray per lane, straight-line use of cur)
 // take it; the refill and persistent schedules keep the compiler's loads.
