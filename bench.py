@@ -6,7 +6,8 @@ Workloads (BASELINE.json):
          yaw 0.3, fov 1.25.
   N > 1  configs[3]: the same tree, one fixed 3840x2160 frame split over the
          N ranks (strong scaling; --scaling weak grows the frame with N
-         instead).  Rows are dealt in 8-row chunks round-robin over ranks, and
+         instead).  Rows are dealt in 8-row chunks over ranks by their cost in one
+         timed render on rank 0 (--deal rr: round-robin), and
          every frame ends with an RCCL all-gather of the slices (1-byte colour
          codes) plus an on-device shade + unshard.  Rank 0 builds the pool and
          broadcasts it over RCCL.
@@ -350,6 +351,11 @@ def main():
                     help="N > 1: every rank all-gathers the frame's codes; 'display' = only rank 0 (the display) "
                          "expands them to RGBA8 frames, 'all' = every rank does")
     ap.add_argument("--no-cull-off", action="store_true", help="skip the cull-off window (value_cull_off)")
+    ap.add_argument("--deal", choices=("cost", "rr"), default="cost",
+                    help="N > 1: row chunks dealt by their cost in one timed render on rank 0 (och_gpu_chunk_costs "
+                         "+ och_deal_chunks), or round-robin")
+    ap.add_argument("--display-weight", type=float, default=0.9,
+                    help="N > 1 with --shade display: rank 0's share of the render work per rank (it also shades)")
     ap.add_argument("--no-direct", action="store_true",
                     help="N = 1: render codes and shade them in a second pass, as ranks do at N > 1, instead of "
                          "the fused launch writing the RGBA8 frames directly")
@@ -397,6 +403,19 @@ def main():
     indexed = not a.rgba_frames and ort.VoxelData().get_colours().size // 6 <= pool.CODE_MAX_VOXELS
     direct = world == 1 and not a.no_direct
     cams = [ort.camera(ORIGIN, YAW, p, FOV, W, H) for p in PITCHES]
+    # N > 1: which rank renders which row chunks.  Rank 0 times one render of
+    # the whole frame per chunk and deals the chunks longest first onto the
+    # least loaded rank (rank 0, which also shades for the display, counts its
+    # share at --display-weight); every rank gets the same table.
+    deal = None
+    if world > 1 and a.deal == "cost":
+        n_chunks = -(-H // a.row_chunk)
+        table = torch.zeros(n_chunks, dtype=torch.int32, device=dev)
+        if rank == 0:
+            w = [a.display_weight if a.shade == "display" else 1.0] + [1.0] * (world - 1)
+            table.copy_(torch.from_numpy(ort.deal_chunks(pool.chunk_costs(cams, a.row_chunk), world, w)))
+        coll(dist.broadcast, table, 0)
+        deal = table.cpu().numpy()
     # One frame buffer set and one HIP stream per frame in flight.
     if a.fresh_streams:      # every frame in flight on a new stream (none on the current one)
         streams = [torch.cuda.Stream(device=dev) for _ in range(max(1, a.inflight))]
@@ -406,7 +425,7 @@ def main():
     for s_ in streams:
         with torch.cuda.stream(s_):
             sfs.append(ShardedFrame(pool, W, H, a.row_chunk, n_views=len(PITCHES), indexed=indexed, shade=a.shade,
-                                    direct=direct))
+                                    direct=direct, deal=deal))
     pool.set_stream(stream)
     # Launch order: one planning render of these views times every tile, and
     # the costliest tiles go first (och_gpu_plan_views; dispatch order only,
@@ -418,7 +437,7 @@ def main():
 
     # PUSH counts of this rank's rays (for the algorithmic byte count): trace
     # the rank's own rows once with counting on; not part of the timed region.
-    rows = torch.from_numpy(slice_row_map(H, a.row_chunk, world, rank))
+    rows = torch.from_numpy(slice_row_map(H, a.row_chunk, world, rank, deal))
     push_total, walk_push, culled, hits_total, rays_rank = 0, 0, 0, 0, 0
     dirs = torch.empty(W * H * 3, dtype=torch.float32, device=dev)
     o_t = torch.tensor(ORIGIN, dtype=torch.float32, device=dev)
@@ -751,6 +770,11 @@ def main():
                        "pool_mb": round(nodes.nbytes / 2**20, 1), "build_s": round(build_s, 2),
                        "build": "och_build_terrain, use_gpu=1: 32^3 bricks voxelised, hash-consed and renumbered on the GPU",
                        "parallelism": f"rows{world}",
+                       "row_deal": (None if world == 1 else
+                                    "round-robin 8-row chunks" if deal is None else
+                                    f"row chunks dealt by cost (one timed render on rank 0), rank 0 weight "
+                                    f"{a.display_weight if a.shade == 'display' else 1.0}; chunks per rank "
+                                    f"{np.bincount(deal, minlength=world).tolist()}"),
                        "shade": ("every rank all-gathers the frame's codes; " +
                                  ("rank 0 (the display) shades them to RGBA8" if a.shade == "display" and world > 1
                                   else "every rank shades them to RGBA8")),

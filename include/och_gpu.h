@@ -273,6 +273,27 @@ OCH_API int och_gpu_plan_views(och_gpu_pool *pool, const och_camera *cams, int n
  * halved (RGB >> 1, alpha kept) when the secondary ray is blocked. */
 OCH_API int och_gpu_render_bounce_views_dev(och_gpu_pool *pool, const och_camera *cams, int n_views,
                                             uint32_t *rgba_slices, int row_chunk, int shard, int n_shards);
+/* Row deal: instead of round-robin, row chunk g of frames `height` rows tall
+ * (chunks of row_chunk rows over n_shards) belongs to shard chunk_shard[g],
+ * for ceil(height / row_chunk) chunks; each shard's chunks keep their order.
+ * Render, plan, shade and unshard calls of exactly this geometry use it.  A
+ * slice then holds och_gpu_slice_rows rows -- the largest shard's chunks, the
+ * others' slices padded -- so slices stay equal for an all-gather.  Every
+ * rank must set the same deal.  chunk_shard = NULL restores round-robin.
+ * Waits for the device (frames in flight may read the old tables). */
+OCH_API int och_gpu_set_row_deal(och_gpu_pool *pool, int height, int row_chunk, int n_shards, const int32_t *chunk_shard);
+/* Rows per slice for this geometry under the pool's deal (och_shard_rows without one). */
+OCH_API int och_gpu_slice_rows(const och_gpu_pool *pool, int height, int row_chunk, int n_shards, int *rows);
+/* The cost of every row chunk of these views: one timed render of the whole
+ * frame (every workgroup timed, shader clocks), spread over its tiles' rows.
+ * costs: ceil(height / row_chunk) floats.  Synchronous. */
+OCH_API int och_gpu_chunk_costs(och_gpu_pool *pool, const och_camera *cams, int n_views, int row_chunk, float *costs);
+/* Host only: deal n_chunks chunks of the given costs over n_shards, longest
+ * first onto the shard with the least cost per weight (weights NULL = all 1;
+ * a shard with other fixed work, e.g. the display rank's shading, gets a
+ * smaller weight), at most ceil(n_chunks * max weight / sum) + 2 chunks per
+ * shard.  Deterministic: the same costs give the same deal on every rank. */
+OCH_API int och_deal_chunks(const float *costs, int n_chunks, int n_shards, const float *weights, int32_t *chunk_shard);
 /* Reassemble n_shards gathered slices (slice s at gathered + s*rows*W) into a
  * full W*H frame on the device. */
 OCH_API int och_gpu_unshard_dev(och_gpu_pool *pool, const uint32_t *gathered, uint32_t *frame,
@@ -305,7 +326,9 @@ OCH_API int och_gpu_shade_unshard_views_dev(och_gpu_pool *pool, const uint8_t *g
  * palette has at most OCH_CODE_MAX_VOXELS ids, as RGBA8 otherwise.  RCCL is
  * loaded on first use (dlopen; an RCCL already in the process is reused);
  * OCH_E_NODEV when it cannot be.  devices = NULL means the first n_devices gfx950 devices (och_device_list).
- * Replaces the per-pixel loop of ORT/test_och_h_octree.cpp:437-457 across GPUs. */
+ * Replaces the per-pixel loop of ORT/test_och_h_octree.cpp:437-457 across GPUs.
+ * och_frame_group_plan also deals the row chunks by cost (och_gpu_chunk_costs,
+ * och_deal_chunks) so that every device gets an equal share of the work. */
 typedef struct och_frame_group och_frame_group;
 OCH_API int och_frame_group_create(const int *devices, int n_devices, const uint32_t *nodes, uint32_t n_nodes,
                                    uint32_t root, int depth, int index_base, float miss_t, och_frame_group **out);

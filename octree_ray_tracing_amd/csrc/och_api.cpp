@@ -171,7 +171,17 @@ struct och_gpu_pool {
     uint32_t *d_order[3] = {nullptr, nullptr, nullptr};
     uint32_t *d_order_xcd[3] = {nullptr, nullptr, nullptr};   // OCH_OPT_TILE_ORDER = 3: grouped per XCD
     uint32_t order_blocks[3] = {0, 0, 0};
-    int64_t plan_key[3][8] = {};
+    int64_t plan_key[3][9] = {};
+    // row deal (och_gpu_set_row_deal): for frames of deal_h rows in chunks of
+    // deal_chunk over deal_n shards, chunk g belongs to a chosen shard instead
+    // of g % n; slices hold deal_max chunks (the largest shard's, the rest padded)
+    int deal_h = 0, deal_chunk = 0, deal_n = 0, deal_max = 0;
+    uint64_t deal_serial = 0;                 // changes with every deal (plan keys)
+    int32_t *d_chunk_map = nullptr;           // [deal_n][deal_max] global chunk, -1 = padding
+    int32_t *d_owner = nullptr;               // [n_chunks] shard << 16 | local chunk
+    std::vector<int32_t> deal_table;          // the chunk -> shard table as set
+    bool deal_for(int H, int rc, int n) const { return deal_n && H == deal_h && rc == deal_chunk && n == deal_n; }
+    int slice_rows(int H, int rc, int n) const { return deal_for(H, rc, n) ? deal_max * rc : och_shard_rows(H, rc, n); }
 
     hipStream_t stream() const { return use_ext ? ext_stream : own_stream; }
 
@@ -598,6 +608,8 @@ OCH_API int och_gpu_pool_destroy(och_gpu_pool *p)
     for (uint32_t *o : p->d_order_xcd)
         if (o) (void)hipFree(o);
     if (p->d_counter) (void)hipFree(p->d_counter);
+    if (p->d_chunk_map) (void)hipFree(p->d_chunk_map);
+    if (p->d_owner) (void)hipFree(p->d_owner);
     if (p->ev_start) (void)hipEventDestroy(p->ev_start);
     if (p->ev_stop) (void)hipEventDestroy(p->ev_stop);
     if (p->own_stream) (void)hipStreamDestroy(p->own_stream);
@@ -988,9 +1000,9 @@ int tiled_args(const och_gpu_pool *p, const float *origin, int origin_stride, co
 }
 
 // The key of a tiled batch's launch plan: the geometry and the block size.
-void batch_key(const och_gpu_pool *p, uint32_t n, uint32_t width, int64_t key[8])
+void batch_key(const och_gpu_pool *p, uint32_t n, uint32_t width, int64_t key[9])
 {
-    const int64_t k[8] = {n, width, p->opt_block, p->opt_schedule, 0, 0, 0, 0};
+    const int64_t k[9] = {n, width, p->opt_block, p->opt_schedule, 0, 0, 0, 0, 0};
     std::memcpy(key, k, sizeof k);
 }
 
@@ -1005,7 +1017,7 @@ OCH_API int och_gpu_trace_batch_tiled_dev(och_gpu_pool *p, const float *origin, 
     DeviceGuard g(p->device);
     och::Schedule sc = p->schedule();
     if (p->opt_tile_order >= 2 && p->opt_schedule == 0 && p->d_order[2]) {
-        int64_t key[8];
+        int64_t key[9];
         batch_key(p, n, width, key);
         if (std::memcmp(key, p->plan_key[2], sizeof key) == 0) sc.order = p->d_order[2];
     }
@@ -1171,12 +1183,14 @@ int render_views(och_gpu_pool *p, const och_camera *cams, int n_views, uint32_t 
     f.row_chunk = row_chunk;
     f.shard = shard;
     f.n_shards = n_shards;
-    f.slice_rows = och_shard_rows(cams[0].height, row_chunk, n_shards);
+    f.slice_rows = p->slice_rows(cams[0].height, row_chunk, n_shards);
+    const bool dealt = p->deal_for(cams[0].height, row_chunk, n_shards);
+    f.chunk_map = dealt ? p->d_chunk_map + (size_t)shard * p->deal_max : nullptr;
     och::Schedule sc = p->schedule();
     const int which = bounce ? 1 : 0;
     if (p->opt_tile_order >= 2 && (bounce || p->opt_schedule == 0) && p->d_order[which]) {
-        const int64_t key[8] = {cams[0].width, cams[0].height, n_views, row_chunk, shard, n_shards, p->opt_block,
-                                bounce ? p->opt_bounce_compact : 0};
+        const int64_t key[9] = {cams[0].width, cams[0].height, n_views, row_chunk, shard, n_shards, p->opt_block,
+                                bounce ? p->opt_bounce_compact : 0, dealt ? (int64_t)p->deal_serial : 0};
         if (std::memcmp(key, p->plan_key[which], sizeof key) == 0)
             sc.order = p->opt_tile_order == 3 ? p->d_order_xcd[which] : p->d_order[which];
     }
@@ -1205,7 +1219,8 @@ OCH_API int och_gpu_plan_views(och_gpu_pool *p, const och_camera *cams, int n_vi
     // One planning render per kernel (primary grid, config-5 bounce) into
     // scratch in natural order, timing every workgroup.
     const int W = cams[0].width, H = cams[0].height;
-    const int rows = och_shard_rows(H, row_chunk, n_shards);
+    const int rows = p->slice_rows(H, row_chunk, n_shards);
+    const bool dealt = p->deal_for(H, row_chunk, n_shards);
     const size_t frame_bytes = (size_t)n_views * rows * W * 4;
     const uint32_t max_blocks = (uint32_t)((size_t)n_views * ((rows + 7) / 8) * ((W + 7) / 8)) + 1024;
     int st = ensure_scratch(p, frame_bytes + (size_t)max_blocks * 4);
@@ -1222,6 +1237,7 @@ OCH_API int och_gpu_plan_views(och_gpu_pool *p, const och_camera *cams, int n_vi
     f.shard = shard;
     f.n_shards = n_shards;
     f.slice_rows = rows;
+    f.chunk_map = dealt ? p->d_chunk_map + (size_t)shard * p->deal_max : nullptr;
     for (int which = 0; which < 2; ++which) {
         OCH_HIP(hipMemsetAsync(cost, 0xFF, (size_t)max_blocks * 4, p->stream()));
         och::Schedule sc = p->schedule();
@@ -1276,9 +1292,151 @@ OCH_API int och_gpu_plan_views(och_gpu_pool *p, const och_camera *cams, int n_vi
         }
         OCH_HIP(hipMemcpy(p->d_order[which], order.data(), (size_t)n_blocks * 4, hipMemcpyHostToDevice));
         OCH_HIP(hipMemcpy(p->d_order_xcd[which], grouped.data(), (size_t)n_blocks * 4, hipMemcpyHostToDevice));
-        const int64_t key[8] = {W, H, n_views, row_chunk, shard, n_shards, p->opt_block,
-                                which ? p->opt_bounce_compact : 0};
+        const int64_t key[9] = {W, H, n_views, row_chunk, shard, n_shards, p->opt_block,
+                                which ? p->opt_bounce_compact : 0, dealt ? (int64_t)p->deal_serial : 0};
         std::memcpy(p->plan_key[which], key, sizeof key);
+    }
+    return OCH_OK;
+}
+
+OCH_API int och_gpu_set_row_deal(och_gpu_pool *p, int height, int row_chunk, int n_shards, const int32_t *chunk_shard)
+{
+    if (!p) return fail(OCH_E_INVALID, "pool is NULL");
+    if (!chunk_shard && !p->deal_n) return OCH_OK;                      // round-robin already
+    if (chunk_shard && p->deal_for(height, row_chunk, n_shards) && row_chunk > 0 &&
+        std::equal(p->deal_table.begin(), p->deal_table.end(), chunk_shard))
+        return OCH_OK;                                                  // this deal already (plans stay valid)
+    DeviceGuard g(p->device);
+    OCH_HIP(hipDeviceSynchronize());          // frames in flight may still read the old tables
+    if (p->d_chunk_map) OCH_HIP(hipFree(p->d_chunk_map));
+    if (p->d_owner) OCH_HIP(hipFree(p->d_owner));
+    p->d_chunk_map = nullptr;
+    p->d_owner = nullptr;
+    p->deal_n = p->deal_h = p->deal_chunk = p->deal_max = 0;
+    p->deal_table.clear();
+    ++p->deal_serial;
+    if (!chunk_shard) return OCH_OK;           // back to round-robin
+    if (height <= 0 || row_chunk <= 0 || n_shards <= 0 || n_shards > 32767)
+        return fail(OCH_E_INVALID, "bad row deal geometry (%d, %d, %d)", height, row_chunk, n_shards);
+    const int n_chunks = (height + row_chunk - 1) / row_chunk;
+    std::vector<std::vector<int32_t>> mine(n_shards);
+    for (int c = 0; c < n_chunks; ++c) {
+        if (chunk_shard[c] < 0 || chunk_shard[c] >= n_shards)
+            return fail(OCH_E_INVALID, "chunk %d dealt to shard %d of %d", c, chunk_shard[c], n_shards);
+        mine[chunk_shard[c]].push_back(c);
+    }
+    int max_chunks = 1;
+    for (const auto &m : mine) max_chunks = std::max(max_chunks, (int)m.size());
+    if (max_chunks > 65535) return fail(OCH_E_INVALID, "more than 65535 chunks for one shard");
+    std::vector<int32_t> map((size_t)n_shards * max_chunks, -1), owner(n_chunks);
+    for (int sh = 0; sh < n_shards; ++sh)
+        for (size_t l = 0; l < mine[sh].size(); ++l) {
+            map[(size_t)sh * max_chunks + l] = mine[sh][l];
+            owner[mine[sh][l]] = (sh << 16) | (int32_t)l;
+        }
+    OCH_HIP(hipMalloc(&p->d_chunk_map, map.size() * 4));
+    OCH_HIP(hipMalloc(&p->d_owner, owner.size() * 4));
+    OCH_HIP(hipMemcpy(p->d_chunk_map, map.data(), map.size() * 4, hipMemcpyHostToDevice));
+    OCH_HIP(hipMemcpy(p->d_owner, owner.data(), owner.size() * 4, hipMemcpyHostToDevice));
+    p->deal_h = height;
+    p->deal_chunk = row_chunk;
+    p->deal_n = n_shards;
+    p->deal_max = max_chunks;
+    p->deal_table.assign(chunk_shard, chunk_shard + n_chunks);
+    return OCH_OK;
+}
+
+OCH_API int och_gpu_slice_rows(const och_gpu_pool *p, int height, int row_chunk, int n_shards, int *rows)
+{
+    if (!p || !rows) return fail(OCH_E_INVALID, "NULL argument");
+    *rows = p->slice_rows(height, row_chunk, n_shards);
+    return OCH_OK;
+}
+
+OCH_API int och_gpu_chunk_costs(och_gpu_pool *p, const och_camera *cams, int n_views, int row_chunk, float *costs)
+{
+    if (!p || !cams || !costs || row_chunk <= 0) return fail(OCH_E_INVALID, "bad chunk-cost arguments");
+    if (n_views < 1 || n_views > OCH_MAX_VIEWS) return fail(OCH_E_INVALID, "n_views %d outside 1..%d", n_views, OCH_MAX_VIEWS);
+    for (int v = 0; v < n_views; ++v)
+        if (cams[v].width != cams[0].width || cams[v].height != cams[0].height || cams[v].width <= 0 || cams[v].height <= 0)
+            return fail(OCH_E_INVALID, "views must share one positive width and height");
+    if (int rs = check_ready(p)) return rs;
+    DeviceGuard g(p->device);
+    // one whole-frame render, natural 8x8-tile order, every workgroup timed
+    const int W = cams[0].width, H = cams[0].height;
+    const uint32_t tiles_x = (uint32_t)(W + 7) / 8, tiles_y = (uint32_t)(H + 7) / 8;
+    const uint32_t tiles = (uint32_t)n_views * tiles_x * tiles_y, per_block = (uint32_t)p->opt_block / 64;
+    const uint32_t n_blocks = (tiles + per_block - 1) / per_block;
+    const size_t frame_bytes = ((size_t)n_views * H * W * 4 + 255) & ~(size_t)255;
+    int st = ensure_scratch(p, frame_bytes + (size_t)n_blocks * 4);
+    if (st != OCH_OK) return st;
+    uint32_t *cost = reinterpret_cast<uint32_t *>(static_cast<char *>(p->d_scratch) + frame_bytes);
+    och::DevFrame f;
+    for (int v = 0; v < n_views; ++v) f.cams[v] = cams[v];
+    f.n_views = n_views;
+    f.palette = p->d_palette;
+    f.n_voxels = p->n_voxels;
+    f.out = static_cast<uint32_t *>(p->d_scratch);
+    f.codes = nullptr;
+    f.row_chunk = H;
+    f.shard = 0;
+    f.n_shards = 1;
+    f.slice_rows = H;
+    f.chunk_map = nullptr;
+    och::Schedule sc = p->schedule();
+    sc.kind = 0;
+    sc.tile_order = 0;
+    sc.cost = cost;
+    OCH_HIP(och::launch_render(p->dev(), f, sc, p->stream()));
+    std::vector<uint32_t> c(n_blocks);
+    OCH_HIP(hipMemcpyAsync(c.data(), cost, (size_t)n_blocks * 4, hipMemcpyDeviceToHost, p->stream()));
+    OCH_HIP(hipStreamSynchronize(p->stream()));
+    // a workgroup's time spread over its tiles, a tile's over its 8 rows
+    const int n_chunks = (H + row_chunk - 1) / row_chunk;
+    std::vector<double> acc(n_chunks, 0.0);
+    for (uint32_t b = 0; b < n_blocks; ++b)
+        for (uint32_t t = b * per_block; t < std::min(tiles, (b + 1) * per_block); ++t) {
+            const uint32_t ty = (t % (tiles_x * tiles_y)) / tiles_x;
+            const int r0 = (int)ty * 8, r1 = std::min(H, r0 + 8);
+            for (int r = r0; r < r1; ++r) acc[r / row_chunk] += (double)c[b] / per_block / (r1 - r0);
+        }
+    for (int k = 0; k < n_chunks; ++k) costs[k] = (float)acc[k];
+    return OCH_OK;
+}
+
+OCH_API int och_deal_chunks(const float *costs, int n_chunks, int n_shards, const float *weights, int32_t *chunk_shard)
+{
+    if (!costs || !chunk_shard || n_chunks <= 0 || n_shards <= 0) return fail(OCH_E_INVALID, "bad deal arguments");
+    std::vector<double> w(n_shards, 1.0);
+    double w_sum = 0.0, w_max = 0.0;
+    for (int s = 0; s < n_shards; ++s) {
+        if (weights) w[s] = weights[s];
+        if (!(w[s] > 0.0)) return fail(OCH_E_INVALID, "shard %d weight %g is not positive", s, w[s]);
+        w_sum += w[s];
+        w_max = std::max(w_max, w[s]);
+    }
+    // a shard holds at most its weighted share of the chunks plus two, which
+    // bounds the padding of the equal-size slices an all-gather needs
+    const int cap = (int)std::ceil(n_chunks * w_max / w_sum) + 2;
+    std::vector<int> order(n_chunks);
+    for (int k = 0; k < n_chunks; ++k) order[k] = k;
+    std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return costs[a] > costs[b]; });
+    std::vector<double> load(n_shards, 0.0);
+    std::vector<int> count(n_shards, 0);
+    for (int k : order) {             // longest processing time first, onto the least loaded shard (per weight)
+        int best = -1;
+        double best_score = 0.0;
+        for (int s = 0; s < n_shards; ++s) {
+            if (count[s] >= cap) continue;
+            const double score = (load[s] + std::max(0.0f, costs[k])) / w[s];
+            if (best < 0 || score < best_score || (score == best_score && count[s] < count[best])) {
+                best = s;
+                best_score = score;
+            }
+        }
+        chunk_shard[k] = best;
+        load[best] += std::max(0.0f, costs[k]);
+        ++count[best];
     }
     return OCH_OK;
 }
@@ -1311,7 +1469,8 @@ OCH_API int och_gpu_shade_unshard_views_dev(och_gpu_pool *p, const uint8_t *gath
         return fail(OCH_E_INVALID, "no code table: set a palette of at most %d voxel ids", OCH_CODE_MAX_VOXELS);
     DeviceGuard g(p->device);
     OCH_HIP(och::launch_shade_unshard(gathered, frames, p->d_code_table, width, height, row_chunk, n_shards,
-                                      och_shard_rows(height, row_chunk, n_shards), n_views, p->stream()));
+                                      p->slice_rows(height, row_chunk, n_shards), n_views,
+                                      p->deal_for(height, row_chunk, n_shards) ? p->d_owner : nullptr, p->stream()));
     return OCH_OK;
 }
 
@@ -1329,7 +1488,8 @@ OCH_API int och_gpu_unshard_views_dev(och_gpu_pool *p, const uint32_t *gathered,
         return fail(OCH_E_INVALID, "bad unshard arguments");
     DeviceGuard g(p->device);
     OCH_HIP(och::launch_unshard(gathered, frames, width, height, row_chunk, n_shards,
-                                och_shard_rows(height, row_chunk, n_shards), n_views, p->stream()));
+                                p->slice_rows(height, row_chunk, n_shards), n_views,
+                                p->deal_for(height, row_chunk, n_shards) ? p->d_owner : nullptr, p->stream()));
     return OCH_OK;
 }
 

@@ -118,7 +118,9 @@ void free_buffers(och_frame_group *g)
 // Buffers for n_views frames of W x H, slices of rows x W in `elem`-byte pixels.
 int ensure_buffers(och_frame_group *g, int W, int H, int n_views, int row_chunk, size_t elem)
 {
-    const size_t rows = (size_t)och_shard_rows(H, row_chunk, g->n);
+    int slice_rows = 0;
+    if (och_gpu_slice_rows(g->pools[0], H, row_chunk, g->n, &slice_rows) != OCH_OK) return OCH_E_INVALID;
+    const size_t rows = (size_t)slice_rows;
     const size_t slice = (size_t)n_views * rows * W * elem;
     const size_t frame = (size_t)n_views * H * W * 4;
     if (slice <= g->slice_bytes && frame <= g->frame_bytes) return OCH_OK;
@@ -249,7 +251,19 @@ OCH_API int och_frame_group_set_option(och_frame_group *g, int option, int value
 
 OCH_API int och_frame_group_plan(och_frame_group *g, const och_camera *cams, int n_views, int row_chunk)
 {
-    if (!g || !cams) return group_fail(OCH_E_INVALID, "NULL argument");
+    if (!g || !cams || row_chunk < 1 || n_views < 1) return group_fail(OCH_E_INVALID, "bad plan arguments");
+    if (g->n > 1) {
+        // deal the row chunks by their cost in one timed render of these views
+        // (device 0), instead of round-robin, so every device gets an equal share
+        const int H = cams[0].height, n_chunks = (H + row_chunk - 1) / row_chunk;
+        std::vector<float> costs(n_chunks);
+        std::vector<int32_t> deal(n_chunks);
+        int st = och_gpu_chunk_costs(g->pools[0], cams, n_views, row_chunk, costs.data());
+        if (st == OCH_OK) st = och_deal_chunks(costs.data(), n_chunks, g->n, nullptr, deal.data());
+        for (int r = 0; r < g->n && st == OCH_OK; ++r)
+            st = och_gpu_set_row_deal(g->pools[r], H, row_chunk, g->n, deal.data());
+        if (st != OCH_OK) return st;
+    }
     for (int r = 0; r < g->n; ++r) {
         int st = och_gpu_plan_views(g->pools[r], cams, n_views, row_chunk, r, g->n);
         if (st == OCH_OK) st = och_gpu_set_option(g->pools[r], OCH_OPT_TILE_ORDER, 2);
@@ -270,8 +284,10 @@ OCH_API int och_frame_group_render(och_frame_group *g, const och_camera *cams, i
     const bool codes = n_vox <= OCH_CODE_MAX_VOXELS;
     st = ensure_buffers(g, W, H, n_views, row_chunk, codes ? 1 : 4);
     if (st != OCH_OK) return st;
-    const size_t rows = (size_t)och_shard_rows(H, row_chunk, g->n);
-    const size_t count = (size_t)n_views * rows * W;
+    int slice_rows = 0;
+    st = och_gpu_slice_rows(g->pools[0], H, row_chunk, g->n, &slice_rows);
+    if (st != OCH_OK) return st;
+    const size_t count = (size_t)n_views * slice_rows * W;
     for (int r = 0; r < g->n && st == OCH_OK; ++r)
         st = codes ? och_gpu_render_codes_views_dev(g->pools[r], cams, n_views, static_cast<uint8_t *>(g->slice[r]),
                                                     row_chunk, r, g->n, bounce)

@@ -108,6 +108,7 @@ struct DevFrame {
     uint32_t *out;            // n_views compact slices, each slice_rows x width (RGBA8)
     uint8_t *codes;           // or the same slices as indexed colour (launch_render_codes)
     int32_t row_chunk, shard, n_shards, slice_rows;
+    const int32_t *chunk_map; // row deal: this shard's global chunk per local chunk (-1 = padding), or null
 };
 
 // Threads per workgroup of the config-5 (bounce) kernels: compaction spans
@@ -156,9 +157,12 @@ hipError_t launch_render(const DevPool &p, const DevFrame &f, const Schedule &sc
 // Indexed-colour frames (OCH_CODE_*): render into f.codes, and turn gathered
 // code slices into RGBA8 frames through a 256-entry table.
 hipError_t launch_render_codes(const DevPool &p, const DevFrame &f, const Schedule &sc, bool bounce, hipStream_t stream);
+// owner: the row deal's table (global chunk -> shard << 16 | local chunk), or
+// null for round-robin chunks.
 hipError_t launch_shade_unshard(const uint8_t *gathered, uint32_t *frames, const uint32_t *table, int width, int height,
-                                int row_chunk, int n_shards, int slice_rows, int n_views, hipStream_t stream);
+                                int row_chunk, int n_shards, int slice_rows, int n_views, const int32_t *owner,
+                                hipStream_t stream);
 hipError_t launch_unshard(const uint32_t *gathered, uint32_t *frames, int width, int height, int row_chunk,
-                          int n_shards, int slice_rows, int n_views, hipStream_t stream);
+                          int n_shards, int slice_rows, int n_views, const int32_t *owner, hipStream_t stream);
 
 }  // namespace och

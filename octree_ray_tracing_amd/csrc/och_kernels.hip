@@ -799,6 +799,16 @@ struct CameraSource {
     int32_t n_views, row_chunk, shard, n_shards, slice_rows, width, height, order;
     uint32_t tiles_x, supertiles_x, per_view, slice_pixels;
     FastDiv by_per_view, by_tiles_x, by_supertiles_x, by_row_chunk;
+    // Row deal (och_gpu_set_row_deal): the global chunk of each of this
+    // shard's local chunks, -1 past its last; null = round-robin.
+    const int32_t *chunk_map;
+    // Global row of local chunk `chunk`, row `within` of it; height (no ray)
+    // for a padding chunk of a dealt slice.
+    __device__ __forceinline__ int global_row(int chunk, int within) const
+    {
+        const int g = chunk_map ? chunk_map[chunk] : chunk * n_shards + shard;
+        return g < 0 ? height : g * row_chunk + within;
+    }
     __host__ __device__ __forceinline__ uint32_t count() const { return per_view * (uint32_t)n_views; }
     // Tile of ray i (tile-granular index math, identical in get and get_wave).
     __device__ __forceinline__ void tile_of(uint32_t i, uint32_t &view, uint32_t &tx, uint32_t &ty) const
@@ -834,7 +844,7 @@ struct CameraSource {
         const int srow = (int)(ty * kTileH + lane / kTileW);
         if (col >= width || srow >= slice_rows) return false;
         const int chunk = (int)by_row_chunk.div((uint32_t)srow), within = srow - chunk * row_chunk;
-        return finish(view, col, srow, (chunk * n_shards + shard) * row_chunk + within, o, d, out);
+        return finish(view, col, srow, global_row(chunk, within), o, d, out);
     }
     // One wave's tile: wave_base (a multiple of 64, wave-uniform) moves the
     // tile arithmetic, divisions included, to the scalar unit.
@@ -880,10 +890,10 @@ struct CameraSource {
         if (col >= width || srow >= slice_rows) return false;
         if (row_chunk % (int)kTileH == 0) {                // the tile lies inside one row chunk
             const int chunk = __builtin_amdgcn_readfirstlane((int)by_row_chunk.div((uint32_t)srow0));
-            row = (chunk * n_shards + shard) * row_chunk + (srow - chunk * row_chunk);
+            row = global_row(chunk, srow - chunk * row_chunk);
         } else {
             const int chunk = (int)by_row_chunk.div((uint32_t)srow);
-            row = (chunk * n_shards + shard) * row_chunk + (srow - chunk * row_chunk);
+            row = global_row(chunk, srow - chunk * row_chunk);
         }
         return row < height;
     }
@@ -915,10 +925,10 @@ struct CameraSource {
             const int ca = __builtin_amdgcn_readfirstlane((int)by_row_chunk.div(tya * kTileH));
             const int cb = __builtin_amdgcn_readfirstlane((int)by_row_chunk.div(tyb * kTileH));
             const int chunk = in_a ? ca : cb;
-            row = (chunk * n_shards + shard) * row_chunk + (srow - chunk * row_chunk);
+            row = global_row(chunk, srow - chunk * row_chunk);
         } else {
             const int chunk = (int)by_row_chunk.div((uint32_t)srow);
-            row = (chunk * n_shards + shard) * row_chunk + (srow - chunk * row_chunk);
+            row = global_row(chunk, srow - chunk * row_chunk);
         }
         return finish(view, col, srow, row, o, d, out);
     }
@@ -1360,16 +1370,33 @@ __global__ __launch_bounds__(256) void k_raygen(och_camera C, float *__restrict_
 }
 
 // gathered: [n_shards][n_views][slice_rows][width] -> frames: [n_views][height][width]
+// Source row of global row `row` in the gathered slices [n_shards][n_views]
+// [slice_rows][W]: round-robin chunks, or the row deal's owner table
+// (owner[gchunk] = shard << 16 | local chunk).
+__device__ __forceinline__ size_t gathered_row(int row, int row_chunk, int n_shards, int slice_rows, int n_views,
+                                               int view, const int32_t *__restrict__ owner)
+{
+    const int gchunk = row / row_chunk, within = row - gchunk * row_chunk;
+    int shard, lchunk;
+    if (owner) {
+        const int32_t w = owner[gchunk];
+        shard = w >> 16;
+        lchunk = w & 0xFFFF;
+    } else {
+        shard = gchunk % n_shards;
+        lchunk = gchunk / n_shards;
+    }
+    return ((size_t)shard * n_views + view) * slice_rows + (size_t)lchunk * row_chunk + within;
+}
+
 __global__ __launch_bounds__(256) void k_unshard(const uint32_t *__restrict__ gathered, uint32_t *__restrict__ frames,
                                                  int width, int height, int row_chunk, int n_shards, int slice_rows,
-                                                 int n_views)
+                                                 int n_views, const int32_t *__restrict__ owner)
 {
     const int col = blockIdx.x * 256 + threadIdx.x;
     const int row = blockIdx.y, view = blockIdx.z;
     if (col >= width || row >= height) return;
-    const int gchunk = row / row_chunk, within = row - gchunk * row_chunk;
-    const int shard = gchunk % n_shards, lchunk = gchunk / n_shards;
-    const size_t src = (((size_t)shard * n_views + view) * slice_rows + (size_t)lchunk * row_chunk + within) * width + col;
+    const size_t src = gathered_row(row, row_chunk, n_shards, slice_rows, n_views, view, owner) * width + col;
     frames[((size_t)view * height + row) * width + col] = gathered[src];
 }
 
@@ -1378,7 +1405,8 @@ __global__ __launch_bounds__(256) void k_unshard(const uint32_t *__restrict__ ga
 // code_table: palette words, the fixed colours, the halved blocked variants).
 __global__ __launch_bounds__(256) void k_shade_unshard(const uint8_t *__restrict__ gathered, uint32_t *__restrict__ frames,
                                                        const uint32_t *__restrict__ table, int width, int height,
-                                                       int row_chunk, int n_shards, int slice_rows, int n_views)
+                                                       int row_chunk, int n_shards, int slice_rows, int n_views,
+                                                       const int32_t *__restrict__ owner)
 {
     __shared__ uint32_t lut[256];
     lut[threadIdx.x] = table[threadIdx.x];
@@ -1386,9 +1414,7 @@ __global__ __launch_bounds__(256) void k_shade_unshard(const uint8_t *__restrict
     const int col = blockIdx.x * 256 + threadIdx.x;
     const int row = blockIdx.y, view = blockIdx.z;
     if (col >= width || row >= height) return;
-    const int gchunk = row / row_chunk, within = row - gchunk * row_chunk;
-    const int shard = gchunk % n_shards, lchunk = gchunk / n_shards;
-    const size_t src = (((size_t)shard * n_views + view) * slice_rows + (size_t)lchunk * row_chunk + within) * width + col;
+    const size_t src = gathered_row(row, row_chunk, n_shards, slice_rows, n_views, view, owner) * width + col;
     frames[((size_t)view * height + row) * width + col] = lut[gathered[src]];
 }
 
@@ -1397,7 +1423,8 @@ __global__ __launch_bounds__(256) void k_shade_unshard(const uint8_t *__restrict
 // launches of the frames in flight).
 __global__ __launch_bounds__(256) void k_shade_unshard4(const uint8_t *__restrict__ gathered, uint32_t *__restrict__ frames,
                                                         const uint32_t *__restrict__ table, int width, int height,
-                                                        int row_chunk, int n_shards, int slice_rows, int n_views)
+                                                        int row_chunk, int n_shards, int slice_rows, int n_views,
+                                                        const int32_t *__restrict__ owner)
 {
     __shared__ uint32_t lut[256];
     lut[threadIdx.x] = table[threadIdx.x];
@@ -1405,9 +1432,7 @@ __global__ __launch_bounds__(256) void k_shade_unshard4(const uint8_t *__restric
     const int col = (blockIdx.x * 256 + threadIdx.x) * 4;
     const int row = blockIdx.y, view = blockIdx.z;
     if (col >= width || row >= height) return;
-    const int gchunk = row / row_chunk, within = row - gchunk * row_chunk;
-    const int shard = gchunk % n_shards, lchunk = gchunk / n_shards;
-    const size_t src = (((size_t)shard * n_views + view) * slice_rows + (size_t)lchunk * row_chunk + within) * width + col;
+    const size_t src = gathered_row(row, row_chunk, n_shards, slice_rows, n_views, view, owner) * width + col;
     // streaming accesses: the codes are read once and the frame is not read
     // back here, so neither should evict the DAG's lines from L2 / MALL
     const uint32_t c = __builtin_nontemporal_load(reinterpret_cast<const uint32_t *>(gathered + src));
@@ -1520,6 +1545,7 @@ CameraSource camera_source(const DevFrame &f, const Schedule &sc)
     src.by_tiles_x.init(src.tiles_x);
     src.by_supertiles_x.init(src.supertiles_x);
     src.by_row_chunk.init((uint32_t)src.row_chunk);
+    src.chunk_map = f.chunk_map;
     return src;
 }
 
@@ -1609,18 +1635,19 @@ hipError_t launch_render_codes(const DevPool &p, const DevFrame &f, const Schedu
 }
 
 hipError_t launch_shade_unshard(const uint8_t *gathered, uint32_t *frames, const uint32_t *table, int width, int height,
-                                int row_chunk, int n_shards, int slice_rows, int n_views, hipStream_t stream)
+                                int row_chunk, int n_shards, int slice_rows, int n_views, const int32_t *owner,
+                                hipStream_t stream)
 {
     const bool vec4 = width % 4 == 0 && ((uintptr_t)gathered & 3u) == 0 && ((uintptr_t)frames & 15u) == 0;
     if (vec4) {
         const dim3 grid((width / 4 + 255) / 256, height, n_views);
         hipLaunchKernelGGL(k_shade_unshard4, grid, dim3(256), 0, stream, gathered, frames, table, width, height,
-                           row_chunk, n_shards, slice_rows, n_views);
+                           row_chunk, n_shards, slice_rows, n_views, owner);
         return hipGetLastError();
     }
     const dim3 grid((width + 255) / 256, height, n_views);
     hipLaunchKernelGGL(k_shade_unshard, grid, dim3(256), 0, stream, gathered, frames, table, width, height, row_chunk,
-                       n_shards, slice_rows, n_views);
+                       n_shards, slice_rows, n_views, owner);
     return hipGetLastError();
 }
 
@@ -1651,11 +1678,11 @@ hipError_t launch_scatter_slots(const uint32_t *ids, const uint32_t *raw, const 
 }
 
 hipError_t launch_unshard(const uint32_t *gathered, uint32_t *frames, int width, int height, int row_chunk,
-                          int n_shards, int slice_rows, int n_views, hipStream_t stream)
+                          int n_shards, int slice_rows, int n_views, const int32_t *owner, hipStream_t stream)
 {
     const dim3 grid((width + 255) / 256, height, n_views);
     hipLaunchKernelGGL(k_unshard, grid, dim3(256), 0, stream, gathered, frames, width, height, row_chunk, n_shards,
-                       slice_rows, n_views);
+                       slice_rows, n_views, owner);
     return hipGetLastError();
 }
 

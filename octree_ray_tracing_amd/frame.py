@@ -19,21 +19,35 @@ from ._lib import Camera, call
 from .tracer import GpuPool, shard_rows
 
 
-def slice_row_map(height: int, row_chunk: int, n_shards: int, shard: int) -> np.ndarray:
-    """Global row of each row of `shard`'s compact slice (-1 = padding)."""
-    rows = shard_rows(height, row_chunk, n_shards)
+def deal_slice_rows(height: int, row_chunk: int, n_shards: int, deal=None) -> int:
+    """Rows per slice: och_shard_rows, or the largest shard's chunks under a row deal."""
+    if deal is None:
+        return shard_rows(height, row_chunk, n_shards)
+    deal = np.asarray(deal)
+    return int(max(1, np.bincount(deal, minlength=n_shards).max())) * row_chunk
+
+
+def slice_row_map(height: int, row_chunk: int, n_shards: int, shard: int, deal=None) -> np.ndarray:
+    """Global row of each row of `shard`'s compact slice (-1 = padding).
+    deal: chunk -> shard (och_gpu_set_row_deal), or None for round-robin."""
+    rows = deal_slice_rows(height, row_chunk, n_shards, deal)
     local = np.arange(rows)
-    gchunk = (local // row_chunk) * n_shards + shard
+    if deal is None:
+        gchunk = (local // row_chunk) * n_shards + shard
+    else:
+        mine = np.nonzero(np.asarray(deal) == shard)[0]
+        lchunk = local // row_chunk
+        gchunk = np.where(lchunk < mine.size, mine[np.minimum(lchunk, max(mine.size - 1, 0))] if mine.size else -1, -1)
     g = gchunk * row_chunk + local % row_chunk
-    return np.where(g < height, g, -1)
+    return np.where((gchunk >= 0) & (g < height), g, -1)
 
 
-def unshard_host(gathered: np.ndarray, height: int, row_chunk: int) -> np.ndarray:
+def unshard_host(gathered: np.ndarray, height: int, row_chunk: int, deal=None) -> np.ndarray:
     """Host restatement of the unshard kernel: (n, rows, W) slices -> (H, W) frame."""
     n, rows, width = gathered.shape
     frame = np.zeros((height, width), gathered.dtype)
     for s in range(n):
-        m = slice_row_map(height, row_chunk, n, s)
+        m = slice_row_map(height, row_chunk, n, s, deal)
         ok = m >= 0
         frame[m[ok]] = gathered[s][ok]
     return frame
@@ -52,7 +66,7 @@ class ShardedFrame:
 
     def __init__(self, pool: GpuPool, width: int, height: int, row_chunk: int = 8, n_views: int = 1, group=None,
                  indexed: bool = False, shard: tuple[int, int] | None = None, shade: str = "all",
-                 direct: bool = False):
+                 direct: bool = False, deal=None):
         import torch
         import torch.distributed as dist
 
@@ -67,7 +81,12 @@ class ShardedFrame:
         if self.proxy:
             self.rank, self.world = shard
             assert 0 <= self.rank < self.world
-        self.rows = shard_rows(height, row_chunk, self.world)
+        # deal: the row chunk -> rank table (och_gpu_set_row_deal; every rank
+        # must pass the same one), None for round-robin chunks
+        self.deal = None if deal is None else np.ascontiguousarray(deal, np.int32)
+        if self.world > 1 or self.deal is not None:
+            pool.set_row_deal(height, row_chunk, self.world, self.deal)
+        self.rows = pool.slice_rows(height, row_chunk, self.world)
         # indexed=True: ranks render and exchange 1-byte colour codes (OCH_CODE_*)
         # and shade after the gather -- a quarter of the RGBA8 bytes on xGMI,
         # the same frames (needs a palette of <= CODE_MAX_VOXELS ids).

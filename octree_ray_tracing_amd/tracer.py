@@ -289,6 +289,31 @@ class GpuPool:
         call("och_gpu_render_bounce_views_dev", self._h, C.cast(arr, C.c_void_p), len(cams), _dev_ptr(rgba_slices),
              int(row_chunk), int(shard), int(n_shards))
 
+    # Row deal (och_gpu_set_row_deal): which shard renders each row chunk.
+    def set_row_deal(self, height: int, row_chunk: int, n_shards: int, chunk_shard=None):
+        """chunk_shard[g] = shard of row chunk g (None = round-robin) for frames of this geometry."""
+        if chunk_shard is None:
+            call("och_gpu_set_row_deal", self._h, int(height), int(row_chunk), int(n_shards), None)
+            return
+        deal = np.ascontiguousarray(chunk_shard, np.int32).reshape(-1)
+        if deal.size != -(-int(height) // int(row_chunk)):
+            raise ValueError("one shard per row chunk expected")
+        call("och_gpu_set_row_deal", self._h, int(height), int(row_chunk), int(n_shards), _np_ptr(deal))
+
+    def slice_rows(self, height: int, row_chunk: int, n_shards: int) -> int:
+        """Rows per slice for this geometry under the pool's deal (och_gpu_slice_rows)."""
+        v = C.c_int()
+        call("och_gpu_slice_rows", self._h, int(height), int(row_chunk), int(n_shards), C.byref(v))
+        return v.value
+
+    def chunk_costs(self, cams, row_chunk: int) -> np.ndarray:
+        """Per-row-chunk cost of these views from one timed render (och_gpu_chunk_costs)."""
+        cams = list(cams) if isinstance(cams, (list, tuple)) else [cams]
+        arr = (Camera * len(cams))(*cams)
+        out = np.empty(-(-cams[0].height // int(row_chunk)), np.float32)
+        call("och_gpu_chunk_costs", self._h, C.cast(arr, C.c_void_p), len(cams), int(row_chunk), _np_ptr(out))
+        return out
+
     def unshard_dev(self, gathered, frame, width: int, height: int, row_chunk: int, n_shards: int, n_views: int = 1):
         call("och_gpu_unshard_views_dev", self._h, _dev_ptr(gathered), _dev_ptr(frame), int(width), int(height),
              int(row_chunk), int(n_shards), int(n_views))
@@ -313,6 +338,17 @@ class GpuPool:
 
 def shard_rows(height: int, row_chunk: int, n_shards: int) -> int:
     return call("och_shard_rows", int(height), int(row_chunk), int(n_shards))
+
+
+def deal_chunks(costs, n_shards: int, weights=None) -> np.ndarray:
+    """och_deal_chunks: row chunks dealt longest-first onto the least loaded shard per weight."""
+    costs = np.ascontiguousarray(costs, np.float32).reshape(-1)
+    out = np.empty(costs.size, np.int32)
+    w = None if weights is None else np.ascontiguousarray(weights, np.float32).reshape(-1)
+    if w is not None and w.size != n_shards:
+        raise ValueError("one weight per shard expected")
+    call("och_deal_chunks", _np_ptr(costs), costs.size, int(n_shards), None if w is None else _np_ptr(w), _np_ptr(out))
+    return out
 
 
 class HOctree(GpuPool):

@@ -115,23 +115,44 @@ def test_bench_instance_d12_1080p(ort, O, gpu_device, d12, d12_ref, pal):
     pool.close()
 
 
-def test_config4_2160p_as_8_shards(ort, O, gpu_device, d12, d12_ref, pal):
-    """configs[3]: 3840x2160, rows dealt in 8-row chunks over 8 shards, gathered, shaded."""
+@pytest.mark.parametrize("deal", ["rr", "cost"])
+def test_config4_2160p_as_8_shards(ort, O, gpu_device, d12, d12_ref, pal, deal):
+    """configs[3]: 3840x2160, rows in 8-row chunks over 8 shards -- round-robin,
+    or dealt by cost as bench.py deals them at N > 1 (och_gpu_chunk_costs +
+    och_deal_chunks, rank 0 at weight 0.9; padded slices) -- rendered in the
+    planned order, gathered, shaded; config 5 too with the deal."""
     import torch
     W, H, n, chunk = 3840, 2160, 8, 8
     pool = ort.HOctree(d12.nodes, d12.root, 12, device=0)
     pool.set_palette(pal)
     pool.set_stream(torch.cuda.current_stream())
     cams = [ort.camera(tuple(ORIGIN), YAW, p, FOV, W, H) for p in PITCHES]
-    rows = ort.shard_rows(H, chunk, n)
-    gathered = torch.full((n, 2, rows, W), 255, dtype=torch.uint8, device="cuda")
-    for s in range(n):
-        pool.render_codes_views_dev(cams, gathered[s], chunk, s, n)
-    frames = torch.empty((2, H, W), dtype=torch.int32, device="cuda")
-    pool.shade_unshard_dev(gathered, frames, W, H, chunk, n, 2)
-    torch.cuda.synchronize()
-    want = oracle_frames(O, d12_ref, pal, W, H)
-    assert_frames(frames, want)
+    table = None
+    if deal == "cost":
+        table = ort.deal_chunks(pool.chunk_costs(cams, chunk), n, [0.9] + [1.0] * 7)
+        assert np.bincount(table, minlength=n).min() > 0
+    pool.set_row_deal(H, chunk, n, table)
+    rows = pool.slice_rows(H, chunk, n)
+    assert rows == (ort.shard_rows(H, chunk, n) if table is None else int(np.bincount(table).max()) * chunk)
+    pool.set_option("tile_order", 2)
+    for bounce in (False, True) if deal == "cost" else (False,):
+        gathered = torch.full((n, 2, rows, W), 255, dtype=torch.uint8, device="cuda")
+        for s in range(n):
+            pool.plan_views(cams, chunk, s, n)
+            pool.render_codes_views_dev(cams, gathered[s], chunk, s, n, bounce)
+        frames = torch.empty((2, H, W), dtype=torch.int32, device="cuda")
+        pool.shade_unshard_dev(gathered, frames, W, H, chunk, n, 2)
+        torch.cuda.synchronize()
+        assert_frames(frames, oracle_frames(O, d12_ref, pal, W, H, bounce=bounce))
+    if table is not None:
+        # RGBA8 slices through the same deal
+        g32 = torch.zeros((n, 2, rows, W), dtype=torch.int32, device="cuda")
+        for s in range(n):
+            pool.render_views_dev(cams, g32[s], chunk, s, n)
+        frames = torch.empty((2, H, W), dtype=torch.int32, device="cuda")
+        pool.unshard_dev(g32, frames, W, H, chunk, n, 2)
+        torch.cuda.synchronize()
+        assert_frames(frames, oracle_frames(O, d12_ref, pal, W, H))
     pool.close()
 
 
