@@ -351,11 +351,13 @@ def main():
                     help="N > 1: every rank all-gathers the frame's codes; 'display' = only rank 0 (the display) "
                          "expands them to RGBA8 frames, 'all' = every rank does")
     ap.add_argument("--no-cull-off", action="store_true", help="skip the cull-off window (value_cull_off)")
-    ap.add_argument("--deal", choices=("cost", "rr"), default="cost",
+    ap.add_argument("--deal", choices=("cost", "count", "rr"), default="count",
                     help="N > 1: row chunks dealt by their cost in one timed render on rank 0 (och_gpu_chunk_costs "
-                         "+ och_deal_chunks), or round-robin")
-    ap.add_argument("--display-weight", type=float, default=0.9,
-                    help="N > 1 with --shade display: rank 0's share of the render work per rank (it also shades)")
+                         "+ och_deal_chunks), by count (rank 0 at --display-weight), or round-robin")
+    ap.add_argument("--display-weight", type=float, default=None,
+                    help="N > 1 with --shade display: rank 0's share of the row chunks relative to the other ranks "
+                         "(it also shades the whole frame); default 1 - 0.05 N, from tools/proxy_rank.py sweeps "
+                         "(DESIGN.md §5)")
     ap.add_argument("--no-direct", action="store_true",
                     help="N = 1: render codes and shade them in a second pass, as ranks do at N > 1, instead of "
                          "the fused launch writing the RGBA8 frames directly")
@@ -408,12 +410,15 @@ def main():
     # least loaded rank (rank 0, which also shades for the display, counts its
     # share at --display-weight); every rank gets the same table.
     deal = None
-    if world > 1 and a.deal == "cost":
+    if a.display_weight is None:
+        a.display_weight = max(0.5, 1.0 - 0.05 * world)
+    if world > 1 and a.deal != "rr":
         n_chunks = -(-H // a.row_chunk)
         table = torch.zeros(n_chunks, dtype=torch.int32, device=dev)
         if rank == 0:
             w = [a.display_weight if a.shade == "display" else 1.0] + [1.0] * (world - 1)
-            table.copy_(torch.from_numpy(ort.deal_chunks(pool.chunk_costs(cams, a.row_chunk), world, w)))
+            costs = pool.chunk_costs(cams, a.row_chunk) if a.deal == "cost" else np.ones(n_chunks, np.float32)
+            table.copy_(torch.from_numpy(ort.deal_chunks(costs, world, w)))
         coll(dist.broadcast, table, 0)
         deal = table.cpu().numpy()
     # One frame buffer set and one HIP stream per frame in flight.
@@ -772,7 +777,7 @@ def main():
                        "parallelism": f"rows{world}",
                        "row_deal": (None if world == 1 else
                                     "round-robin 8-row chunks" if deal is None else
-                                    f"row chunks dealt by cost (one timed render on rank 0), rank 0 weight "
+                                    f"row chunks dealt by {a.deal} (och_deal_chunks), rank 0 weight "
                                     f"{a.display_weight if a.shade == 'display' else 1.0}; chunks per rank "
                                     f"{np.bincount(deal, minlength=world).tolist()}"),
                        "shade": ("every rank all-gathers the frame's codes; " +

@@ -66,7 +66,7 @@ class ShardedFrame:
 
     def __init__(self, pool: GpuPool, width: int, height: int, row_chunk: int = 8, n_views: int = 1, group=None,
                  indexed: bool = False, shard: tuple[int, int] | None = None, shade: str = "all",
-                 direct: bool = False, deal=None):
+                 direct: bool = False, deal=None, shade_stream=None):
         import torch
         import torch.distributed as dist
 
@@ -108,6 +108,15 @@ class ShardedFrame:
         self.slice = torch.empty((n_views, self.rows, width), dtype=dt, device=dev)
         self.gathered = torch.empty((self.world, n_views, self.rows, width), dtype=dt, device=dev)
         self.frames = torch.empty((n_views, height, width), dtype=torch.int32, device=dev)
+        # shade_stream (N > 1): the shade + unshard of the gathered frame runs on
+        # this stream, after an event on the gather, so the next frame's render
+        # on the frame's own stream does not wait for it; the next gather into
+        # this frame's buffer waits for the shade that read it
+        self.shade_stream = shade_stream if (self.world > 1 and not self.direct) else None
+        if self.shade_stream is not None:
+            self._gathered = torch.cuda.Event()
+            self._shaded = torch.cuda.Event()
+            self._shade_pending = False
         pool.set_stream(torch.cuda.current_stream())
 
     def render_local(self, cams, bounce: bool = False):
@@ -128,11 +137,14 @@ class ShardedFrame:
         return self.slice
 
     def exchange(self):
+        import torch
         import torch.distributed as dist
 
         if self.direct:
             return self.frames
         src = self.slice
+        if self.shade_stream is not None and self._shade_pending:
+            torch.cuda.current_stream().wait_event(self._shaded)   # the last shade has read `gathered`
         if self.proxy:
             # the bytes a gather lands in this rank's buffer, written on the
             # device (every slot gets this rank's slice; no xGMI time)
@@ -148,6 +160,22 @@ class ShardedFrame:
             src = self.gathered
         if self.shade == "display" and self.rank != 0:
             return None
+        if self.shade_stream is not None:
+            cur = torch.cuda.current_stream()
+            self._gathered.record(cur)
+            self.shade_stream.wait_event(self._gathered)
+            self.pool.set_stream(self.shade_stream)
+            try:
+                self._shade(src)
+                self._shaded.record(self.shade_stream)
+                self._shade_pending = True
+            finally:
+                self.pool.set_stream(cur)
+            return self.frames
+        self._shade(src)
+        return self.frames
+
+    def _shade(self, src):
         if self.indexed:
             self.pool.shade_unshard_dev(src, self.frames, self.width, self.height, self.row_chunk, self.world,
                                         self.n_views)

@@ -48,8 +48,9 @@ def main():
     ap.add_argument("--shards", default="0", help="'all', or a comma list of shards to time")
     ap.add_argument("--shade", choices=("display", "all"), default="display",
                     help="as bench.py: 'display' = only rank 0 shades the gathered frame")
-    ap.add_argument("--deal", choices=("cost", "rr"), default="cost", help="as bench.py")
-    ap.add_argument("--display-weight", type=float, default=0.9, help="as bench.py")
+    ap.add_argument("--deal", choices=("cost", "count", "rr"), default="count", help="as bench.py")
+    ap.add_argument("--display-weight", type=float, default=None, help="as bench.py (default 1 - 0.05 N)")
+    ap.add_argument("--shade-stream", action="store_true", help="as bench.py: the display rank shades on its own stream")
     a = ap.parse_args()
 
     import torch
@@ -79,18 +80,22 @@ def main():
         cams = [ort.camera((1.5, 1.5, 1.5), 0.3, p, 1.25, W, H) for p in (0.0, -0.6)]
         shards = list(range(world)) if a.shards == "all" else [int(x) for x in a.shards.split(",") if int(x) < world]
         deal = None
-        if world > 1 and a.deal == "cost":          # as bench.py: one timed render, chunks dealt by cost
-            w = [a.display_weight if a.shade == "display" else 1.0] + [1.0] * (world - 1)
-            deal = ort.deal_chunks(pool.chunk_costs(cams, 8), world, w)
+        w0 = max(0.5, 1.0 - 0.05 * world) if a.display_weight is None else a.display_weight
+        if world > 1 and a.deal != "rr":            # as bench.py: chunks dealt by cost (or count) per weight
+            w = [w0 if a.shade == "display" else 1.0] + [1.0] * (world - 1)
+            costs = pool.chunk_costs(cams, 8) if a.deal == "cost" else np.ones(-(-H // 8), np.float32)
+            deal = ort.deal_chunks(costs, world, w)
         if world > 1:
             pool.set_row_deal(H, 8, world, deal)
         for nf in [int(x) for x in a.inflight.split(",")]:
             streams = [base] + [torch.cuda.Stream() for _ in range(nf - 1)]
+            shade_stream = torch.cuda.Stream() if a.shade_stream else None
             per_shard = []
             for shard in shards:
                 pool.set_stream(base)
                 pool.plan_views(cams, 8, shard, world)
-                row = arm(a, torch, pool, streams, cams, W, H, world, shard, nf, opts, deal)
+                row = arm(a, torch, pool, streams, cams, W, H, world, shard, nf, opts, deal, shade_stream)
+                row["display_weight"] = w0
                 print(json.dumps(row), flush=True)
                 res.append(row)
                 per_shard.append(row)
@@ -118,14 +123,14 @@ def main():
     pool.close()
 
 
-def arm(a, torch, pool, streams, cams, W, H, world, shard, nf, opts, deal=None):
+def arm(a, torch, pool, streams, cams, W, H, world, shard, nf, opts, deal=None, shade_stream=None):
     """One shard's pipelined steps: 20-step windows (median) and sustained runs."""
     from octree_ray_tracing_amd.frame import ShardedFrame, slice_row_map
     sfs = []
     for s_ in streams:
         with torch.cuda.stream(s_):
             sfs.append(ShardedFrame(pool, W, H, 8, n_views=2, indexed=True, shard=(shard, world),
-                                    shade=a.shade, deal=deal))
+                                    shade=a.shade, deal=deal, shade_stream=shade_stream))
     rows = sfs[0].rows
     rays_rank = int((slice_row_map(H, 8, world, shard, deal) >= 0).sum()) * W * 2
 
@@ -152,7 +157,7 @@ def arm(a, torch, pool, streams, cams, W, H, world, shard, nf, opts, deal=None):
     sus = [run(a.sustain_steps) for _ in range(3)]
     row = {"world": world, "shard": shard, "frame": f"{W}x{H}", "inflight": nf, "opts": opts,
            "exchange": not a.no_exchange, "shade": a.shade, "shades": a.shade == "all" or shard == 0,
-           "deal": a.deal, "display_weight": a.display_weight,
+           "deal": a.deal, "shade_stream": a.shade_stream,
            "events": a.events, "rays_per_step_rank": rays_rank, "slice_rows": rows,
            "ms_per_step_20": round(statistics.median(wins) / a.steps * 1e3, 4),
            "mrays_s_rank_20": round(rays_rank * a.steps / statistics.median(wins) / 1e6, 1),
