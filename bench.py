@@ -576,10 +576,16 @@ def main():
         if marked:
             mark()
         if world > 1:
-            every = torch.zeros(world, dtype=torch.float64, device=dev)
-            coll(dist.all_gather_into_tensor, every, el)
-            rank_s.append(every.tolist())
-            return float(every.max().item())
+            if dist.get_backend() == "gloo":               # the rehearsal backend: host tensors
+                outs = [torch.zeros(1, dtype=torch.float64) for _ in range(world)]
+                dist.all_gather(outs, el.cpu())
+                every = [float(o.item()) for o in outs]
+            else:
+                buf = torch.zeros(world, dtype=torch.float64, device=dev)
+                dist.all_gather_into_tensor(buf, el)
+                every = buf.tolist()
+            rank_s.append(every)
+            return max(every)
         rank_s.append([float(el.item())])
         return float(el.item())
 
