@@ -164,12 +164,16 @@ typedef enum och_option {
     OCH_OPT_BOUNCE_COMPACT = 6,/* config 5: 1 (default) = compact each block's secondary rays into its first lanes
                                   (wave ballot/popcount + LDS queue) before tracing them; 0 = trace in place */
     OCH_OPT_CHUNK_TILES = 7,   /* schedule 2: 64-ray tiles per wave, a power of two in 1..64 (default 4) */
-    OCH_OPT_CULL = 8           /* 1 (default) = a ray whose walk provably never enters the bounding box of the
+    OCH_OPT_CULL = 8,          /* 1 (default) = a ray whose walk provably never enters the bounding box of the
                                   pool's voxels (och_pool_occupied_box) is recorded as the miss it would end in,
                                   without walking (camera rays: a cheaper conservative test first, before the
                                   ray's setup); exact, for launches that do not count
                                   PUSHes.  0 = every ray walks.  2 = diagnostic: launches that count PUSHes
                                   cull too, a culled ray counting 0 (the PUSHes the culled launch walks) */
+    OCH_OPT_MERGE = 9          /* K > 0: grid launches without PUSH counts on the packed layout, with a block of
+                                  128..1024 threads, merge the block's waves every K iterations: the rays left
+                                  move into the free lanes of the fewest waves, the emptied waves exit (records
+                                  unchanged).  0 (default) = off */
 } och_option;
 OCH_API int och_gpu_set_option(och_gpu_pool *pool, int option, int value);
 OCH_API int och_gpu_get_option(const och_gpu_pool *pool, int option, int *value);

@@ -156,6 +156,7 @@ struct och_gpu_pool {
     int opt_tile_order = 0;
     int opt_bounce_compact = 1;
     int opt_cull = 1;
+    int opt_merge = 0;
     // bounding box of the pool's voxels (voxel units, [lo, hi)), for the cull
     bool box_any = false;
     int32_t box_lo[3] = {0, 0, 0}, box_hi[3] = {0, 0, 0};
@@ -201,6 +202,7 @@ struct och_gpu_pool {
         sc.stamp_cap = stamp_cap;
         sc.order = nullptr;
         sc.cost = nullptr;
+        sc.merge_k = opt_merge;
         return sc;
     }
 
@@ -891,6 +893,10 @@ OCH_API int och_gpu_set_option(och_gpu_pool *p, int option, int value)
         if (value < 0 || value > 2) return fail(OCH_E_INVALID, "cull must be 0, 1 or 2");
         p->opt_cull = value;
         return OCH_OK;
+    case OCH_OPT_MERGE:
+        if (value < 0 || value > 4096) return fail(OCH_E_INVALID, "merge rounds %d outside 0..4096", value);
+        p->opt_merge = value;
+        return OCH_OK;
     default:
         return fail(OCH_E_INVALID, "unknown option %d", option);
     }
@@ -909,6 +915,7 @@ OCH_API int och_gpu_get_option(const och_gpu_pool *p, int option, int *value)
     case OCH_OPT_BOUNCE_COMPACT: *value = p->opt_bounce_compact; return OCH_OK;
     case OCH_OPT_CHUNK_TILES: *value = p->opt_chunk_tiles; return OCH_OK;
     case OCH_OPT_CULL: *value = p->opt_cull; return OCH_OK;
+    case OCH_OPT_MERGE: *value = p->opt_merge; return OCH_OK;
     default: return fail(OCH_E_INVALID, "unknown option %d", option);
     }
 }

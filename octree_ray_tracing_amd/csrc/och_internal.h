@@ -131,6 +131,7 @@ struct Schedule {
     uint32_t stamp_cap;
     const uint32_t *order;  // grid: optional workgroup permutation (och_gpu_plan_views)
     uint32_t *cost;         // grid: optional per-workgroup duration output (the planning launch)
+    int merge_k;            // grid, packed, no PUSH counts: in-block wave merging every merge_k iterations (0 off)
 };
 
 hipError_t launch_trace_batch(const DevPool &p, const float *origin, int origin_stride, const float *dirs,

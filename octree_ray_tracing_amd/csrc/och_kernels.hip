@@ -1157,7 +1157,138 @@ __global__ void k_trace_grid(DevPool P, Src S, Sink K, uint32_t xcd_group, const
     if (stamps) stamp(stamps, stamp_cap, t0, 64);
 }
 
-// Config 5: primary rays, then wavefront compaction -- the block's hit
+// Grid schedule with in-block wave merging (OCH_OPT_MERGE = K; the lever
+// DESIGN.md §8's lockstep model priced at -6..-9 % VALU per wave).  A block of
+// several waves walks its rays K iterations at a time; between rounds the
+// waves retire their finished rays and count the rest, and when the rays left
+// fit in fewer waves, the highest waves hand theirs to the free lanes of the
+// lower ones and exit, so no wave keeps issuing for a handful of lanes.  A
+// moved ray keeps its LDS stack column (the block's LDS outlives its waves);
+// its registers travel as 13 words through the LDS column of the free lane
+// that adopts it (a finished ray's stack, idle until then).  Every exchange
+// is behind block barriers, which count only the waves still running.
+constexpr int kMergeWords = 13;
+
+__device__ __forceinline__ void merge_pack(const Ray &r, uint32_t out, uint32_t column, uint32_t w[kMergeWords])
+{
+    for (int a = 0; a < 3; ++a) {
+        w[a] = fbits(r.c[a]);
+        w[3 + a] = fbits(r.b[a]);
+        w[6 + a] = r.p[a];
+    }
+    w[9] = r.cur;
+    w[10] = r.t_min;
+    w[11] = out;
+    // ctz(dim) 5 bits | idx 3 | inv & 7 3 | min_axis 4 | mode 4 | stack column 13
+    w[12] = (uint32_t)__builtin_ctz(r.dim) | (r.idx << 5) | ((r.inv & 7u) << 8) | (r.min_axis << 11) |
+            (r.mode << 15) | (column << 19);
+}
+
+__device__ __forceinline__ void merge_unpack(Ray &r, uint32_t &out, const uint32_t w[kMergeWords], uint32_t *lds,
+                                             uint32_t stride)
+{
+    for (int a = 0; a < 3; ++a) {
+        r.c[a] = ffrom(w[a]);
+        r.b[a] = ffrom(w[3 + a]);
+        r.p[a] = w[6 + a];
+    }
+    r.cur = w[9];
+    r.t_min = w[10];
+    out = w[11];
+    const uint32_t m = w[12], k = m & 31u;
+    r.dim = 1u << k;
+    r.idx = (m >> 5) & 7u;
+    r.inv = 24u | ((m >> 8) & 7u);
+    r.min_axis = (m >> 11) & 15u;
+    r.mode = (m >> 15) & 15u;
+    r.sp23 = lds + (m >> 19) + 23u * stride;
+    r.sp = r.sp23 - k * stride;
+}
+
+template <class Src, class Sink>
+__global__ void k_trace_grid_merge(DevPool P, Src S, Sink K, int merge_k, const uint32_t *__restrict__ order)
+{
+    extern __shared__ uint32_t lds_stack[];
+    __shared__ uint32_t wave_count[16];
+    __shared__ uint32_t free_list[1024];
+    const uint32_t nb = blockDim.x, n_waves = nb >> 6;
+    const uint32_t blk = order ? order[blockIdx.x] : blockIdx.x;
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+    const uint64_t below = (1ull << lane) - 1ull;
+    const uint32_t wave_base = blk * nb + (threadIdx.x & ~63u);
+    float o[3], d[3];
+    uint32_t out = 0;
+    bool miss, has = false;
+    Ray r;
+    r.dim = 0;
+    if (wave_base + lane < S.count() && S.get_wave_culled(wave_base, lane, P, P.cull != 0, o, d, out, miss)) {
+        if (miss) {
+            K.put(out, Hit{OCH_EXIT, 0u, P.miss_bits, 0u});
+        } else {
+            ray_init<true, false, true, kAsmLoad>(r, P, o, d, lds_stack + threadIdx.x, nb);
+            has = true;
+        }
+    }
+    uint32_t alive = n_waves;                                   // waves 0 .. alive-1 still run (block-uniform)
+    for (;;) {
+        for (int k = 0; k < merge_k; ++k) {                     // one round of walking
+            const bool walking = has && ray_active(r, P);
+            if (__ballot(walking) == 0) break;
+            if (walking) ray_iterate<true, false, kAsmLoad>(r, P, nb);
+        }
+        if (has && !ray_active(r, P)) {                         // retire
+            K.put(out, ray_result<true, kAsmLoad>(r, P));
+            has = false;
+        }
+        const uint64_t bal = __ballot(has);
+        if (lane == 0) wave_count[wave] = (uint32_t)__popcll(bal);
+        __syncthreads();
+        uint32_t total = 0;
+        for (uint32_t w = 0; w < alive; ++w) total += wave_count[w];
+        if (total == 0) break;                                  // every surviving wave sees the same total
+        const uint32_t keep = (total + 63u) >> 6;               // waves the rays left fit in
+        if (keep < alive) {
+            // free lanes of the kept waves, ranked, publish their thread ids
+            if (wave < keep && !has) {
+                uint32_t rank = (uint32_t)__popcll(~bal & below);
+                for (uint32_t w = 0; w < wave; ++w) rank += 64u - wave_count[w];
+                free_list[rank] = threadIdx.x;
+            }
+            __syncthreads();
+            if (wave >= keep && has) {                          // the movers: write into the adopter's column
+                uint32_t rank = (uint32_t)__popcll(bal & below);
+                for (uint32_t w = keep; w < wave; ++w) rank += wave_count[w];
+                wait_cur<kAsmLoad>(r);
+                uint32_t st[kMergeWords];
+                merge_pack(r, out, threadIdx.x, st);
+                uint32_t *dst = lds_stack + free_list[rank];
+                for (int i = 0; i < kMergeWords; ++i) dst[i * nb] = st[i];
+                has = false;
+            }
+            __syncthreads();
+            uint32_t movers = 0;
+            for (uint32_t w = keep; w < alive; ++w) movers += wave_count[w];
+            if (wave < keep && !has) {                          // the adopters
+                uint32_t rank = (uint32_t)__popcll(~bal & below);
+                for (uint32_t w = 0; w < wave; ++w) rank += 64u - wave_count[w];
+                if (rank < movers) {
+                    uint32_t st[kMergeWords];
+                    const uint32_t *src = lds_stack + threadIdx.x;
+                    for (int i = 0; i < kMergeWords; ++i) st[i] = src[i * nb];
+                    merge_unpack(r, out, st, lds_stack, nb);
+                    has = true;
+                }
+            }
+            __syncthreads();                                    // columns read; counts reusable
+            if (wave >= keep) return;                           // this wave's rays live on in the kept waves
+            alive = keep;
+        } else {
+            __syncthreads();                                    // counts read before the next round writes them
+        }
+    }
+}
+
+// Config 5: primary rays, then wavefront compaction -- the block's hit// Config 5: primary rays, then wavefront compaction -- the block's hit
 // lanes (ballot + popcount per wave, wave offsets through LDS) write their
 // secondary rays into an LDS queue, and the first lanes of the block trace
 // them, so waves whose tiles mostly missed retire instead of idling beside
@@ -1484,6 +1615,10 @@ hipError_t launch_as(const DevPool &p, const Src &s, const Sink &k, uint32_t n, 
         if (grid > needed) grid = needed;
         hipLaunchKernelGGL((k_trace_persistent<Src, Sink, kPacked, kCount>), dim3(grid), dim3(block), lds, stream, p, s,
                            k, sc.counter, sc.refill_min, sc.stamps, sc.stamp_cap);
+    } else if (sc.merge_k > 0 && kPacked && !kCount && block >= 128 && block <= 1024) {
+        hipLaunchKernelGGL((k_trace_grid_merge<Src, Sink>), dim3((n + block - 1) / block), dim3(block),
+                           lds > kMergeWords * 4u * (size_t)block ? lds : kMergeWords * 4u * (size_t)block, stream, p,
+                           s, k, sc.merge_k, sc.order);
     } else {
         const uint32_t xcd_group = supertile_rays >= (uint32_t)block ? supertile_rays / (uint32_t)block : 0u;
         const uint32_t per_block = OCH_DUAL ? 2u * (uint32_t)block : (uint32_t)block;
