@@ -2,6 +2,7 @@
 set -o pipefail
 O=gpurun_out/r03m; mkdir -p $O
 export TMPDIR=/tmp
+timeout -k 10 90 python -u tools/merge_probe.py > $O/probe.log 2>&1 || exit 9
 timeout -k 10 500 python -u -m pytest tests/test_gpu_merge.py -m gpu -x -v --timeout 400 --timeout-method thread > $O/tests.log 2>&1 || exit 1
 timeout -k 10 500 python -u tools/ab_render.py --rounds 4 --pipelined 400 --cache /tmp/och_terrain_cache.npz --out $O/ab.json \
   --arm '{"tile_order": 2}' --arm '{"tile_order": 2, "block": 256}' --arm '{"tile_order": 2, "block": 256, "merge": 4}' \
