@@ -1260,7 +1260,10 @@ __global__ void k_trace_grid_merge(DevPool P, Src S, Sink K, int merge_k, const 
                 for (uint32_t w = keep; w < wave; ++w) rank += wave_count[w];
                 wait_cur<kAsmLoad>(r);
                 uint32_t st[kMergeWords];
-                merge_pack(r, out, threadIdx.x, st);
+                // the ray's own stack column (not this lane's: a ray adopted
+                // earlier walks on the column it started in)
+                const uint32_t column = (uint32_t)(r.sp23 - lds_stack) - 23u * nb;
+                merge_pack(r, out, column, st);
                 uint32_t *dst = lds_stack + free_list[rank];
                 for (int i = 0; i < kMergeWords; ++i) dst[i * nb] = st[i];
                 has = false;
