@@ -171,7 +171,8 @@ struct och_gpu_pool {
     // [2] tiled trace batches (och_gpu_plan_batch_tiled)
     uint32_t *d_order[3] = {nullptr, nullptr, nullptr};
     uint32_t *d_order_xcd[3] = {nullptr, nullptr, nullptr};   // OCH_OPT_TILE_ORDER = 3: grouped per XCD
-    uint32_t order_blocks[3] = {0, 0, 0};
+    uint32_t order_blocks[3] = {0, 0, 0};     // allocated entries
+    uint32_t plan_blocks[3] = {0, 0, 0};      // entries of the current plan (its launch's grid)
     int64_t plan_key[3][9] = {};
     // row deal (och_gpu_set_row_deal): for frames of deal_h rows in chunks of
     // deal_chunk over deal_n shards, chunk g belongs to a chosen shard instead
@@ -201,6 +202,7 @@ struct och_gpu_pool {
         sc.stamps = stamps;
         sc.stamp_cap = stamp_cap;
         sc.order = nullptr;
+        sc.order_n = 0;
         sc.cost = nullptr;
         sc.merge_k = opt_merge;
         return sc;
@@ -1026,7 +1028,10 @@ OCH_API int och_gpu_trace_batch_tiled_dev(och_gpu_pool *p, const float *origin, 
     if (p->opt_tile_order >= 2 && p->opt_schedule == 0 && p->d_order[2]) {
         int64_t key[9];
         batch_key(p, n, width, key);
-        if (std::memcmp(key, p->plan_key[2], sizeof key) == 0) sc.order = p->d_order[2];
+        if (std::memcmp(key, p->plan_key[2], sizeof key) == 0) {
+            sc.order = p->d_order[2];
+            sc.order_n = p->plan_blocks[2];
+        }
     }
     OCH_HIP(hipEventRecord(p->ev_start, p->stream()));
     OCH_HIP(och::launch_trace_batch_tiled(p->dev(), origin, origin_stride, dirs, n, width, hit_dir, hit_voxel,
@@ -1054,6 +1059,7 @@ OCH_API int och_gpu_plan_batch_tiled(och_gpu_pool *p, const float *origin, int o
     sc.kind = 0;
     sc.tile_order = 0;
     sc.cost = cost;
+    sc.merge_k = 0;
     OCH_HIP(och::launch_trace_batch_tiled(p->dev(), origin, origin_stride, dirs, n, width,
                                           reinterpret_cast<int32_t *>(base), reinterpret_cast<uint32_t *>(base + out_bytes),
                                           reinterpret_cast<uint32_t *>(base + 2 * out_bytes), nullptr, sc, p->stream()));
@@ -1074,6 +1080,7 @@ OCH_API int och_gpu_plan_batch_tiled(och_gpu_pool *p, const float *origin, int o
     }
     OCH_HIP(hipMemcpy(p->d_order[2], order.data(), (size_t)max_blocks * 4, hipMemcpyHostToDevice));
     batch_key(p, n, width, p->plan_key[2]);
+    p->plan_blocks[2] = max_blocks;
     return OCH_OK;
 }
 
@@ -1198,8 +1205,10 @@ int render_views(och_gpu_pool *p, const och_camera *cams, int n_views, uint32_t 
     if (p->opt_tile_order >= 2 && (bounce || p->opt_schedule == 0) && p->d_order[which]) {
         const int64_t key[9] = {cams[0].width, cams[0].height, n_views, row_chunk, shard, n_shards, p->opt_block,
                                 bounce ? p->opt_bounce_compact : 0, dealt ? (int64_t)p->deal_serial : 0};
-        if (std::memcmp(key, p->plan_key[which], sizeof key) == 0)
+        if (std::memcmp(key, p->plan_key[which], sizeof key) == 0) {
             sc.order = p->opt_tile_order == 3 ? p->d_order_xcd[which] : p->d_order[which];
+            sc.order_n = p->plan_blocks[which];
+        }
     }
     OCH_HIP(hipEventRecord(p->ev_start, p->stream()));
     if (code_slices)
@@ -1251,6 +1260,7 @@ OCH_API int och_gpu_plan_views(och_gpu_pool *p, const och_camera *cams, int n_vi
         sc.kind = 0;
         sc.tile_order = 0;
         sc.cost = cost;
+        sc.merge_k = 0;                       // costs come from the plain grid kernel (same grid)
         if (which == 0)
             OCH_HIP(och::launch_render(p->dev(), f, sc, p->stream()));
         else
@@ -1260,6 +1270,10 @@ OCH_API int och_gpu_plan_views(och_gpu_pool *p, const och_camera *cams, int n_vi
         OCH_HIP(hipStreamSynchronize(p->stream()));
         uint32_t n_blocks = 0;
         while (n_blocks < max_blocks && c[n_blocks] != 0xFFFFFFFFu) ++n_blocks;   // launched blocks wrote a cost
+        if (n_blocks == 0) {
+            p->plan_key[which][0] = -1;          // no plan: later launches run in natural order
+            return fail(OCH_E_INVALID, "planning render wrote no workgroup costs (kernel without cost output?)");
+        }
         std::vector<uint32_t> order(n_blocks);
         for (uint32_t i = 0; i < n_blocks; ++i) order[i] = i;
         std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return c[a] > c[b]; });
@@ -1302,6 +1316,7 @@ OCH_API int och_gpu_plan_views(och_gpu_pool *p, const och_camera *cams, int n_vi
         const int64_t key[9] = {W, H, n_views, row_chunk, shard, n_shards, p->opt_block,
                                 which ? p->opt_bounce_compact : 0, dealt ? (int64_t)p->deal_serial : 0};
         std::memcpy(p->plan_key[which], key, sizeof key);
+        p->plan_blocks[which] = n_blocks;
     }
     return OCH_OK;
 }

@@ -130,6 +130,7 @@ struct Schedule {
     uint64_t *stamps;       // optional per-wave residency records
     uint32_t stamp_cap;
     const uint32_t *order;  // grid: optional workgroup permutation (och_gpu_plan_views)
+    uint32_t order_n;       // entries in *order: a launch whose grid differs runs in natural order
     uint32_t *cost;         // grid: optional per-workgroup duration output (the planning launch)
     int merge_k;            // grid, packed, no PUSH counts: in-block wave merging every merge_k iterations (0 off)
 };

@@ -1619,15 +1619,19 @@ hipError_t launch_as(const DevPool &p, const Src &s, const Sink &k, uint32_t n, 
         hipLaunchKernelGGL((k_trace_persistent<Src, Sink, kPacked, kCount>), dim3(grid), dim3(block), lds, stream, p, s,
                            k, sc.counter, sc.refill_min, sc.stamps, sc.stamp_cap);
     } else if (sc.merge_k > 0 && kPacked && !kCount && block >= 128 && block <= 1024) {
-        hipLaunchKernelGGL((k_trace_grid_merge<Src, Sink>), dim3((n + block - 1) / block), dim3(block),
+        const uint32_t grid = (n + block - 1) / block;
+        hipLaunchKernelGGL((k_trace_grid_merge<Src, Sink>), dim3(grid), dim3(block),
                            lds > kMergeWords * 4u * (size_t)block ? lds : kMergeWords * 4u * (size_t)block, stream, p,
-                           s, k, sc.merge_k, sc.order);
+                           s, k, sc.merge_k, sc.order_n == grid ? sc.order : nullptr);
     } else {
         const uint32_t xcd_group = supertile_rays >= (uint32_t)block ? supertile_rays / (uint32_t)block : 0u;
         const uint32_t per_block = OCH_DUAL ? 2u * (uint32_t)block : (uint32_t)block;
-        hipLaunchKernelGGL((k_trace_grid<Src, Sink, kPacked, kCount>), dim3((n + per_block - 1) / per_block), dim3(block),
-                           OCH_DUAL ? 2 * lds : lds, stream, p, s, k, xcd_group, sc.order, sc.cost, sc.stamps,
-                           sc.stamp_cap);
+        const uint32_t grid = (n + per_block - 1) / per_block;
+        // a plan is a permutation of exactly this grid's workgroups; any other
+        // (stale or for another block size) would index past it
+        hipLaunchKernelGGL((k_trace_grid<Src, Sink, kPacked, kCount>), dim3(grid), dim3(block),
+                           OCH_DUAL ? 2 * lds : lds, stream, p, s, k, xcd_group, sc.order_n == grid ? sc.order : nullptr,
+                           sc.cost, sc.stamps, sc.stamp_cap);
     }
     return hipGetLastError();
 }
@@ -1649,12 +1653,13 @@ hipError_t launch_bounce(const DevPool &p, const Src &s, const Sink &k, uint32_t
     const size_t queue = 8u * (size_t)block * sizeof(uint32_t);
     const size_t lds = stack_bytes(p.depth, block) > queue ? stack_bytes(p.depth, block) : queue;
     const dim3 grid((n + block - 1) / block);
+    const uint32_t *order = sc.order_n == grid.x ? sc.order : nullptr;   // a plan of exactly this grid
     if (p.packed)
         hipLaunchKernelGGL((k_trace_bounce<Src, Sink, true, kCount>), grid, dim3(block), lds, stream, p, s, k,
-                           sc.bounce_compact, sc.order, sc.cost, sc.stamps, sc.stamp_cap);
+                           sc.bounce_compact, order, sc.cost, sc.stamps, sc.stamp_cap);
     else
         hipLaunchKernelGGL((k_trace_bounce<Src, Sink, false, kCount>), grid, dim3(block), lds, stream, p, s, k,
-                           sc.bounce_compact, sc.order, sc.cost, sc.stamps, sc.stamp_cap);
+                           sc.bounce_compact, order, sc.cost, sc.stamps, sc.stamp_cap);
     return hipGetLastError();
 }
 

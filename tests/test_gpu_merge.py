@@ -35,7 +35,7 @@ def test_merge_frames_and_batches(ort, O, gpu_device, depth):
     d[:5000, 0] = 0.0
     d[5000:8000] *= np.float32(1e-30)
     ref = O.trace_batch(ref_pool, O.Rcp(None), o, d, nthreads=16)
-    blocks = (256,) if depth == 12 else (128, 256, 512)
+    blocks = (128, 256) if depth == 12 else (128, 256, 512)
     for block in blocks:
         pool.set_option("block", block)
         for k in ((1, 8) if depth == 12 else (1, 4, 8, 32)):
