@@ -62,6 +62,57 @@ PMC_PATH = ROOT / "profiles" / "pmc_summary.json"
 WINDOW_PATH = ROOT / "profiles" / "window_summary.json"
 
 
+class FenceFreeEvent:
+    """A HIP timing event created with hipEventDisableSystemFence, recorded on a
+    torch stream.  torch.cuda.Event records with a system-scope release (an L2
+    writeback and invalidate on every record): two per step put ~10 us of idle
+    GPU between each lockstep group of frames in the bench window
+    (profiles/r03/window/).  Timestamps need no such fence; the
+    host reads them only after torch.cuda.synchronize().  The HIP runtime is
+    torch's own (libamdhip64.so.7 is already loaded by soname)."""
+    _hip = None
+
+    def __init__(self):
+        import ctypes
+        if FenceFreeEvent._hip is None:
+            hip = ctypes.CDLL("libamdhip64.so.7")
+            hip.hipEventCreateWithFlags.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_uint]
+            hip.hipEventRecord.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+            hip.hipEventElapsedTime.argtypes = [ctypes.POINTER(ctypes.c_float), ctypes.c_void_p, ctypes.c_void_p]
+            hip.hipEventDestroy.argtypes = [ctypes.c_void_p]
+            FenceFreeEvent._hip = hip
+        self._c = ctypes
+        self.h = ctypes.c_void_p()
+        rc = self._hip.hipEventCreateWithFlags(ctypes.byref(self.h), 0x20000000)    # hipEventDisableSystemFence
+        if rc != 0:
+            raise RuntimeError(f"hipEventCreateWithFlags failed ({rc})")
+
+    def record(self, stream):
+        rc = self._hip.hipEventRecord(self.h, self._c.c_void_p(stream.cuda_stream))
+        if rc != 0:
+            raise RuntimeError(f"hipEventRecord failed ({rc})")
+
+    def elapsed_time(self, end) -> float:
+        ms = self._c.c_float()
+        rc = self._hip.hipEventElapsedTime(self._c.byref(ms), self.h, end.h)
+        if rc != 0:
+            raise RuntimeError(f"hipEventElapsedTime failed ({rc})")
+        return float(ms.value)
+
+    def __del__(self):
+        if self._hip is not None and self.h:
+            self._hip.hipEventDestroy(self.h)
+
+
+def make_event(kind: str):
+    return FenceFreeEvent() if kind == "nofence" else torch_event()
+
+
+def torch_event():
+    import torch
+    return torch.cuda.Event(enable_timing=True)
+
+
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
@@ -345,6 +396,13 @@ def main():
                     help="render and exchange RGBA8 slices instead of 1-byte indexed-colour codes")
     ap.add_argument("--fresh-streams", action="store_true",
                     help="put every frame in flight on a new stream, none on the current stream")
+    ap.add_argument("--no-step-events", action="store_true",
+                    help="diagnostic: no per-step timing events in the headline window (no per-launch kernel_ms)")
+    ap.add_argument("--step-events", choices=("nofence", "torch"), default="nofence",
+                    help="per-step timing events: HIP events without the system-scope fence (default), or "
+                         "torch.cuda.Event (a system-scope release per record)")
+    ap.add_argument("--stream-priority", default="",
+                    help="diagnostic: comma-separated HIP priorities of the new frame streams (lower = higher)")
     ap.add_argument("--extra-windows", type=int, default=0,
                     help="diagnostic: this many more warmup + timed windows after the first (reported, not value)")
     ap.add_argument("--shade", choices=("display", "all"), default="display",
@@ -425,7 +483,9 @@ def main():
     if a.fresh_streams:      # every frame in flight on a new stream (none on the current one)
         streams = [torch.cuda.Stream(device=dev) for _ in range(max(1, a.inflight))]
     else:
-        streams = [stream] + [torch.cuda.Stream(device=dev) for _ in range(max(1, a.inflight) - 1)]
+        prio = [int(x) for x in a.stream_priority.split(",") if x.strip()]
+        streams = [stream] + [torch.cuda.Stream(device=dev, priority=prio[i] if i < len(prio) else 0)
+                              for i in range(max(1, a.inflight) - 1)]
     sfs = []
     for s_ in streams:
         with torch.cuda.stream(s_):
@@ -524,8 +584,7 @@ def main():
     del hd, hv, ht, hp, dirs
 
     # timing events for every step of a window, created once, outside the timed region
-    ev_pool = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-               for _ in range(max(a.steps, 1))]
+    ev_pool = [(make_event(a.step_events), make_event(a.step_events)) for _ in range(max(a.steps, 1))]
 
     def step(k, ev=None, bounce=False):
         """One step: render both views of this rank's rows, all-gather, unshard --
@@ -604,8 +663,9 @@ def main():
     # warmup, then the timed steps
     for k in range(a.warmup):
         step(k)
-    ev = []
+    ev = None if a.no_step_events else []
     elapsed = timed(a.steps, ev=ev, marked=True)
+    ev = ev or []
     per_rank_ms = [round(t / a.steps * 1e3, 4) for t in rank_s[-1]]
     last = (a.steps - 1) % len(sfs)
     frames_host = sfs[last].frames.cpu().numpy() if rank == 0 else None
@@ -615,11 +675,15 @@ def main():
     total_rays = W * H * frames
     value = total_rays / elapsed / 1e6
     host_issue_ms = round(issue_s[-1] * 1e3, 4)
-    extra = []
+    extra, extra_noev = [], []
     for _ in range(a.extra_windows):
+        # alternately with and without the per-step timing events
         for k in range(a.warmup):
             step(k)
         extra.append(round(total_rays / timed(a.steps, ev=[]) / 1e6, 1))
+        for k in range(a.warmup):
+            step(k)
+        extra_noev.append(round(total_rays / timed(a.steps) / 1e6, 1))
 
     # Sustained: >= a.sustain seconds of steps, three runs, median.
     sustained = None
@@ -697,7 +761,7 @@ def main():
     # pipelined step, against the chip's issue peak.  HBM: SURVEY §8(d)'s
     # canonical algorithmic bytes, 24 B in + 12 B out + 4 B per PUSH per ray.
     step_s = elapsed / a.steps
-    k_avg_ms = float(kms.mean())
+    k_avg_ms = float(kms.mean()) if kms.size else latency_ms    # --no-step-events: the lone launch instead
     canon_bytes = 36 * rays_rank + 4 * walk_push
     hbm = {"bound": "hbm", "bytes_per_launch": int(canon_bytes),
            "bytes_model": "SURVEY 8(d) canonical: 24 B ray in + 12 B hit record out per ray + 4 B per PUSH the "
@@ -802,7 +866,7 @@ def main():
             "walked_rays_note": "Mrays/s of the rays that walk the DAG (value x (1 - culled_frac)); the "
                                 "occupied-box cull ends the rest as proven misses",
             "per_rank_ms_per_step": per_rank_ms,
-            **({"extra_windows": extra} if extra else {}),
+            **({"extra_windows": extra, "extra_windows_no_events": extra_noev} if extra else {}),
             "trace_batch": trace_only,
             "bounce": bounce,
             "other_configs": others,
