@@ -36,6 +36,7 @@ of the last timed step -- primary and config 5 -- pixel for pixel (`parity`).
 from __future__ import annotations
 
 import argparse
+import ctypes
 import gc
 import hashlib
 import json
@@ -105,7 +106,7 @@ class FenceFreeEvent:
 
 
 def make_event(kind: str):
-    return FenceFreeEvent() if kind == "nofence" else torch_event()
+    return torch_event() if kind == "torch" else FenceFreeEvent()
 
 
 def torch_event():
@@ -398,9 +399,25 @@ def main():
                     help="put every frame in flight on a new stream, none on the current stream")
     ap.add_argument("--no-step-events", action="store_true",
                     help="diagnostic: no per-step timing events in the headline window (no per-launch kernel_ms)")
-    ap.add_argument("--step-events", choices=("nofence", "torch"), default="nofence",
-                    help="per-step timing events: HIP events without the system-scope fence (default), or "
-                         "torch.cuda.Event (a system-scope release per record)")
+    ap.add_argument("--step-events", choices=("dispatch", "nofence", "torch"), default="dispatch",
+                    help="per-step timing events of the render launch: recorded by the launch's own dispatch "
+                         "(och_gpu_set_launch_events, default), or hipEventRecord of fence-free events before "
+                         "and after it, or torch.cuda.Event records (a system-scope release per record)")
+    ap.add_argument("--wait", choices=("spin", "block"), default="spin",
+                    help="end of a timed window: poll the frame streams (hipStreamQuery) until they are idle, then "
+                         "synchronize (default), or synchronize at once (a wait of milliseconds sleeps on an "
+                         "interrupt, whose wake-up lands inside the window)")
+    ap.add_argument("--host-spin-us", type=int, default=0,
+                    help="diagnostic: busy-loop the host this long after each synchronize around a window")
+    ap.add_argument("--pool-timing", type=int, default=None,
+                    help="diagnostic: the pool's OCH_OPT_TIMING for launches without step events (default 1)")
+    ap.add_argument("--no-fast-issue", action="store_true",
+                    help="diagnostic: issue N = 1 steps through the Python wrappers and torch stream contexts")
+    ap.add_argument("--host-rehearse", action="store_true",
+                    help="diagnostic: before a window, switch the pool and torch to each frame stream (no GPU work)")
+    ap.add_argument("--host-stamps", action="store_true",
+                    help="diagnostic: report the headline window's host clock readings (ns, CLOCK_MONOTONIC and "
+                         "CLOCK_BOOTTIME) to line them up with a rocprofv3 kernel trace")
     ap.add_argument("--stream-priority", default="",
                     help="diagnostic: comma-separated HIP priorities of the new frame streams (lower = higher)")
     ap.add_argument("--extra-windows", type=int, default=0,
@@ -497,6 +514,8 @@ def main():
     # frames identical), so no frame ends on a few late grazing tiles.
     if not any(kv.startswith("tile_order=") for kv in a.opt):
         pool.set_option("tile_order", 2)
+    if a.pool_timing is not None:
+        pool.set_option("timing", a.pool_timing)
     if pool.get_option("tile_order") >= 2:
         pool.plan_views(cams, a.row_chunk, rank, world)
 
@@ -586,22 +605,68 @@ def main():
     # timing events for every step of a window, created once, outside the timed region
     ev_pool = [(make_event(a.step_events), make_event(a.step_events)) for _ in range(max(a.steps, 1))]
 
+    # N = 1 with direct RGBA8 frames: a step is the render launch alone, issued as
+    # three prepared C-ABI calls (stream, events, render) with their arguments built
+    # here -- no torch stream context or wrapper code per step.  The first step of a
+    # window otherwise took ~0.1 ms longer to issue than the rest, while the GPU
+    # waited (rocprofv3 --hip-trace, profiles/r03/window/).
+    fast = None
+    if direct and not a.no_fast_issue:
+        from octree_ray_tracing_amd._lib import Camera, load as load_lib
+        lib = load_lib()
+        cam_arr = (Camera * len(cams))(*cams)
+        h = pool._h
+        fast = {"lib": lib, "cams": cam_arr, "h": h,
+                "args": [[(h, ctypes.c_void_p(s_.cuda_stream)),
+                          (h, ctypes.cast(cam_arr, ctypes.c_void_p), len(cams), ctypes.c_void_p(f_.frames.data_ptr()),
+                           a.row_chunk, 0, 1)] for s_, f_ in zip(streams, sfs)]}
+
+    def step_fast(k, ev, bounce):
+        lib, (sa, ra) = fast["lib"], fast["args"][k % len(streams)]
+        st = lib.och_gpu_set_stream(*sa)
+        if ev is not None:
+            e0, e1 = ev_pool[len(ev) % len(ev_pool)]
+            st |= lib.och_gpu_set_launch_events(fast["h"], e0.h, e1.h)
+            ev.append((e0, e1))
+        st |= (lib.och_gpu_render_bounce_views_dev if bounce else lib.och_gpu_render_views_dev)(*ra)
+        if st:
+            raise RuntimeError(f"step {k}: {lib.och_last_error().decode()}")
+
     def step(k, ev=None, bounce=False):
         """One step: render both views of this rank's rows, all-gather, unshard --
         on stream k % inflight, into that stream's own frame buffers."""
+        if fast is not None and a.step_events == "dispatch":
+            return step_fast(k, ev, bounce)
         s_, f_ = streams[k % len(streams)], sfs[k % len(sfs)]
+        sub = stamps.setdefault("step_parts", []) if (trace_parts and k < 3) else None
+        if sub is not None:
+            sub.append(("begin", time.monotonic_ns()))
         pool.set_stream(s_)
         with torch.cuda.stream(s_):
+            if sub is not None:
+                sub.append(("stream", time.monotonic_ns()))
             if ev is not None:
-                # event pairs are made before the timed region (ev_pool); recorded here
+                # event pairs are made before the timed region (ev_pool); the render
+                # launch's dispatch records them (or a record before and after it)
                 e0, e1 = ev_pool[len(ev) % len(ev_pool)]
-                e0.record(s_)
+                if a.step_events == "dispatch":
+                    pool.set_launch_events(e0, e1)
+                else:
+                    e0.record(s_)
+            if sub is not None:
+                sub.append(("events", time.monotonic_ns()))
             f_.render_local(cams, bounce)
+            if sub is not None:
+                sub.append(("render", time.monotonic_ns()))
             if ev is not None:
-                e1.record(s_)
+                if a.step_events != "dispatch":
+                    e1.record(s_)
                 ev.append((e0, e1))
             f_.exchange()
 
+    stamps = {}                            # --host-stamps
+    trace_parts = False
+    in_window = False
     issue_s = []                           # host time to issue each timed window's steps
     rank_s = []                            # every rank's wall time of each timed window
     marker = torch.zeros(1, dtype=torch.int64, device=dev)
@@ -611,25 +676,63 @@ def main():
         rocprofv3 kernel trace (tools/window_trace.py), outside the timed region."""
         torch.bitwise_not(marker, out=marker)
 
+    def drain():
+        """torch.cuda.synchronize(), after polling the streams (hipStreamQuery)
+        until they are idle (--wait spin, default).  A blocking wait of
+        milliseconds sleeps on an interrupt: the wake-up lands inside the window
+        at its end, and at its start the woken core issued the first step ~5x
+        slower than the next ones (~0.17 ms, profiles/r03/window/)."""
+        if a.wait == "spin":
+            watch = list(streams) + [torch.cuda.current_stream()]
+            while not all(s_.query() for s_ in watch):
+                pass
+        torch.cuda.synchronize()
+        if a.host_spin_us > 0 and not in_window:
+            t_end = time.perf_counter_ns() + a.host_spin_us * 1000
+            while time.perf_counter_ns() < t_end:
+                pass
+        if a.host_rehearse and not in_window:
+            for s_ in streams:                 # the step's host calls, no GPU work
+                pool.set_stream(s_)
+                with torch.cuda.stream(s_):
+                    pool.get_option("cull")
+            pool.set_stream(stream)
+
     def timed(n, bounce=False, ev=None, marked=False):
         """n steps between barrier + synchronize; max over ranks of the wall time."""
         if marked:
             mark()
-        torch.cuda.synchronize()
+        drain()
         if world > 1:
             dist.barrier()
-        torch.cuda.synchronize()
+        drain()
         gc_was = gc.isenabled()
         gc.disable()                       # no collector pause inside the timed region (as timeit)
+        if marked and a.host_stamps:
+            stamps["t0"] = (time.monotonic_ns(), time.clock_gettime_ns(time.CLOCK_BOOTTIME))
         t0 = time.perf_counter()
-        for k in range(n):
-            step(k, ev, bounce)
+        nonlocal trace_parts, in_window
+        trace_parts = marked and a.host_stamps
+        if marked and a.host_stamps:
+            issued = stamps.setdefault("issued", [])
+            for k in range(n):
+                step(k, ev, bounce)
+                issued.append(time.monotonic_ns())
+        else:
+            for k in range(n):
+                step(k, ev, bounce)
         issue_s.append(time.perf_counter() - t0)
-        torch.cuda.synchronize()
+        trace_parts = False
+        in_window = True
+        drain()
         if world > 1:
             dist.barrier()
-        torch.cuda.synchronize()
-        el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
+        drain()
+        in_window = False
+        t1 = time.perf_counter()
+        if marked and a.host_stamps:
+            stamps["t1"] = (time.monotonic_ns(), time.clock_gettime_ns(time.CLOCK_BOOTTIME))
+        el = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
         if gc_was:
             gc.enable()
         if marked:
@@ -867,6 +970,7 @@ def main():
                                 "occupied-box cull ends the rest as proven misses",
             "per_rank_ms_per_step": per_rank_ms,
             **({"extra_windows": extra, "extra_windows_no_events": extra_noev} if extra else {}),
+            **({"host_stamps_ns": stamps} if stamps else {}),
             "trace_batch": trace_only,
             "bounce": bounce,
             "other_configs": others,

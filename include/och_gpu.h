@@ -170,10 +170,14 @@ typedef enum och_option {
                                   ray's setup); exact, for launches that do not count
                                   PUSHes.  0 = every ray walks.  2 = diagnostic: launches that count PUSHes
                                   cull too, a culled ray counting 0 (the PUSHes the culled launch walks) */
-    OCH_OPT_MERGE = 9          /* K > 0: grid launches without PUSH counts on the packed layout, with a block of
+    OCH_OPT_MERGE = 9,         /* K > 0: grid launches without PUSH counts on the packed layout, with a block of
                                   128..1024 threads, merge the block's waves every K iterations: the rays left
                                   move into the free lanes of the fewest waves, the emptied waves exit (records
                                   unchanged).  0 (default) = off */
+    OCH_OPT_TIMING = 10        /* per-launch timing of trace/render kernels (och_gpu_last_kernel_ms):
+                                  1 (default) = recorded by the kernel's own dispatch (hipExtLaunchKernel: no
+                                  packets between two launches of a stream); 2 = hipEventRecord before and
+                                  after the launch; 0 = not timed */
 } och_option;
 OCH_API int och_gpu_set_option(och_gpu_pool *pool, int option, int value);
 OCH_API int och_gpu_get_option(const och_gpu_pool *pool, int option, int *value);
@@ -186,8 +190,17 @@ OCH_API int och_gpu_set_stamp_buffer(och_gpu_pool *pool, uint64_t *stamps, uint3
  * pool's block size and stack depth. */
 OCH_API int och_gpu_occupancy(const och_gpu_pool *pool, int kind, int *blocks_per_cu);
 /* Duration of the most recent trace/render kernel launched on the pool,
- * measured with HIP events on the stream it ran on (blocks until it ends). */
+ * measured with HIP events on the stream it ran on (blocks until it ends).
+ * OCH_E_INVALID if that launch was not timed (OCH_OPT_TIMING 0, n = 0, or it
+ * recorded the caller's events). */
 OCH_API int och_gpu_last_kernel_ms(och_gpu_pool *pool, float *ms);
+/* The next trace/render launch on the pool records these HIP events
+ * (hipEvent_t, created by the caller; either may be NULL) at its kernel's
+ * start and end, through the dispatch itself, instead of the pool's own.
+ * One launch only; a call that launches nothing (n = 0) leaves them
+ * unrecorded.  For frame timers: no event packets between the launches of a
+ * stream. */
+OCH_API int och_gpu_set_launch_events(och_gpu_pool *pool, void *start_event, void *stop_event);
 
 /* ------------------------------------------------------------ tracing */
 /* Reference signature: one ray, synchronous (the pick ray of

@@ -79,6 +79,7 @@ PROTOTYPES = {
     "och_gpu_set_stamp_buffer": (C.c_int, [_P, _P, _u32]),
     "och_gpu_occupancy": (C.c_int, [_P, C.c_int, C.POINTER(C.c_int)]),
     "och_gpu_last_kernel_ms": (C.c_int, [_P, C.POINTER(C.c_float)]),
+    "och_gpu_set_launch_events": (C.c_int, [_P, C.c_void_p, C.c_void_p]),
     "och_gpu_trace": (C.c_int, [_P] + [_f32] * 6 + [C.POINTER(_i32), C.POINTER(_u32), C.POINTER(_f32)]),
     "och_gpu_trace_batch": (C.c_int, [_P, _P, C.c_int, _P, _u32, _P, _P, _P]),
     "och_gpu_trace_batch_dev": (C.c_int, [_P, _P, C.c_int, _P, _u32, _P, _P, _P, _P]),

@@ -157,6 +157,9 @@ struct och_gpu_pool {
     int opt_bounce_compact = 1;
     int opt_cull = 1;
     int opt_merge = 0;
+    int opt_timing = 1;                        // OCH_OPT_TIMING
+    hipEvent_t next_ev_start = nullptr;        // och_gpu_set_launch_events: the next launch's events
+    hipEvent_t next_ev_stop = nullptr;
     // bounding box of the pool's voxels (voxel units, [lo, hi)), for the cull
     bool box_any = false;
     int32_t box_lo[3] = {0, 0, 0}, box_hi[3] = {0, 0, 0};
@@ -205,6 +208,8 @@ struct och_gpu_pool {
         sc.order_n = 0;
         sc.cost = nullptr;
         sc.merge_k = opt_merge;
+        sc.ev_start = nullptr;
+        sc.ev_stop = nullptr;
         return sc;
     }
 
@@ -580,7 +585,9 @@ OCH_API int och_gpu_pool_create(const uint32_t *nodes, uint32_t n_nodes, uint32_
         p->cus = prop.multiProcessorCount;
     if (hipMalloc(&p->d_counter, 256) != hipSuccess) return bail(fail(OCH_E_NOMEM, "counter allocation failed"));
     if (hipStreamCreateWithFlags(&p->own_stream, hipStreamNonBlocking) != hipSuccess ||
-        hipEventCreate(&p->ev_start) != hipSuccess || hipEventCreate(&p->ev_stop) != hipSuccess)
+        // timing only: no system-scope release at the timed kernel's end
+        hipEventCreateWithFlags(&p->ev_start, hipEventDisableSystemFence) != hipSuccess ||
+        hipEventCreateWithFlags(&p->ev_stop, hipEventDisableSystemFence) != hipSuccess)
         return bail(fail(OCH_E_HIP, "stream/event creation failed"));
     const HostRcp &rc = host_rcp();
     if (rc.status == OCH_OK) {
@@ -899,6 +906,10 @@ OCH_API int och_gpu_set_option(och_gpu_pool *p, int option, int value)
         if (value < 0 || value > 4096) return fail(OCH_E_INVALID, "merge rounds %d outside 0..4096", value);
         p->opt_merge = value;
         return OCH_OK;
+    case OCH_OPT_TIMING:
+        if (value < 0 || value > 2) return fail(OCH_E_INVALID, "timing must be 0, 1 or 2");
+        p->opt_timing = value;
+        return OCH_OK;
     default:
         return fail(OCH_E_INVALID, "unknown option %d", option);
     }
@@ -918,6 +929,7 @@ OCH_API int och_gpu_get_option(const och_gpu_pool *p, int option, int *value)
     case OCH_OPT_CHUNK_TILES: *value = p->opt_chunk_tiles; return OCH_OK;
     case OCH_OPT_CULL: *value = p->opt_cull; return OCH_OK;
     case OCH_OPT_MERGE: *value = p->opt_merge; return OCH_OK;
+    case OCH_OPT_TIMING: *value = p->opt_timing; return OCH_OK;
     default: return fail(OCH_E_INVALID, "unknown option %d", option);
     }
 }
@@ -938,6 +950,56 @@ OCH_API int och_gpu_set_stamp_buffer(och_gpu_pool *p, uint64_t *stamps, uint32_t
     return OCH_OK;
 }
 
+namespace {
+
+// Per-launch timing of the traversal kernel (OCH_OPT_TIMING).  1 (default):
+// the dispatch itself records the pool's events (hipExtLaunchKernel, no
+// packets of its own); 2: hipEventRecord before and after the launch (two
+// marker packets, each with a system-scope release: ~10 us of idle GPU
+// between two launches of a stream); 0: none.  Events handed
+// over by och_gpu_set_launch_events take the place of the pool's for one launch.
+och::Schedule timed_schedule(och_gpu_pool *p, int &st)
+{
+    och::Schedule sc = p->schedule();
+    st = OCH_OK;
+    if (p->next_ev_start || p->next_ev_stop) {
+        sc.ev_start = p->next_ev_start;
+        sc.ev_stop = p->next_ev_stop;
+        p->next_ev_start = p->next_ev_stop = nullptr;
+    } else if (p->opt_timing == 1) {
+        sc.ev_start = p->ev_start;
+        sc.ev_stop = p->ev_stop;
+    } else if (p->opt_timing == 2 && hipEventRecord(p->ev_start, p->stream()) != hipSuccess) {
+        st = fail(OCH_E_HIP, "hipEventRecord: %s", hipGetErrorString(hipGetLastError()));
+    }
+    return sc;
+}
+
+// After the launch: och_gpu_last_kernel_ms reads the pool's events only if
+// this launch recorded them (n = 0 launches nothing).
+int timed_done(och_gpu_pool *p, const och::Schedule &sc, bool launched)
+{
+    if (sc.ev_start == p->ev_start && sc.ev_start) {
+        p->timed = launched;
+    } else if (!sc.ev_start && !sc.ev_stop && p->opt_timing == 2) {
+        OCH_HIP(hipEventRecord(p->ev_stop, p->stream()));
+        p->timed = true;
+    } else {
+        p->timed = false;
+    }
+    return OCH_OK;
+}
+
+}  // namespace
+
+OCH_API int och_gpu_set_launch_events(och_gpu_pool *p, void *start_event, void *stop_event)
+{
+    if (!p) return fail(OCH_E_INVALID, "pool is NULL");
+    p->next_ev_start = static_cast<hipEvent_t>(start_event);
+    p->next_ev_stop = static_cast<hipEvent_t>(stop_event);
+    return OCH_OK;
+}
+
 OCH_API int och_gpu_synchronize(och_gpu_pool *p)
 {
     if (!p) return fail(OCH_E_INVALID, "pool is NULL");
@@ -949,7 +1011,9 @@ OCH_API int och_gpu_synchronize(och_gpu_pool *p)
 OCH_API int och_gpu_last_kernel_ms(och_gpu_pool *p, float *ms)
 {
     if (!p || !ms) return fail(OCH_E_INVALID, "pool/ms is NULL");
-    if (!p->timed) return fail(OCH_E_INVALID, "no kernel has been launched on this pool");
+    if (!p->timed)
+        return fail(OCH_E_INVALID, "the last launch on this pool was not timed (none yet, n = 0, OCH_OPT_TIMING 0, "
+                                   "or the caller's events)");
     DeviceGuard g(p->device);
     OCH_HIP(hipEventSynchronize(p->ev_stop));
     OCH_HIP(hipEventElapsedTime(ms, p->ev_start, p->ev_stop));
@@ -965,12 +1029,12 @@ OCH_API int och_gpu_trace_batch_dev(och_gpu_pool *p, const float *origin, int or
     if (origin_stride != 0 && origin_stride != 3) return fail(OCH_E_INVALID, "origin_stride must be 0 or 3");
     if (int rs = check_ready(p)) return rs;
     DeviceGuard g(p->device);
-    OCH_HIP(hipEventRecord(p->ev_start, p->stream()));
+    int ts;
+    const och::Schedule sc = timed_schedule(p, ts);
+    if (ts) return ts;
     OCH_HIP(och::launch_trace_batch(p->dev(), origin, origin_stride, dirs, n, hit_dir, hit_voxel,
-                                    reinterpret_cast<uint32_t *>(hit_time), push_count, p->schedule(), p->stream()));
-    OCH_HIP(hipEventRecord(p->ev_stop, p->stream()));
-    p->timed = true;
-    return OCH_OK;
+                                    reinterpret_cast<uint32_t *>(hit_time), push_count, sc, p->stream()));
+    return timed_done(p, sc, n > 0);
 }
 
 OCH_API int och_gpu_trace_bounce_batch_dev(och_gpu_pool *p, const float *origin, int origin_stride, const float *dirs,
@@ -984,14 +1048,13 @@ OCH_API int och_gpu_trace_bounce_batch_dev(och_gpu_pool *p, const float *origin,
     if (origin_stride != 0 && origin_stride != 3) return fail(OCH_E_INVALID, "origin_stride must be 0 or 3");
     if (int rs = check_ready(p)) return rs;
     DeviceGuard g(p->device);
-    OCH_HIP(hipEventRecord(p->ev_start, p->stream()));
+    int ts;
+    const och::Schedule sc = timed_schedule(p, ts);
+    if (ts) return ts;
     OCH_HIP(och::launch_trace_bounce_batch(p->dev(), origin, origin_stride, dirs, n, hit_dir, hit_voxel,
                                            reinterpret_cast<uint32_t *>(hit_time), bounce_dir, bounce_voxel,
-                                           reinterpret_cast<uint32_t *>(bounce_time), push_count, p->schedule(),
-                                           p->stream()));
-    OCH_HIP(hipEventRecord(p->ev_stop, p->stream()));
-    p->timed = true;
-    return OCH_OK;
+                                           reinterpret_cast<uint32_t *>(bounce_time), push_count, sc, p->stream()));
+    return timed_done(p, sc, n > 0);
 }
 
 namespace {
@@ -1024,7 +1087,9 @@ OCH_API int och_gpu_trace_batch_tiled_dev(och_gpu_pool *p, const float *origin, 
     if (int st = tiled_args(p, origin, origin_stride, dirs, n, width)) return st;
     if (n && (!hit_dir || !hit_voxel || !hit_time)) return fail(OCH_E_INVALID, "NULL argument");
     DeviceGuard g(p->device);
-    och::Schedule sc = p->schedule();
+    int ts;
+    och::Schedule sc = timed_schedule(p, ts);
+    if (ts) return ts;
     if (p->opt_tile_order >= 2 && p->opt_schedule == 0 && p->d_order[2]) {
         int64_t key[9];
         batch_key(p, n, width, key);
@@ -1033,12 +1098,9 @@ OCH_API int och_gpu_trace_batch_tiled_dev(och_gpu_pool *p, const float *origin, 
             sc.order_n = p->plan_blocks[2];
         }
     }
-    OCH_HIP(hipEventRecord(p->ev_start, p->stream()));
     OCH_HIP(och::launch_trace_batch_tiled(p->dev(), origin, origin_stride, dirs, n, width, hit_dir, hit_voxel,
                                           reinterpret_cast<uint32_t *>(hit_time), push_count, sc, p->stream()));
-    OCH_HIP(hipEventRecord(p->ev_stop, p->stream()));
-    p->timed = true;
-    return OCH_OK;
+    return timed_done(p, sc, n > 0);
 }
 
 OCH_API int och_gpu_plan_batch_tiled(och_gpu_pool *p, const float *origin, int origin_stride, const float *dirs,
@@ -1200,7 +1262,9 @@ int render_views(och_gpu_pool *p, const och_camera *cams, int n_views, uint32_t 
     f.slice_rows = p->slice_rows(cams[0].height, row_chunk, n_shards);
     const bool dealt = p->deal_for(cams[0].height, row_chunk, n_shards);
     f.chunk_map = dealt ? p->d_chunk_map + (size_t)shard * p->deal_max : nullptr;
-    och::Schedule sc = p->schedule();
+    int ts;
+    och::Schedule sc = timed_schedule(p, ts);
+    if (ts) return ts;
     const int which = bounce ? 1 : 0;
     if (p->opt_tile_order >= 2 && (bounce || p->opt_schedule == 0) && p->d_order[which]) {
         const int64_t key[9] = {cams[0].width, cams[0].height, n_views, row_chunk, shard, n_shards, p->opt_block,
@@ -1210,16 +1274,13 @@ int render_views(och_gpu_pool *p, const och_camera *cams, int n_views, uint32_t 
             sc.order_n = p->plan_blocks[which];
         }
     }
-    OCH_HIP(hipEventRecord(p->ev_start, p->stream()));
     if (code_slices)
         OCH_HIP(och::launch_render_codes(p->dev(), f, sc, bounce, p->stream()));
     else if (bounce)
         OCH_HIP(och::launch_render_bounce(p->dev(), f, sc, p->stream()));
     else
         OCH_HIP(och::launch_render(p->dev(), f, sc, p->stream()));
-    OCH_HIP(hipEventRecord(p->ev_stop, p->stream()));
-    p->timed = true;
-    return OCH_OK;
+    return timed_done(p, sc, true);
 }
 
 }  // namespace

@@ -133,6 +133,8 @@ struct Schedule {
     uint32_t order_n;       // entries in *order: a launch whose grid differs runs in natural order
     uint32_t *cost;         // grid: optional per-workgroup duration output (the planning launch)
     int merge_k;            // grid, packed, no PUSH counts: in-block wave merging every merge_k iterations (0 off)
+    hipEvent_t ev_start;    // optional: recorded by the traversal kernel's own dispatch (hipExtLaunchKernel)
+    hipEvent_t ev_stop;
 };
 
 hipError_t launch_trace_batch(const DevPool &p, const float *origin, int origin_stride, const float *dirs,

@@ -20,10 +20,24 @@
 // Two ray sources (a ray array, or the camera of tree_camera::update_position
 // mapped 8x8-pixel tile per wave) and two sinks (hit records, or the shaded
 // RGBA8 framebuffer of update_image) make up trace_batch and render.
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
 #include "och_internal.h"
+
+// A traversal launch, timed by the dispatch itself when the schedule carries
+// events (Schedule::ev_start / ev_stop, OCH_OPT_TIMING): hipExtLaunchKernel
+// takes the kernel's own start and end times, with no packets of its own
+// between two launches of a stream.
+#define OCH_LAUNCH_TIMED(sc, kernel, grid, block, lds, stream, ...)                                                   \
+    do {                                                                                                             \
+        if ((sc).ev_start || (sc).ev_stop)                                                                           \
+            hipExtLaunchKernelGGL(kernel, grid, block, (uint32_t)(lds), stream, (sc).ev_start, (sc).ev_stop, 0u,     \
+                                  __VA_ARGS__);                                                                      \
+        else                                                                                                         \
+            hipLaunchKernelGGL(kernel, grid, block, lds, stream, __VA_ARGS__);                                       \
+    } while (0)
 
 namespace och {
 namespace {
@@ -1607,7 +1621,7 @@ hipError_t launch_as(const DevPool &p, const Src &s, const Sink &k, uint32_t n, 
     if (sc.kind == 2) {
         const uint32_t chunk = 64u * (uint32_t)sc.chunk_tiles;
         const uint32_t waves = (n + chunk - 1) / chunk, wpb = (uint32_t)block / 64u;
-        hipLaunchKernelGGL((k_trace_refill<Src, Sink, kPacked, kCount>), dim3((waves + wpb - 1) / wpb), dim3(block),
+        OCH_LAUNCH_TIMED(sc, (k_trace_refill<Src, Sink, kPacked, kCount>), dim3((waves + wpb - 1) / wpb), dim3(block),
                            lds, stream, p, s, k, chunk, sc.refill_min, sc.stamps, sc.stamp_cap);
     } else if (sc.kind == 1) {
         hipError_t e = hipMemsetAsync(sc.counter, 0, sizeof(uint32_t), stream);
@@ -1616,11 +1630,11 @@ hipError_t launch_as(const DevPool &p, const Src &s, const Sink &k, uint32_t n, 
         uint32_t grid = (uint32_t)sc.cus * blocks_per_cu;
         const uint32_t needed = (n + block - 1) / block;
         if (grid > needed) grid = needed;
-        hipLaunchKernelGGL((k_trace_persistent<Src, Sink, kPacked, kCount>), dim3(grid), dim3(block), lds, stream, p, s,
+        OCH_LAUNCH_TIMED(sc, (k_trace_persistent<Src, Sink, kPacked, kCount>), dim3(grid), dim3(block), lds, stream, p, s,
                            k, sc.counter, sc.refill_min, sc.stamps, sc.stamp_cap);
     } else if (sc.merge_k > 0 && kPacked && !kCount && block >= 128 && block <= 1024) {
         const uint32_t grid = (n + block - 1) / block;
-        hipLaunchKernelGGL((k_trace_grid_merge<Src, Sink>), dim3(grid), dim3(block),
+        OCH_LAUNCH_TIMED(sc, (k_trace_grid_merge<Src, Sink>), dim3(grid), dim3(block),
                            lds > kMergeWords * 4u * (size_t)block ? lds : kMergeWords * 4u * (size_t)block, stream, p,
                            s, k, sc.merge_k, sc.order_n == grid ? sc.order : nullptr);
     } else {
@@ -1629,7 +1643,7 @@ hipError_t launch_as(const DevPool &p, const Src &s, const Sink &k, uint32_t n, 
         const uint32_t grid = (n + per_block - 1) / per_block;
         // a plan is a permutation of exactly this grid's workgroups; any other
         // (stale or for another block size) would index past it
-        hipLaunchKernelGGL((k_trace_grid<Src, Sink, kPacked, kCount>), dim3(grid), dim3(block),
+        OCH_LAUNCH_TIMED(sc, (k_trace_grid<Src, Sink, kPacked, kCount>), dim3(grid), dim3(block),
                            OCH_DUAL ? 2 * lds : lds, stream, p, s, k, xcd_group, sc.order_n == grid ? sc.order : nullptr,
                            sc.cost, sc.stamps, sc.stamp_cap);
     }
@@ -1655,10 +1669,10 @@ hipError_t launch_bounce(const DevPool &p, const Src &s, const Sink &k, uint32_t
     const dim3 grid((n + block - 1) / block);
     const uint32_t *order = sc.order_n == grid.x ? sc.order : nullptr;   // a plan of exactly this grid
     if (p.packed)
-        hipLaunchKernelGGL((k_trace_bounce<Src, Sink, true, kCount>), grid, dim3(block), lds, stream, p, s, k,
+        OCH_LAUNCH_TIMED(sc, (k_trace_bounce<Src, Sink, true, kCount>), grid, dim3(block), lds, stream, p, s, k,
                            sc.bounce_compact, order, sc.cost, sc.stamps, sc.stamp_cap);
     else
-        hipLaunchKernelGGL((k_trace_bounce<Src, Sink, false, kCount>), grid, dim3(block), lds, stream, p, s, k,
+        OCH_LAUNCH_TIMED(sc, (k_trace_bounce<Src, Sink, false, kCount>), grid, dim3(block), lds, stream, p, s, k,
                            sc.bounce_compact, order, sc.cost, sc.stamps, sc.stamp_cap);
     return hipGetLastError();
 }

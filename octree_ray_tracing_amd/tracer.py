@@ -160,7 +160,7 @@ class GpuPool:
         call("och_gpu_pool_update", self._h, int(first), nodes.shape[0], _np_ptr(nodes), int(root))
 
     OPTIONS = {"schedule": 0, "block": 1, "waves_per_cu": 2, "refill": 3, "layout": 4, "tile_order": 5,
-               "bounce_compact": 6, "chunk_tiles": 7, "cull": 8, "merge": 9}
+               "bounce_compact": 6, "chunk_tiles": 7, "cull": 8, "merge": 9, "timing": 10}
 
     def set_option(self, name: str, value: int):
         """Launch options (och_gpu_set_option): schedule (0 grid / 1 persistent / 2 grid with lane
@@ -190,6 +190,16 @@ class GpuPool:
         ms = C.c_float()
         call("och_gpu_last_kernel_ms", self._h, C.byref(ms))
         return ms.value
+
+    def set_launch_events(self, start, stop):
+        """The next trace/render launch records these HIP events (raw hipEvent_t
+        handles, or objects with an ``h`` handle) through its own dispatch."""
+        def handle(e):
+            if e is None:
+                return None
+            h = getattr(e, "h", e)
+            return h.value if hasattr(h, "value") else int(h)
+        call("och_gpu_set_launch_events", self._h, handle(start), handle(stop))
 
     # -- tracing (reference signature)
     def sse_trace(self, ox, oy, oz, dx, dy, dz):
