@@ -413,6 +413,8 @@ def main():
                     help="diagnostic: the pool's OCH_OPT_TIMING for launches without step events (default 1)")
     ap.add_argument("--no-fast-issue", action="store_true",
                     help="diagnostic: issue N = 1 steps through the Python wrappers and torch stream contexts")
+    ap.add_argument("--pin-core", action="store_true",
+                    help="diagnostic: pin the issuing (main) thread to one of its allowed CPUs")
     ap.add_argument("--host-rehearse", action="store_true",
                     help="diagnostic: before a window, switch the pool and torch to each frame stream (no GPU work)")
     ap.add_argument("--host-stamps", action="store_true",
@@ -664,6 +666,8 @@ def main():
                 ev.append((e0, e1))
             f_.exchange()
 
+    if a.pin_core:
+        os.sched_setaffinity(0, {sorted(os.sched_getaffinity(0))[0]})
     stamps = {}                            # --host-stamps
     trace_parts = False
     in_window = False

@@ -9,5 +9,5 @@ for m in fast slow fast slow; do
   timeout -k 10 300 python -u bench.py $B $X > $O/b_$m.json 2> $O/b_$m.err || exit 2
   cp $O/b_$m.json $O/b_${m}_$(date +%s%N).json
 done
-EXTRA="" bash tools/r03t_run.sh || exit 3
+EXTRA="$EXTRA" bash tools/r03t_run.sh || exit 3
 cp gpurun_out/r03t/stamps.txt $O/stamps_fast.txt
