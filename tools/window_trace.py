@@ -79,9 +79,12 @@ def window(rows):
 
 
 def summarise(win, steps: int) -> dict:
-    t0 = min(r["start"] for r in win)
-    t1 = max(r["end"] for r in win)
-    ev = sorted([(r["start"], 1) for r in win] + [(r["end"], -1) for r in win])
+    # the step kernels; "other" is runtime copies (the window's elapsed-time
+    # tensor goes to the device after the host has stopped its clock)
+    steps_k = [r for r in win if r["fam"] != "other"] or win
+    t0 = min(r["start"] for r in steps_k)
+    t1 = max(r["end"] for r in steps_k)
+    ev = sorted([(r["start"], 1) for r in steps_k] + [(r["end"], -1) for r in steps_k])
     hist = defaultdict(int)
     busy, k, last = 0, 0, ev[0][0]
     for t, d in ev:
@@ -90,7 +93,7 @@ def summarise(win, steps: int) -> dict:
         hist[k] += t - last
         k += d
         last = t
-    total = sum(r["end"] - r["start"] for r in win)
+    total = sum(r["end"] - r["start"] for r in steps_k)
     fams = defaultdict(list)
     for r in win:
         fams[r["fam"]].append((r["end"] - r["start"]) / 1e6)
@@ -110,15 +113,20 @@ def summarise(win, steps: int) -> dict:
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("trace_dir")
+    ap.add_argument("trace_dir", help="rocprofv3 output directory, or a window CSV of an earlier run")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--config", default="d12_1920x1080_n1")
     ap.add_argument("--bench-json", help="the bench line printed by the profiled run (its ms_per_step)")
     ap.add_argument("--out")
     ap.add_argument("--csv", help="write the window's kernel rows here")
     a = ap.parse_args()
-    rows = read_trace(Path(a.trace_dir))
-    win = window(rows)
+    if a.trace_dir.endswith(".csv"):          # a window CSV written by --csv (times in us)
+        with open(a.trace_dir, newline="") as fh:
+            win = [{"name": r["kernel"], "fam": r["kernel"], "stream": r["stream"], "queue": r["queue"],
+                    "start": int(float(r["start_us"]) * 1e3), "end": int(float(r["end_us"]) * 1e3)}
+                   for r in csv.DictReader(fh)]
+    else:
+        win = window(read_trace(Path(a.trace_dir)))
     d = {"config": a.config, "kernel_source_sha": kernel_source_digest(), **summarise(win, a.steps)}
     if a.bench_json:
         line = json.loads(Path(a.bench_json).read_text().strip().splitlines()[-1])
