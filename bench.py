@@ -612,16 +612,21 @@ def main():
     # here -- no torch stream context or wrapper code per step.  The first step of a
     # window otherwise took ~0.1 ms longer to issue than the rest, while the GPU
     # waited (rocprofv3 --hip-trace, profiles/r03/window/).
+    # N > 1 (colour codes): the render is issued the same way; the all-gather and
+    # the display rank's shade stay in ShardedFrame.exchange, on the frame's stream.
     fast = None
-    if direct and not a.no_fast_issue:
+    if (direct or (indexed and world > 1)) and not a.no_fast_issue:
         from octree_ray_tracing_amd._lib import Camera, load as load_lib
         lib = load_lib()
         cam_arr = (Camera * len(cams))(*cams)
         h = pool._h
-        fast = {"lib": lib, "cams": cam_arr, "h": h,
-                "args": [[(h, ctypes.c_void_p(s_.cuda_stream)),
-                          (h, ctypes.cast(cam_arr, ctypes.c_void_p), len(cams), ctypes.c_void_p(f_.frames.data_ptr()),
-                           a.row_chunk, 0, 1)] for s_, f_ in zip(streams, sfs)]}
+        cp = ctypes.cast(cam_arr, ctypes.c_void_p)
+        if direct:
+            args = [(h, cp, len(cams), ctypes.c_void_p(f_.frames.data_ptr()), a.row_chunk, 0, 1) for f_ in sfs]
+        else:
+            args = [(h, cp, len(cams), ctypes.c_void_p(f_.slice.data_ptr()), a.row_chunk, rank, world) for f_ in sfs]
+        fast = {"lib": lib, "cams": cam_arr, "h": h, "direct": direct,
+                "args": [[(h, ctypes.c_void_p(s_.cuda_stream)), ra] for s_, ra in zip(streams, args)]}
 
     def step_fast(k, ev, bounce):
         lib, (sa, ra) = fast["lib"], fast["args"][k % len(streams)]
@@ -630,9 +635,16 @@ def main():
             e0, e1 = ev_pool[len(ev) % len(ev_pool)]
             st |= lib.och_gpu_set_launch_events(fast["h"], e0.h, e1.h)
             ev.append((e0, e1))
-        st |= (lib.och_gpu_render_bounce_views_dev if bounce else lib.och_gpu_render_views_dev)(*ra)
+        if fast["direct"]:
+            st |= (lib.och_gpu_render_bounce_views_dev if bounce else lib.och_gpu_render_views_dev)(*ra)
+        else:
+            st |= lib.och_gpu_render_codes_views_dev(*ra, int(bool(bounce)))
         if st:
             raise RuntimeError(f"step {k}: {lib.och_last_error().decode()}")
+        if not fast["direct"]:
+            s_ = streams[k % len(streams)]
+            with torch.cuda.stream(s_):
+                sfs[k % len(sfs)].exchange()
 
     def step(k, ev=None, bounce=False):
         """One step: render both views of this rank's rows, all-gather, unshard --
