@@ -43,7 +43,8 @@ def main():
     ap.add_argument("--cache", default="/tmp/och_terrain_cache.npz")
     ap.add_argument("--out", default="gpurun_out/proxy_rank.json")
     ap.add_argument("--no-exchange", action="store_true", help="render only: no gather copy, no shade")
-    ap.add_argument("--events", action="store_true", help="record timing events around every render, as bench.py")
+    ap.add_argument("--events", action="store_true",
+                    help="timing events on every render, recorded by its dispatch (as bench.py)")
     ap.add_argument("--opt", action="append", default=[], metavar="NAME=VALUE", help="pool option, e.g. chain=1")
     ap.add_argument("--shards", default="0", help="'all', or a comma list of shards to time")
     ap.add_argument("--shade", choices=("display", "all"), default="display",
@@ -134,22 +135,28 @@ def arm(a, torch, pool, streams, cams, W, H, world, shard, nf, opts, deal=None, 
     rows = sfs[0].rows
     rays_rank = int((slice_row_map(H, 8, world, shard, deal) >= 0).sum()) * W * 2
 
-    def run(n):
+    from bench import FenceFreeEvent
+    evs = [(FenceFreeEvent(), FenceFreeEvent()) for _ in range(64)] if a.events else None
+
+    def drain():
+        # as bench.py: poll the streams idle, then synchronize (no interrupt wake-up)
+        while not all(s_.query() for s_ in streams):
+            pass
         torch.cuda.synchronize()
+
+    def run(n):
+        drain()
         t0 = time.perf_counter()
         for k in range(n):
             s_, f_ = streams[k % nf], sfs[k % nf]
             pool.set_stream(s_)
             with torch.cuda.stream(s_):
-                if a.events:
-                    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                    e0.record(s_)
+                if evs is not None:                 # as bench.py: recorded by the render's own dispatch
+                    pool.set_launch_events(*evs[k % len(evs)])
                 f_.render_local(cams)
-                if a.events:
-                    e1.record(s_)
                 if not a.no_exchange:
                     f_.exchange()
-        torch.cuda.synchronize()
+        drain()
         return time.perf_counter() - t0
 
     run(5)
