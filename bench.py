@@ -16,7 +16,7 @@ config is quoted at), each being the reference's update_position +
 update_image (raygen, SVO-DAG traversal, palette shading) as one fused gfx950
 launch for both views, then the exchange.
 
-Steps alternate over --inflight (default 3) HIP streams with their own frame
+Steps alternate over --inflight (default 3; 6 at N >= 8) HIP streams with their own frame
 buffers, so one step's slowest rays (a few grazing tiles)
 overlap the next step's bulk; every step is rendered in full.  The serial
 frame latency is reported beside it (roofline.kernel_ms_serial).
@@ -438,10 +438,29 @@ def main():
     ap.add_argument("--no-direct", action="store_true",
                     help="N = 1: render codes and shade them in a second pass, as ranks do at N > 1, instead of "
                          "the fused launch writing the RGBA8 frames directly")
-    ap.add_argument("--inflight", type=int, default=3,
+    ap.add_argument("--inflight", type=int, default=None,
                     help="frames in flight: steps alternate over this many HIP streams, so one step's "
-                         "slowest rays overlap the next step's bulk (1 = serialised)")
+                         "slowest rays overlap the next step's bulk (1 = serialised); default 3, 6 at N >= 8")
+    ap.add_argument("--hw-queues", type=int, default=None,
+                    help="GPU_MAX_HW_QUEUES for this process (set before HIP starts); default the "
+                         "environment's (4 on the box), 8 at N >= 8")
     a = ap.parse_args()
+
+    # Frames in flight and hardware queues by world size (tools/proxy_rank.py,
+    # every shard, profiles/r03/proxy/r03z*): at N = 8 a rank's launches are half
+    # the size of N = 1's and end on the same ~0.2 ms grazing tiles, so more
+    # frames must overlap -- 6 frames on 8 hardware queues: job 192 -> 211 G rays/s
+    # over 20 steps, 215 -> 242 G sustained; at N = 1, 2, 4 the default 3 on 4
+    # queues is best.
+    world_env = int(os.environ.get("WORLD_SIZE", "1"))
+    if a.inflight is None:
+        a.inflight = 6 if world_env >= 8 else 3
+    if a.hw_queues is None and world_env >= 8:
+        a.hw_queues = 8
+    if a.hw_queues is not None:
+        if not 1 <= a.hw_queues <= 32:
+            raise SystemExit("--hw-queues must be in 1..32")
+        os.environ["GPU_MAX_HW_QUEUES"] = str(a.hw_queues)
 
     import torch
     import torch.distributed as dist
@@ -964,6 +983,8 @@ def main():
                        "pool_mb": round(nodes.nbytes / 2**20, 1), "build_s": round(build_s, 2),
                        "build": "och_build_terrain, use_gpu=1: 32^3 bricks voxelised, hash-consed and renumbered on the GPU",
                        "parallelism": f"rows{world}",
+                       "frames_in_flight": len(streams),
+                       "hw_queues": int(os.environ.get("GPU_MAX_HW_QUEUES", "4")),
                        "row_deal": (None if world == 1 else
                                     "round-robin 8-row chunks" if deal is None else
                                     f"row chunks dealt by {a.deal} (och_deal_chunks), rank 0 weight "
