@@ -189,7 +189,8 @@ def build_pool_nodes(depth: int, rank: int, world: int, dev):
     return nodes, root, tree_nodes, build_s
 
 
-def cpu_leg(nodes, root, depth, width, height, frames, bounce_frames, time_it: bool, budget_s: float):
+def cpu_leg(nodes, root, depth, width, height, frames, bounce_frames, time_it: bool, budget_s: float,
+            moving=None):
     """The cpu leg, rank 0: the CPU oracle (a C port of the reference tracer
     with the host's native RCPPS; test infrastructure, used only here as the
     baseline and the checker).
@@ -229,7 +230,16 @@ def cpu_leg(nodes, root, depth, width, height, frames, bounce_frames, time_it: b
             parity["frames"] += 1
             parity["pixels"] += int(w.size)
             parity["mismatches"] += int(np.count_nonzero(bounce_frames[v].view(np.uint32) != w))
+    if moving is not None:                   # (yaw, frames) of the moving-camera window's last step
+        yaw_m, frames_m = moving
+        for v, p in enumerate(PITCHES):
+            r = O.trace_batch(pool, rcp, origin, O.raygen(yaw_m, p, FOV, width, height), nthreads=threads)
+            w = O.shade_fast(r["dir"], r["voxel"], pal).reshape(height, width)
+            parity["frames"] += 1
+            parity["pixels"] += int(w.size)
+            parity["mismatches"] += int(np.count_nonzero(frames_m[v].view(np.uint32) != w))
     parity["checked"] = ("last timed step: both views, primary" + (" and config 5" if bounce_frames is not None else "")
+                         + (" and the moving-camera window's last step" if moving is not None else "")
                          + ", GPU RGBA8 frames vs oracle trace + trace_pixel shading, native RCPPS on both sides")
     if not time_it:
         return None, parity
@@ -411,6 +421,11 @@ def main():
                     help="diagnostic: busy-loop the host this long after each synchronize around a window")
     ap.add_argument("--pool-timing", type=int, default=None,
                     help="diagnostic: the pool's OCH_OPT_TIMING for launches without step events (default 1)")
+    ap.add_argument("--moving-steps", type=int, default=20,
+                    help="N = 1: also time this many steps of a camera panning by --moving-dyaw per step, its "
+                         "launch order planned once from the first step's cameras (and in natural order); 0 = off")
+    ap.add_argument("--moving-dyaw", type=float, default=0.004,
+                    help="yaw change per step of the moving-camera window (radians; 0.004 = 14 deg/s at 60 fps)")
     ap.add_argument("--no-fast-issue", action="store_true",
                     help="diagnostic: issue N = 1 steps through the Python wrappers and torch stream contexts")
     ap.add_argument("--pin-core", action="store_true",
@@ -850,6 +865,59 @@ def main():
             pool.plan_views(cams, a.row_chunk, rank, world)
         pool.set_stream(stream)
 
+    # A moving camera (N = 1): the bench's cameras pan by dyaw per step, so no
+    # step's launch order was planned from its own cameras -- the plan is made
+    # once from the first step's (as an interactive app would plan from an
+    # earlier frame), and the same window runs in natural order for comparison.
+    moving, moving_frames = None, None
+    if direct and a.moving_steps > 0:
+        from octree_ray_tracing_amd._lib import Camera, load as load_lib
+        lib = load_lib()
+        n_mv = a.moving_steps
+        seq = [[ort.camera(ORIGIN, YAW + k * a.moving_dyaw, p, FOV, W, H) for p in PITCHES]
+               for k in range(a.warmup + n_mv)]
+        arrs = [(Camera * len(c))(*c) for c in seq]
+        fr = [ctypes.c_void_p(f_.frames.data_ptr()) for f_ in sfs]
+        sp = [ctypes.c_void_p(s_.cuda_stream) for s_ in streams]
+
+        def mv_step(k):
+            j = k % len(streams)
+            st = lib.och_gpu_set_stream(pool._h, sp[j])
+            st |= lib.och_gpu_render_views_dev(pool._h, ctypes.cast(arrs[k], ctypes.c_void_p), len(PITCHES), fr[j],
+                                               a.row_chunk, 0, 1)
+            if st:
+                raise RuntimeError(lib.och_last_error().decode())
+
+        def mv_window():
+            for k in range(a.warmup):
+                mv_step(k)
+            drain()
+            t0 = time.perf_counter()
+            for k in range(a.warmup, a.warmup + n_mv):
+                mv_step(k)
+            drain()
+            return time.perf_counter() - t0
+
+        order_prev = pool.get_option("tile_order")
+        rays_mv = W * H * len(PITCHES) * n_mv
+        pool.set_option("tile_order", 2)
+        pool.plan_views(seq[0], a.row_chunk, 0, 1)
+        el_plan = mv_window()
+        last = (a.warmup + n_mv - 1) % len(sfs)
+        moving_frames = (YAW + (a.warmup + n_mv - 1) * a.moving_dyaw, sfs[last].frames.cpu().numpy())
+        pool.set_option("tile_order", 0)
+        el_nat = mv_window()
+        pool.set_option("tile_order", order_prev)
+        if order_prev >= 2:
+            pool.plan_views(cams, a.row_chunk, rank, world)
+        pool.set_stream(stream)
+        moving = {"value": round(rays_mv / el_plan / 1e6, 2), "ms_per_step": round(el_plan / n_mv * 1e3, 4),
+                  "value_natural_order": round(rays_mv / el_nat / 1e6, 2), "steps": n_mv, "warmup": a.warmup,
+                  "dyaw_per_step": a.moving_dyaw,
+                  "yaw_range": [YAW, round(YAW + (a.warmup + n_mv - 1) * a.moving_dyaw, 4)],
+                  "note": "camera panning every step; launch order planned once from the first step's cameras "
+                          "(value) or natural order (value_natural_order); the last step is checked in parity"}
+
     # Config 5 (BASELINE configs[4]): the same frames with one mirrored
     # secondary ray per hit pixel, in-block wavefront compaction on; same
     # pipelining and timing discipline.  Rays = primary + secondary.
@@ -952,7 +1020,8 @@ def main():
     cpu, parity = None, None
     if rank == 0 and not a.no_parity:
         cpu, parity = cpu_leg(nodes, root, a.depth, W, H, frames_host, bounce_host,
-                              time_it=world == 1 and not a.no_cpu_baseline, budget_s=a.cpu_budget)
+                              time_it=world == 1 and not a.no_cpu_baseline, budget_s=a.cpu_budget,
+                              moving=moving_frames)
 
     if rank == 0:
         if world == 1:
@@ -1002,6 +1071,7 @@ def main():
             "sustained": sustained,
             "value_cull_off": None if cull_off is None else cull_off["value"],
             "cull_off": cull_off,
+            **({"moving_camera": moving} if moving else {}),
             "walked_rays_per_s": round(value * (1 - culled / rays_rank), 2),
             "walked_rays_note": "Mrays/s of the rays that walk the DAG (value x (1 - culled_frac)); the "
                                 "occupied-box cull ends the rest as proven misses",
