@@ -174,10 +174,13 @@ typedef enum och_option {
                                   128..1024 threads, merge the block's waves every K iterations: the rays left
                                   move into the free lanes of the fewest waves, the emptied waves exit (records
                                   unchanged).  0 (default) = off */
-    OCH_OPT_TIMING = 10        /* per-launch timing of trace/render kernels (och_gpu_last_kernel_ms):
+    OCH_OPT_TIMING = 10,       /* per-launch timing of trace/render kernels (och_gpu_last_kernel_ms):
                                   1 (default) = recorded by the kernel's own dispatch (hipExtLaunchKernel: no
                                   packets between two launches of a stream); 2 = hipEventRecord before and
                                   after the launch; 0 = not timed */
+    OCH_OPT_PLAN = 11          /* shape of och_gpu_plan_views' launch order (set before planning): 0 =
+                                  costliest first; P in 1..99 = the costliest P % first, the rest in natural
+                                  order (default 10); 100 = costliest and cheapest alternating */
 } och_option;
 OCH_API int och_gpu_set_option(och_gpu_pool *pool, int option, int value);
 OCH_API int och_gpu_get_option(const och_gpu_pool *pool, int option, int *value);

@@ -158,6 +158,7 @@ struct och_gpu_pool {
     int opt_cull = 1;
     int opt_merge = 0;
     int opt_timing = 1;                        // OCH_OPT_TIMING
+    int opt_plan = 10;                         // OCH_OPT_PLAN (shape of och_gpu_plan_views' order)
     hipEvent_t next_ev_start = nullptr;        // och_gpu_set_launch_events: the next launch's events
     hipEvent_t next_ev_stop = nullptr;
     // bounding box of the pool's voxels (voxel units, [lo, hi)), for the cull
@@ -910,6 +911,10 @@ OCH_API int och_gpu_set_option(och_gpu_pool *p, int option, int value)
         if (value < 0 || value > 2) return fail(OCH_E_INVALID, "timing must be 0, 1 or 2");
         p->opt_timing = value;
         return OCH_OK;
+    case OCH_OPT_PLAN:
+        if (value < 0 || value > 100) return fail(OCH_E_INVALID, "plan shape must be 0..100");
+        p->opt_plan = value;
+        return OCH_OK;
     default:
         return fail(OCH_E_INVALID, "unknown option %d", option);
     }
@@ -930,6 +935,7 @@ OCH_API int och_gpu_get_option(const och_gpu_pool *p, int option, int *value)
     case OCH_OPT_CULL: *value = p->opt_cull; return OCH_OK;
     case OCH_OPT_MERGE: *value = p->opt_merge; return OCH_OK;
     case OCH_OPT_TIMING: *value = p->opt_timing; return OCH_OK;
+    case OCH_OPT_PLAN: *value = p->opt_plan; return OCH_OK;
     default: return fail(OCH_E_INVALID, "unknown option %d", option);
     }
 }
@@ -1285,6 +1291,42 @@ int render_views(och_gpu_pool *p, const och_camera *cams, int n_views, uint32_t 
 
 }  // namespace
 
+namespace {
+
+// The launch order from the costliest-first list (OCH_OPT_PLAN): 0 = all
+// workgroups costliest first; P in 1..99 = the costliest P % first, then the
+// rest in natural order (the tails a frame ends on start early, while the bulk
+// keeps the raster order's mix of sky and terrain tiles); 100 = alternate the
+// costliest and the cheapest left.  Default 10: with frames in flight, every
+// frame starting all its costly tiles at once cost 3.5 % over long runs
+// (profiles/r03/ab/plan_*).
+void plan_shape(std::vector<uint32_t> &order, int mode)
+{
+    const size_t n = order.size();
+    if (mode <= 0 || n < 2) return;
+    std::vector<uint32_t> out;
+    out.reserve(n);
+    if (mode >= 100) {
+        for (size_t i = 0, j = n - 1; i <= j && j < n; ++i, --j) {
+            out.push_back(order[i]);
+            if (j != i) out.push_back(order[j]);
+            if (j == 0) break;
+        }
+    } else {
+        const size_t head = n * (size_t)mode / 100;
+        std::vector<uint8_t> taken(n, 0);
+        for (size_t i = 0; i < head; ++i) {
+            out.push_back(order[i]);
+            taken[order[i]] = 1;
+        }
+        for (uint32_t b = 0; b < n; ++b)
+            if (!taken[b]) out.push_back(b);
+    }
+    order.swap(out);
+}
+
+}  // namespace
+
 OCH_API int och_gpu_plan_views(och_gpu_pool *p, const och_camera *cams, int n_views, int row_chunk, int shard,
                                int n_shards)
 {
@@ -1338,6 +1380,7 @@ OCH_API int och_gpu_plan_views(och_gpu_pool *p, const och_camera *cams, int n_vi
         std::vector<uint32_t> order(n_blocks);
         for (uint32_t i = 0; i < n_blocks; ++i) order[i] = i;
         std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return c[a] > c[b]; });
+        plan_shape(order, p->opt_plan);
         // Grouped per XCD (OCH_OPT_TILE_ORDER = 3): workgroup slot i runs on XCD
         // i % 8, so deal 64x64-pixel supertiles over the XCDs (each XCD's L2 then
         // holds the nodes of its own neighbouring tiles) and keep the costliest-
