@@ -550,6 +550,11 @@ def main():
     # frames identical), so no frame ends on a few late grazing tiles.
     if not any(kv.startswith("tile_order=") for kv in a.opt):
         pool.set_option("tile_order", 2)
+    if world >= 8 and not any(kv.startswith("plan=") for kv in a.opt):
+        # N = 8 (proxy, 6 frames on 8 queues, profiles/r03/ab/plan_n8/): costliest-first
+        # 204-210 G over 20 steps against 200-202 G for the 10 % shape (sustained
+        # 238-243 against 244-247 G); the driver times 20 steps
+        pool.set_option("plan", 0)
     if a.pool_timing is not None:
         pool.set_option("timing", a.pool_timing)
     if pool.get_option("tile_order") >= 2:
