@@ -537,8 +537,8 @@ def test_refill_schedule_variants(ort, O, gpu_device, chunk, refill):
     pool.close()
 
 
-@pytest.mark.parametrize("order", [2, 3])
-def test_planned_launch_order(ort, O, gpu_device, order):
+@pytest.mark.parametrize("order,shape", [(2, 10), (3, 10), (2, 0), (2, 100)])
+def test_planned_launch_order(ort, O, gpu_device, order, shape):
     """OCH_OPT_TILE_ORDER = 2: the costliest tiles of a planning frame go first
     (och_gpu_plan_views); 3: the same, 64x64-pixel supertiles dealt over the XCDs.  Dispatch order only: frames of the planned geometry,
     of another geometry (natural order) and after the camera moved are all
@@ -552,6 +552,8 @@ def test_planned_launch_order(ort, O, gpu_device, order):
     ref_pool = O.OraclePool(tree.nodes, tree.root, 9, 1)
     W, H = 803, 451
     cams = [ort.camera((1.5, 1.5, 1.5), 0.3, p, 1.25, W, H) for p in (0.0, -0.6)]
+    assert pool.get_option("plan") == 10                 # default shape: costliest 10 % first
+    pool.set_option("plan", shape)                       # OCH_OPT_PLAN: 0 all costliest first, 100 alternating
     pool.plan_views(cams, 8, 0, 1)
     pool.set_option("tile_order", order)
     for yaw in (0.3, 0.9):                   # the planned views, then a moved camera
