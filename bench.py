@@ -44,7 +44,6 @@ import math
 import os
 import statistics
 import sys
-import threading
 import time
 from pathlib import Path
 
@@ -429,8 +428,6 @@ def main():
                     help="yaw change per step of the moving-camera window (radians; 0.004 = 14 deg/s at 60 fps)")
     ap.add_argument("--no-fast-issue", action="store_true",
                     help="diagnostic: issue N = 1 steps through the Python wrappers and torch stream contexts")
-    ap.add_argument("--isolate-main", action="store_true",
-                    help="diagnostic, with --pin-core: move the process's other threads off the issuing CPU")
     ap.add_argument("--pin-core", action="store_true",
                     help="diagnostic: pin the issuing (main) thread to one of its allowed CPUs")
     ap.add_argument("--host-rehearse", action="store_true",
@@ -643,43 +640,7 @@ def main():
                          "per wave; per_view = one launch per view, two_views = both views' rays in one launch "
                          "(W x 2H, planned with och_gpu_plan_batch_tiled)")
         trace_only["tiled"] = tiled
-        # Coherence order (OCH_OPT_SORT): the untiled API sorts the batch by origin
-        # cell and direction on the device, then walks it; timed whole (keys + radix
-        # sort + trace) on the camera rays of both views in one batch, and on a batch
-        # of random rays (per-ray origins in the root, random directions), sorted
-        # and not.
-        def time_batch(o_, d_, n_rays, reps=10):
-            tms_ = []
-            for _ in range(3):
-                pool.trace_batch_dev(o_, d_, bd, bv, bt, n=n_rays)
-            for _ in range(reps):
-                s0, s1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                s0.record(stream)
-                pool.trace_batch_dev(o_, d_, bd, bv, bt, n=n_rays)
-                s1.record(stream)
-                tms_.append((s0, s1))
-            torch.cuda.synchronize()
-            ms_ = np.array([x.elapsed_time(y) for x, y in tms_])
-            return {"mrays_s": round(n_rays * reps / ms_.sum() / 1e3, 1), "ms_per_launch": round(float(ms_.mean()), 4)}
-
-        gen = torch.Generator(device=dev)
-        gen.manual_seed(1)
-        r_o = torch.rand(2 * n_px * 3, generator=gen, device=dev) * 0.98 + 1.01
-        r_d = torch.rand(2 * n_px * 3, generator=gen, device=dev) * 2.0 - 1.0
-        sort_prev = pool.get_option("sort")
-        sorted_ = {}
-        for label, o_, d_ in (("camera_two_views", o_t, both), ("random", r_o, r_d)):
-            pool.set_option("sort", 0)
-            sorted_[label] = {"unsorted": time_batch(o_, d_, 2 * n_px)}
-            pool.set_option("sort", 1)
-            sorted_[label]["sorted"] = time_batch(o_, d_, 2 * n_px)
-        pool.set_option("sort", sort_prev)
-        sorted_["path"] = ("och_gpu_trace_batch_dev with OCH_OPT_SORT 1 (device keys + rocprim radix sort + walk in "
-                           "sorted order, records in the caller's order; timed whole) against 0; "
-                           f"{2 * n_px} rays per batch: both camera views, or random rays (origins in (1.01, 1.99)^3, "
-                           "directions uniform in [-1, 1]^3)")
-        trace_only["sort"] = sorted_
-        del both, bd, bv, bt, r_o, r_d
+        del both, bd, bv, bt
     del hd, hv, ht, hp, dirs
 
     # timing events for every step of a window, created once, outside the timed region
@@ -757,16 +718,7 @@ def main():
             f_.exchange()
 
     if a.pin_core:
-        cpus = sorted(os.sched_getaffinity(0))
-        main_tid = threading.get_native_id()
-        os.sched_setaffinity(0, {cpus[0]})
-        if a.isolate_main and len(cpus) > 1:   # every other thread of the process off the issuing CPU
-            for tid in os.listdir("/proc/self/task"):
-                if int(tid) != main_tid:
-                    try:
-                        os.sched_setaffinity(int(tid), set(cpus[1:]))
-                    except OSError:
-                        pass
+        os.sched_setaffinity(0, {sorted(os.sched_getaffinity(0))[0]})
     stamps = {}                            # --host-stamps
     trace_parts = False
     in_window = False

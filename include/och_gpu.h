@@ -178,12 +178,9 @@ typedef enum och_option {
                                   1 (default) = recorded by the kernel's own dispatch (hipExtLaunchKernel: no
                                   packets between two launches of a stream); 2 = hipEventRecord before and
                                   after the launch; 0 = not timed */
-    OCH_OPT_PLAN = 11,         /* shape of och_gpu_plan_views' launch order (set before planning): 0 =
+    OCH_OPT_PLAN = 11          /* shape of och_gpu_plan_views' launch order (set before planning): 0 =
                                   costliest first; P in 1..99 = the costliest P % first, the rest in natural
                                   order (default 10); 100 = costliest and cheapest alternating */
-    OCH_OPT_SORT = 12          /* 1 = och_gpu_trace_batch(_dev) and the bounce batch walk batches of >= 16384
-                                  rays in coherence order (sorted by origin cell and direction on the device;
-                                  records unchanged, in the caller's order); 0 = the caller's order */
 } och_option;
 OCH_API int och_gpu_set_option(och_gpu_pool *pool, int option, int value);
 OCH_API int och_gpu_get_option(const och_gpu_pool *pool, int option, int *value);

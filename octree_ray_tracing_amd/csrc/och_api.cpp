@@ -159,9 +159,6 @@ struct och_gpu_pool {
     int opt_merge = 0;
     int opt_timing = 1;                        // OCH_OPT_TIMING
     int opt_plan = 10;                         // OCH_OPT_PLAN (shape of och_gpu_plan_views' order)
-    int opt_sort = 0;                          // OCH_OPT_SORT
-    void *d_sort = nullptr;                    // och::sort_rays scratch (keys, indices, radix-sort temp)
-    size_t sort_bytes = 0;
     hipEvent_t next_ev_start = nullptr;        // och_gpu_set_launch_events: the next launch's events
     hipEvent_t next_ev_stop = nullptr;
     // bounding box of the pool's voxels (voxel units, [lo, hi)), for the cull
@@ -625,7 +622,6 @@ OCH_API int och_gpu_pool_destroy(och_gpu_pool *p)
     if (p->d_counter) (void)hipFree(p->d_counter);
     if (p->d_chunk_map) (void)hipFree(p->d_chunk_map);
     if (p->d_owner) (void)hipFree(p->d_owner);
-    if (p->d_sort) (void)hipFree(p->d_sort);
     if (p->ev_start) (void)hipEventDestroy(p->ev_start);
     if (p->ev_stop) (void)hipEventDestroy(p->ev_stop);
     if (p->own_stream) (void)hipStreamDestroy(p->own_stream);
@@ -919,10 +915,6 @@ OCH_API int och_gpu_set_option(och_gpu_pool *p, int option, int value)
         if (value < 0 || value > 100) return fail(OCH_E_INVALID, "plan shape must be 0..100");
         p->opt_plan = value;
         return OCH_OK;
-    case OCH_OPT_SORT:
-        if (value != 0 && value != 1) return fail(OCH_E_INVALID, "sort must be 0 or 1");
-        p->opt_sort = value;
-        return OCH_OK;
     default:
         return fail(OCH_E_INVALID, "unknown option %d", option);
     }
@@ -944,7 +936,6 @@ OCH_API int och_gpu_get_option(const och_gpu_pool *p, int option, int *value)
     case OCH_OPT_MERGE: *value = p->opt_merge; return OCH_OK;
     case OCH_OPT_TIMING: *value = p->opt_timing; return OCH_OK;
     case OCH_OPT_PLAN: *value = p->opt_plan; return OCH_OK;
-    case OCH_OPT_SORT: *value = p->opt_sort; return OCH_OK;
     default: return fail(OCH_E_INVALID, "unknown option %d", option);
     }
 }
@@ -1007,34 +998,6 @@ int timed_done(och_gpu_pool *p, const och::Schedule &sc, bool launched)
 
 }  // namespace
 
-namespace {
-
-// OCH_OPT_SORT: batches of at least this many rays are walked in coherence
-// order (och::sort_rays); smaller ones in the caller's order.
-constexpr uint32_t kSortMin = 16384;
-
-int batch_order(och_gpu_pool *p, const float *origin, int origin_stride, const float *dirs, uint32_t n,
-                const uint32_t **perm)
-{
-    *perm = nullptr;
-    if (!p->opt_sort || n < kSortMin) return OCH_OK;
-    const size_t need = och::sort_rays_bytes(n);
-    if (p->sort_bytes < need) {
-        if (p->d_sort) {
-            OCH_HIP(hipStreamSynchronize(p->stream()));     // an earlier sort may still read it
-            OCH_HIP(hipFree(p->d_sort));
-        }
-        p->d_sort = nullptr;
-        p->sort_bytes = 0;
-        if (hipMalloc(&p->d_sort, need) != hipSuccess) return fail(OCH_E_NOMEM, "sort scratch (%zu bytes)", need);
-        p->sort_bytes = need;
-    }
-    OCH_HIP(och::sort_rays(origin, origin_stride, dirs, n, p->d_sort, p->sort_bytes, perm, p->stream()));
-    return OCH_OK;
-}
-
-}  // namespace
-
 OCH_API int och_gpu_set_launch_events(och_gpu_pool *p, void *start_event, void *stop_event)
 {
     if (!p) return fail(OCH_E_INVALID, "pool is NULL");
@@ -1072,13 +1035,11 @@ OCH_API int och_gpu_trace_batch_dev(och_gpu_pool *p, const float *origin, int or
     if (origin_stride != 0 && origin_stride != 3) return fail(OCH_E_INVALID, "origin_stride must be 0 or 3");
     if (int rs = check_ready(p)) return rs;
     DeviceGuard g(p->device);
-    const uint32_t *perm = nullptr;
-    if (int so = batch_order(p, origin, origin_stride, dirs, n, &perm)) return so;
     int ts;
     const och::Schedule sc = timed_schedule(p, ts);
     if (ts) return ts;
     OCH_HIP(och::launch_trace_batch(p->dev(), origin, origin_stride, dirs, n, hit_dir, hit_voxel,
-                                    reinterpret_cast<uint32_t *>(hit_time), push_count, sc, p->stream(), perm));
+                                    reinterpret_cast<uint32_t *>(hit_time), push_count, sc, p->stream()));
     return timed_done(p, sc, n > 0);
 }
 
@@ -1093,15 +1054,12 @@ OCH_API int och_gpu_trace_bounce_batch_dev(och_gpu_pool *p, const float *origin,
     if (origin_stride != 0 && origin_stride != 3) return fail(OCH_E_INVALID, "origin_stride must be 0 or 3");
     if (int rs = check_ready(p)) return rs;
     DeviceGuard g(p->device);
-    const uint32_t *perm = nullptr;
-    if (int so = batch_order(p, origin, origin_stride, dirs, n, &perm)) return so;
     int ts;
     const och::Schedule sc = timed_schedule(p, ts);
     if (ts) return ts;
     OCH_HIP(och::launch_trace_bounce_batch(p->dev(), origin, origin_stride, dirs, n, hit_dir, hit_voxel,
                                            reinterpret_cast<uint32_t *>(hit_time), bounce_dir, bounce_voxel,
-                                           reinterpret_cast<uint32_t *>(bounce_time), push_count, sc, p->stream(),
-                                           perm));
+                                           reinterpret_cast<uint32_t *>(bounce_time), push_count, sc, p->stream()));
     return timed_done(p, sc, n > 0);
 }
 

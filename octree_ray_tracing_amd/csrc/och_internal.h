@@ -137,18 +137,9 @@ struct Schedule {
     hipEvent_t ev_stop;
 };
 
-// perm (optional): walk ray perm[i] as the i-th ray (sort_rays); records in the caller's order.
 hipError_t launch_trace_batch(const DevPool &p, const float *origin, int origin_stride, const float *dirs,
                               uint32_t n, int32_t *hit_dir, uint32_t *hit_voxel, uint32_t *hit_time,
-                              uint32_t *push_count, const Schedule &sc, hipStream_t stream,
-                              const uint32_t *perm = nullptr);
-// Coherence order of a ray batch (och_sort.hip): perm = the ray indices sorted
-// by a 32-bit key (shared origin: octahedral direction, 16 + 16 bits in Morton
-// order; per-ray origins: 7-bit-per-axis origin cell in Morton order, then 11
-// bits of direction).  scratch: sort_rays_bytes(n) bytes; perm points into it.
-size_t sort_rays_bytes(uint32_t n);
-hipError_t sort_rays(const float *origin, int origin_stride, const float *dirs, uint32_t n, void *scratch,
-                     size_t scratch_bytes, const uint32_t **perm, hipStream_t stream);
+                              uint32_t *push_count, const Schedule &sc, hipStream_t stream);
 // The same rays as a row-major image `width` rays wide, one 8x8 tile per
 // wave (TiledArraySource); records in the caller's order.
 hipError_t launch_trace_batch_tiled(const DevPool &p, const float *origin, int origin_stride, const float *dirs,
@@ -163,8 +154,7 @@ hipError_t occupancy_blocks_per_cu(int kind, int block, int depth, int *blocks);
 hipError_t launch_trace_bounce_batch(const DevPool &p, const float *origin, int origin_stride, const float *dirs,
                                      uint32_t n, int32_t *hit_dir, uint32_t *hit_voxel, uint32_t *hit_time,
                                      int32_t *bounce_dir, uint32_t *bounce_voxel, uint32_t *bounce_time,
-                                     uint32_t *push_count, const Schedule &sc, hipStream_t stream,
-                                     const uint32_t *perm = nullptr);
+                                     uint32_t *push_count, const Schedule &sc, hipStream_t stream);
 hipError_t launch_render_bounce(const DevPool &p, const DevFrame &f, const Schedule &sc, hipStream_t stream);
 hipError_t launch_raygen(const och_camera &cam, float *dirs, hipStream_t stream);
 hipError_t launch_render(const DevPool &p, const DevFrame &f, const Schedule &sc, hipStream_t stream);

@@ -627,19 +627,14 @@ __device__ __forceinline__ void bounce_ray(const float *o, const float *d, const
 // ---------------------------------------------------------------- sources
 
 // Rays from arrays: shared (stride 0) or per-ray (stride 3) origin, AoS float3 dirs.
-// perm (optional, och_sort.hip): the i-th ray walked is ray perm[i] of the
-// arrays, and its record goes to perm[i] -- rays sorted by origin and
-// direction walk as coherent waves, records stay in the caller's order.
 struct ArraySource {
     const float *origin;
     const float *dirs;
     int origin_stride;
     uint32_t n;
-    const uint32_t *perm;
     __device__ __forceinline__ uint32_t count() const { return n; }
     __device__ __forceinline__ bool get(uint32_t i, float *o, float *d, uint32_t &out) const
     {
-        if (perm) i = perm[i];
         const float *po = origin + (size_t)origin_stride * i;
         const float *pd = dirs + 3 * (size_t)i;
         o[0] = po[0]; o[1] = po[1]; o[2] = po[2];
@@ -1732,9 +1727,9 @@ hipError_t occupancy_blocks_per_cu(int kind, int block, int depth, int *blocks)
 
 hipError_t launch_trace_batch(const DevPool &p, const float *origin, int origin_stride, const float *dirs,
                               uint32_t n, int32_t *hit_dir, uint32_t *hit_voxel, uint32_t *hit_time,
-                              uint32_t *push_count, const Schedule &sc, hipStream_t stream, const uint32_t *perm)
+                              uint32_t *push_count, const Schedule &sc, hipStream_t stream)
 {
-    const ArraySource src{origin, dirs, origin_stride, n, perm};
+    const ArraySource src{origin, dirs, origin_stride, n};
     if (push_count)
         return launch<ArraySource, HitSink<true>, true>(p, src, HitSink<true>{hit_dir, hit_voxel, hit_time, push_count},
                                                         n, sc, stream);
@@ -1816,10 +1811,9 @@ hipError_t launch_shade_unshard(const uint8_t *gathered, uint32_t *frames, const
 hipError_t launch_trace_bounce_batch(const DevPool &p, const float *origin, int origin_stride, const float *dirs,
                                      uint32_t n, int32_t *hit_dir, uint32_t *hit_voxel, uint32_t *hit_time,
                                      int32_t *bounce_dir, uint32_t *bounce_voxel, uint32_t *bounce_time,
-                                     uint32_t *push_count, const Schedule &sc, hipStream_t stream,
-                                     const uint32_t *perm)
+                                     uint32_t *push_count, const Schedule &sc, hipStream_t stream)
 {
-    const ArraySource src{origin, dirs, origin_stride, n, perm};
+    const ArraySource src{origin, dirs, origin_stride, n};
     if (push_count)
         return launch_bounce<ArraySource, BounceHitSink<true>, true>(
             p, src, BounceHitSink<true>{HitSink<true>{hit_dir, hit_voxel, hit_time, push_count}, bounce_dir, bounce_voxel,
