@@ -44,6 +44,7 @@ import math
 import os
 import statistics
 import sys
+import threading
 import time
 from pathlib import Path
 
@@ -428,6 +429,8 @@ def main():
                     help="yaw change per step of the moving-camera window (radians; 0.004 = 14 deg/s at 60 fps)")
     ap.add_argument("--no-fast-issue", action="store_true",
                     help="diagnostic: issue N = 1 steps through the Python wrappers and torch stream contexts")
+    ap.add_argument("--isolate-main", action="store_true",
+                    help="diagnostic, with --pin-core: move the process's other threads off the issuing CPU")
     ap.add_argument("--pin-core", action="store_true",
                     help="diagnostic: pin the issuing (main) thread to one of its allowed CPUs")
     ap.add_argument("--host-rehearse", action="store_true",
@@ -718,7 +721,16 @@ def main():
             f_.exchange()
 
     if a.pin_core:
-        os.sched_setaffinity(0, {sorted(os.sched_getaffinity(0))[0]})
+        cpus = sorted(os.sched_getaffinity(0))
+        main_tid = threading.get_native_id()
+        os.sched_setaffinity(0, {cpus[0]})
+        if a.isolate_main and len(cpus) > 1:   # every other thread of the process off the issuing CPU
+            for tid in os.listdir("/proc/self/task"):
+                if int(tid) != main_tid:
+                    try:
+                        os.sched_setaffinity(int(tid), set(cpus[1:]))
+                    except OSError:
+                        pass
     stamps = {}                            # --host-stamps
     trace_parts = False
     in_window = False
