@@ -1076,7 +1076,8 @@ def main():
                                     f"row chunks dealt by {a.deal} (och_deal_chunks), rank 0 weight "
                                     f"{a.display_weight if a.shade == 'display' else 1.0}; chunks per rank "
                                     f"{np.bincount(deal, minlength=world).tolist()}"),
-                       "shade": ("every rank all-gathers the frame's codes; " +
+                       "shade": ("the render launch shades each pixel (trace_pixel) into the RGBA8 frames" if direct
+                                 else "every rank all-gathers the frame's codes; " +
                                  ("rank 0 (the display) shades them to RGBA8" if a.shade == "display" and world > 1
                                   else "every rank shades them to RGBA8")),
                        "frames": ("rgba8 frames written by the fused launch (no exchange at N = 1)" if direct else
