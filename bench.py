@@ -115,6 +115,21 @@ def torch_event():
     return torch.cuda.Event(enable_timing=True)
 
 
+def pipeline_defaults(world: int, inflight=None, hw_queues=None):
+    """Frames in flight and GPU_MAX_HW_QUEUES for a world size (DESIGN.md §5,
+    tools/proxy_rank.py sweeps): 3 frames on the environment's queues below
+    N = 8, 6 frames on 8 queues from N = 8.  Explicit values win."""
+    if inflight is None:
+        inflight = 6 if world >= 8 else 3
+    if hw_queues is None and world >= 8:
+        hw_queues = 8
+    if inflight < 1:
+        raise SystemExit("--inflight must be >= 1")
+    if hw_queues is not None and not 1 <= hw_queues <= 32:
+        raise SystemExit("--hw-queues must be in 1..32")
+    return inflight, hw_queues
+
+
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
@@ -470,14 +485,8 @@ def main():
     # frames must overlap -- 6 frames on 8 hardware queues: job 192 -> 211 G rays/s
     # over 20 steps, 215 -> 242 G sustained; at N = 1, 2, 4 the default 3 on 4
     # queues is best.
-    world_env = int(os.environ.get("WORLD_SIZE", "1"))
-    if a.inflight is None:
-        a.inflight = 6 if world_env >= 8 else 3
-    if a.hw_queues is None and world_env >= 8:
-        a.hw_queues = 8
+    a.inflight, a.hw_queues = pipeline_defaults(int(os.environ.get("WORLD_SIZE", "1")), a.inflight, a.hw_queues)
     if a.hw_queues is not None:
-        if not 1 <= a.hw_queues <= 32:
-            raise SystemExit("--hw-queues must be in 1..32")
         os.environ["GPU_MAX_HW_QUEUES"] = str(a.hw_queues)
 
     import torch
