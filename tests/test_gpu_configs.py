@@ -202,3 +202,49 @@ def test_d12_trace_records_all_schedules(ort, O, gpu_device, d12, d12_ref):
             pool.set_option("layout", layout)
             assert_same(gpu_trace_dev(pool, ORIGIN, rays), ref)
     pool.close()
+
+
+def test_random_cameras_d12(ort, O, gpu_device, d12, d12_ref, pal):
+    """The render path at depth 12 from cameras other than the bench's: random
+    positions in the root (some under the terrain's surface, inside solid
+    voxels or tunnels), one on a voxel boundary, random yaw / pitch, three
+    fields of view; two cameras per launch (each view its own position), in
+    natural and planned order, cull and camera shortcut on -- every pixel the
+    oracle's trace + trace_pixel shading."""
+    import torch
+    rng = np.random.default_rng(12)
+    W, H = 480, 270
+    specs = []
+    for k in range(10):
+        pos = tuple(float(x) for x in rng.uniform(1.02, 1.98, 3))
+        if k == 0:
+            pos = (1.5, 1.5, 1.0 + 1000.0 / 4096.0)            # on a voxel boundary, inside the terrain's box
+        if k == 1:
+            pos = (1.31, 1.77, 1.12)                           # deep under the surface
+        specs.append((pos, float(rng.uniform(-np.pi, np.pi)), float(rng.uniform(-1.2, 1.2)),
+                      float((0.9, 1.25, 1.6)[k % 3])))
+    want = []
+    for pos, yaw, pitch, fov in specs:
+        r = O.trace_batch(d12_ref, O.Rcp(None), np.array(pos, np.float32), O.raygen(yaw, pitch, fov, W, H),
+                          nthreads=16)
+        want.append(O.shade_fast(r["dir"], r["voxel"], pal).reshape(H, W))
+    pool = ort.HOctree(d12.nodes, d12.root, 12, device=0)
+    pool.set_palette(pal)
+    pool.set_stream(torch.cuda.current_stream())
+    inside = 0
+    for order in (0, 2):
+        pool.set_option("tile_order", order)
+        for i in range(0, len(specs), 2):
+            cams = [ort.camera(*[specs[j][0], specs[j][1], specs[j][2], specs[j][3], W, H]) for j in (i, i + 1)]
+            if order == 2:
+                pool.plan_views(cams, H, 0, 1)
+            frames = torch.zeros((2, H, W), dtype=torch.int32, device="cuda")
+            pool.render_views_dev(cams, frames)
+            torch.cuda.synchronize()
+            got = frames.cpu().numpy().view(np.uint32)
+            for v, j in enumerate((i, i + 1)):
+                assert np.array_equal(got[v], want[j]), (order, j, int((got[v] != want[j]).sum()))
+    for w in want:
+        inside += int((w == w[0, 0]).all())
+    assert inside < len(want)                                  # not every view is one colour
+    pool.close()
