@@ -584,3 +584,46 @@ def test_planned_launch_order(ort, O, gpu_device, order, shape):
         want = O.shade_bounce(r["dir"], r["voxel"], r["dir2"], pal).reshape(H, W)
         assert np.array_equal(full[v].cpu().numpy().view(np.uint32), want), ("bounce", v)
     pool.close()
+
+
+def test_eight_views_per_launch(ort, O, gpu_device):
+    """OCH_MAX_VIEWS cameras of one size in one launch, each with its own
+    position, yaw, pitch and fov: RGBA8 frames and colour codes (sharded over
+    3 ranks, shaded after) equal the oracle's per view; a ninth view, or views
+    of different sizes, are refused."""
+    import torch
+    tree = ort.build_terrain(9)
+    pal = ort.VoxelData().get_colours()
+    pool = ort.HOctree(tree.nodes, tree.root, 9, device=0)
+    pool.set_palette(pal)
+    pool.set_stream(torch.cuda.current_stream())
+    ref_pool = O.OraclePool(tree.nodes, tree.root, 9, 1)
+    rng = np.random.default_rng(8)
+    W, H = 333, 187
+    specs = [(tuple(float(x) for x in rng.uniform(1.05, 1.95, 3)), float(rng.uniform(-3, 3)),
+              float(rng.uniform(-1.2, 1.2)), float((0.9, 1.25, 1.6)[k % 3])) for k in range(8)]
+    cams = [ort.camera(pos, yaw, pitch, fov, W, H) for pos, yaw, pitch, fov in specs]
+    want = []
+    for pos, yaw, pitch, fov in specs:
+        r = O.trace_batch(ref_pool, O.Rcp(None), np.array(pos, np.float32), O.raygen(yaw, pitch, fov, W, H),
+                          nthreads=16)
+        want.append(O.shade(r["dir"], r["voxel"], pal).reshape(H, W))
+    frames = torch.zeros((8, H, W), dtype=torch.int32, device="cuda")
+    pool.render_views_dev(cams, frames)
+    n, rc = 3, 8
+    rows = ort.shard_rows(H, rc, n)
+    gathered = torch.full((n, 8, rows, W), 255, dtype=torch.uint8, device="cuda")
+    for s_ in range(n):
+        pool.render_codes_views_dev(cams, gathered[s_], rc, s_, n)
+    full = torch.empty((8, H, W), dtype=torch.int32, device="cuda")
+    pool.shade_unshard_dev(gathered, full, W, H, rc, n, 8)
+    torch.cuda.synchronize()
+    for v in range(8):
+        assert np.array_equal(frames[v].cpu().numpy().view(np.uint32), want[v]), v
+        assert np.array_equal(full[v].cpu().numpy().view(np.uint32), want[v]), v
+    nine = torch.zeros((9, H, W), dtype=torch.int32, device="cuda")
+    with pytest.raises(ort.OchError):
+        pool.render_views_dev(cams + cams[:1], nine)
+    with pytest.raises(ort.OchError):
+        pool.render_views_dev([cams[0], ort.camera((1.5, 1.5, 1.5), 0.3, 0.0, 1.25, W + 1, H)], frames)
+    pool.close()
