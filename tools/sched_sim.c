@@ -94,6 +94,10 @@ static int step_one(Ray *r)
 }
 
 static int SCHED = 0;
+/* schedule 0: iterations in which some lane's PUSH loads a slot word at a node of
+ * level <= DEPTH - 2 (the loads left if the bottom two levels' occupancy rode in
+ * registers), and loads per node level */
+static double IT_LOAD_ABOVE2 = 0, LOADS_AT[40];
 static int THRESH = 0;   /* schedule 0: skip a phase needed by fewer than THRESH lanes (at most one iteration) */
 
 /* schedule 0: the current kernel (step, descend, push; each phase skipped when no lane needs it) */
@@ -106,7 +110,7 @@ static void wave_sched0(Ray *R, int n, Stats *S)
         for (int i = 0; i < n; ++i) any |= active(&R[i]);
         if (!any) break;
         S->iters += 1;
-        int ns = 0, nadv = 0, npopper = 0, npop = 0, nd = 0, ndesc = 0, np = 0, nload = 0;
+        int nload_above2 = 0; int ns = 0, nadv = 0, npopper = 0, npop = 0, nd = 0, ndesc = 0, np = 0, nload = 0;
         int want_step = 0, want_desc = 0;
         for (int i = 0; i < n; ++i) { want_step += active(&R[i]) && R[i].stepping; want_desc += R[i].pending; }
         const int run_step = want_step >= THRESH || skipped_step;
@@ -157,6 +161,7 @@ static void wave_sched0(Ray *R, int n, Stats *S)
             Ray *r = &R[i];
             if (r->stepping || r->pending || !active(r)) continue;
             ++np; push(r); nload += r->pending;
+            if (r->pending) { LOADS_AT[r->level] += 1; nload_above2 += r->level <= DEPTH - 2; }
             fresh[i] = r->stepping;
         }
         if (SCHED == 1) {     /* second STEP + PUSH test in the same iteration for lanes whose PUSH failed */
@@ -184,6 +189,7 @@ static void wave_sched0(Ray *R, int n, Stats *S)
         if (ndesc) { S->valu += C_DESC; S->exec_descbody += 1; }
         if (np) { S->valu += C_PUSHTEST; S->exec_push += 1; S->lane_push += np; }
         if (nload) { S->valu += C_PUSHLOAD; S->exec_load += 1; }
+        if (nload_above2) IT_LOAD_ABOVE2 += 1;
     }
     for (int i = 0; i < n; ++i) S->rays_it += R[i].iters;
     S->waves += 1;
@@ -432,5 +438,10 @@ int main(int argc, char **argv)
            S.lane_step / S.exec_step / 64, S.lane_desc / S.exec_desc / 64, S.lane_push / S.exec_push / 64,
            S.exec_step / S.iters, S.exec_desc / S.iters, S.exec_adv / S.iters, S.exec_popper / S.iters,
            S.exec_load / S.iters);
+    if (SCHED == 0) {
+        fprintf(stderr, "load_frac_above_bottom2 %.3f\nloads per node level:", IT_LOAD_ABOVE2 / S.iters);
+        for (int l = 1; l <= DEPTH; ++l) fprintf(stderr, " %.0f", LOADS_AT[l]);
+        fprintf(stderr, "\n");
+    }
     return 0;
 }
