@@ -1137,6 +1137,8 @@ OCH_API int och_gpu_plan_batch_tiled(och_gpu_pool *p, const float *origin, int o
     std::vector<uint32_t> order(max_blocks);
     for (uint32_t i = 0; i < max_blocks; ++i) order[i] = i;
     std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return c[a] > c[b]; });
+    p->plan_key[2][0] = -1;                   // no plan until the new one is in place (a failure below leaves none)
+    if (int ds = och::pool_drain(p)) return ds;   // launches in flight on other streams may read the old order
     if (p->order_blocks[2] < max_blocks) {
         for (uint32_t **o : {&p->d_order[2], &p->d_order_xcd[2]}) {
             if (*o) OCH_HIP(hipFree(*o));
@@ -1405,6 +1407,8 @@ OCH_API int och_gpu_plan_views(och_gpu_pool *p, const och_camera *cams, int n_vi
                         if (lists[y].size() - at[y] > lists[from].size() - at[from]) from = y;
                 grouped.push_back(lists[from][at[from]++]);
             }
+        p->plan_key[which][0] = -1;           // no plan until the new one is in place (a failure below leaves none)
+        if (int ds = och::pool_drain(p)) return ds;   // launches in flight on other streams may read the old order
         if (p->order_blocks[which] < n_blocks) {
             for (uint32_t **o : {&p->d_order[which], &p->d_order_xcd[which]}) {
                 if (*o) OCH_HIP(hipFree(*o));
