@@ -1,4 +1,4 @@
-"""Row-chunk sharding and the framebuffer all-gather (world size 2, gloo, CPU)."""
+"""Row-chunk sharding and the framebuffer all-gather (world sizes 2 and 8, gloo, CPU)."""
 import os
 
 import numpy as np
@@ -135,6 +135,32 @@ def test_gloo_world2_dealt_exchange(ort):
     for p in procs:
         p.start()
     got = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    want = np.arange(H)[:, None] * 1000 + np.arange(W)[None, :]
+    for r in range(world):
+        assert np.array_equal(got[r], want)
+
+
+def test_gloo_world8_bench_deal_exchange(ort):
+    """The deal the driver's 8-GPU run uses (configs[3]: 2160 rows in 8-row
+    chunks, dealt by count with the display rank at 1 - 0.05 * 8 = 0.6, as
+    bench.py does), broadcast from rank 0 and exchanged by 8 gloo ranks: the
+    padded slices all-gather into the whole frame on every rank."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    H, W, chunk, world = 2160, 4, 8, 8
+    n_chunks = -(-H // chunk)
+    deal = ort.deal_chunks(np.ones(n_chunks, np.float32), world, [1.0 - 0.05 * world] + [1.0] * (world - 1))
+    counts = np.bincount(deal, minlength=world)
+    assert counts[0] < counts[1:].min()                           # the display rank renders fewer rows
+    assert counts.sum() == n_chunks and counts[1:].max() - counts[1:].min() <= 1
+    port = 31700 + os.getpid() % 1000
+    procs = [ctx.Process(target=_deal_worker, args=(r, world, port, H, W, chunk, deal, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=180) for _ in range(world))
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
