@@ -442,6 +442,10 @@ def main():
                          "launch order planned once from the first step's cameras (and in natural order); 0 = off")
     ap.add_argument("--moving-dyaw", type=float, default=0.004,
                     help="yaw change per step of the moving-camera window (radians; 0.004 = 14 deg/s at 60 fps)")
+    ap.add_argument("--issue", choices=("native", "python"), default="native",
+                    help="N = 1 timed windows: 'native' = one och_gpu_render_steps_dev call issues the window's "
+                         "frames from the library's own loop (as a C++ host's frame loop would); 'python' = one "
+                         "prepared C-ABI render call per step from this interpreter")
     ap.add_argument("--no-fast-issue", action="store_true",
                     help="diagnostic: issue N = 1 steps through the Python wrappers and torch stream contexts")
     ap.add_argument("--isolate-main", action="store_true",
@@ -679,6 +683,34 @@ def main():
         fast = {"lib": lib, "cams": cam_arr, "h": h, "direct": direct,
                 "args": [[(h, ctypes.c_void_p(s_.cuda_stream)), ra] for s_, ra in zip(streams, args)]}
 
+    def prepare_native(n, bounce, ev):
+        """N = 1, direct frames: the window's n frames as ONE library call
+        (och_gpu_render_steps_dev) that issues frame k on stream k % inflight into
+        that stream's frames, its dispatch recording event pair k -- the same
+        launches, streams, buffers and events as n step_fast calls, without the
+        interpreter between them.  Arguments are built here, before the window."""
+        lib = fast["lib"]
+        B = len(streams)
+        sp = (ctypes.c_void_p * B)(*[s_.cuda_stream for s_ in streams])
+        fp = (ctypes.c_void_p * B)(*[f_.frames.data_ptr() for f_ in sfs])
+        e0 = e1 = None
+        pairs = []
+        if ev is not None:
+            pairs = [ev_pool[(len(ev) + k) % len(ev_pool)] for k in range(n)]
+            e0 = (ctypes.c_void_p * n)(*[x.h.value for x, _ in pairs])
+            e1 = (ctypes.c_void_p * n)(*[y.h.value for _, y in pairs])
+        args = (fast["h"], fast["cams"], len(cams), n, sp, fp, B, e0, e1, a.row_chunk, int(bool(bounce)))
+        fn = lib.och_gpu_render_steps_dev
+
+        def issue():
+            if fn(*args):
+                raise RuntimeError(f"render steps: {lib.och_last_error().decode()}")
+            if ev is not None:
+                ev.extend(pairs)
+        return issue
+
+    native_issue = fast is not None and fast["direct"] and a.issue == "native" and a.step_events == "dispatch"
+
     def step_fast(k, ev, bounce):
         lib, (sa, ra) = fast["lib"], fast["args"][k % len(streams)]
         st = lib.och_gpu_set_stream(*sa)
@@ -782,6 +814,7 @@ def main():
         if world > 1:
             dist.barrier()
         drain()
+        issue = prepare_native(n, bounce, ev) if native_issue and not (marked and a.host_stamps) else None
         gc_was = gc.isenabled()
         gc.disable()                       # no collector pause inside the timed region (as timeit)
         if marked and a.host_stamps:
@@ -789,7 +822,9 @@ def main():
         t0 = time.perf_counter()
         nonlocal trace_parts, in_window
         trace_parts = marked and a.host_stamps
-        if marked and a.host_stamps:
+        if issue is not None:
+            issue()                        # the n frames, issued by the library's own loop
+        elif marked and a.host_stamps:
             issued = stamps.setdefault("issued", [])
             for k in range(n):
                 step(k, ev, bounce)
@@ -1080,6 +1115,9 @@ def main():
                        "parallelism": f"rows{world}",
                        "frames_in_flight": len(streams),
                        "hw_queues": int(os.environ.get("GPU_MAX_HW_QUEUES", "4")),
+                       "issue": ("one och_gpu_render_steps_dev call per timed window (the library issues each "
+                                 "step's launch)" if native_issue else "one C-ABI render call per step"
+                                 if fast is not None else "Python wrappers per step"),
                        "row_deal": (None if world == 1 else
                                     "round-robin 8-row chunks" if deal is None else
                                     f"row chunks dealt by {a.deal} (och_deal_chunks), rank 0 weight "

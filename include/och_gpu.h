@@ -293,6 +293,19 @@ OCH_API int och_gpu_plan_views(och_gpu_pool *pool, const och_camera *cams, int n
  * halved (RGB >> 1, alpha kept) when the secondary ray is blocked. */
 OCH_API int och_gpu_render_bounce_views_dev(och_gpu_pool *pool, const och_camera *cams, int n_views,
                                             uint32_t *rgba_slices, int row_chunk, int shard, int n_shards);
+/* The frame loop (update_image once per frame, ORT/test_och_h_octree.cpp:
+ * 437-457) issued natively: n_steps whole frames of the same cameras
+ * (och_gpu_render_views_dev, or _bounce_views_dev with bounce = 1; one shard),
+ * frame k on streams[k % n_buffers] into frames[k % n_buffers] (each
+ * n_views * H * W RGBA8 words), so up to n_buffers frames are in flight and a
+ * frame reuses a buffer only behind the previous frame on that stream.  With
+ * start_events / stop_events (n_steps hipEvent_t each, or both NULL) the
+ * dispatch of frame k records start_events[k] and stop_events[k].
+ * Asynchronous; the pool's stream is left as it was. */
+OCH_API int och_gpu_render_steps_dev(och_gpu_pool *pool, const och_camera *cams, int n_views, int n_steps,
+                                     void *const *streams, uint32_t *const *frames, int n_buffers,
+                                     void *const *start_events, void *const *stop_events, int row_chunk,
+                                     int bounce);
 /* Row deal: instead of round-robin, row chunk g of frames `height` rows tall
  * (chunks of row_chunk rows over n_shards) belongs to shard chunk_shard[g],
  * for ceil(height / row_chunk) chunks; each shard's chunks keep their order.

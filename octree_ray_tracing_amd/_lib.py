@@ -94,6 +94,7 @@ PROTOTYPES = {
     "och_gpu_render_views_dev": (C.c_int, [_P, _P, C.c_int, _P, C.c_int, C.c_int, C.c_int]),
     "och_gpu_plan_views": (C.c_int, [_P, _P, C.c_int, C.c_int, C.c_int, C.c_int]),
     "och_gpu_render_bounce_views_dev": (C.c_int, [_P, _P, C.c_int, _P, C.c_int, C.c_int, C.c_int]),
+    "och_gpu_render_steps_dev": (C.c_int, [_P, _P, C.c_int, C.c_int, _P, _P, C.c_int, _P, _P, C.c_int, C.c_int]),
     "och_gpu_set_row_deal": (C.c_int, [_P, C.c_int, C.c_int, C.c_int, _P]),
     "och_gpu_slice_rows": (C.c_int, [_P, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_int)]),
     "och_gpu_chunk_costs": (C.c_int, [_P, _P, C.c_int, C.c_int, _P]),

@@ -1583,6 +1583,38 @@ OCH_API int och_gpu_render_bounce_views_dev(och_gpu_pool *p, const och_camera *c
     return render_views(p, cams, n_views, rgba_slices, row_chunk, shard, n_shards, true);
 }
 
+OCH_API int och_gpu_render_steps_dev(och_gpu_pool *p, const och_camera *cams, int n_views, int n_steps,
+                                     void *const *streams, uint32_t *const *frames, int n_buffers,
+                                     void *const *start_events, void *const *stop_events, int row_chunk, int bounce)
+{
+    if (!p || !cams || !streams || !frames) return fail(OCH_E_INVALID, "NULL argument");
+    if (n_steps < 0 || n_buffers < 1) return fail(OCH_E_INVALID, "n_steps %d / n_buffers %d", n_steps, n_buffers);
+    if ((start_events == nullptr) != (stop_events == nullptr))
+        return fail(OCH_E_INVALID, "start_events and stop_events: both or neither");
+    for (int b = 0; b < n_buffers; ++b)
+        if (!frames[b]) return fail(OCH_E_INVALID, "frames[%d] is NULL", b);
+    // The frame loop of update_image (ORT/test_och_h_octree.cpp:437-457), one
+    // launch per frame, issued here rather than by the caller's interpreter.
+    // The pool's stream is restored afterwards, also after a failure.
+    const bool had_ext = p->use_ext;
+    const hipStream_t prev = p->ext_stream;
+    int st = OCH_OK;
+    for (int k = 0; k < n_steps && st == OCH_OK; ++k) {
+        const int b = k % n_buffers;
+        p->ext_stream = static_cast<hipStream_t>(streams[b]);
+        p->use_ext = true;
+        if (start_events) {
+            p->next_ev_start = static_cast<hipEvent_t>(start_events[k]);
+            p->next_ev_stop = static_cast<hipEvent_t>(stop_events[k]);
+        }
+        st = render_views(p, cams, n_views, frames[b], row_chunk, 0, 1, bounce != 0);
+    }
+    p->next_ev_start = p->next_ev_stop = nullptr;
+    p->ext_stream = prev;
+    p->use_ext = had_ext;
+    return st;
+}
+
 OCH_API int och_gpu_render_codes_views_dev(och_gpu_pool *p, const och_camera *cams, int n_views, uint8_t *code_slices,
                                            int row_chunk, int shard, int n_shards, int bounce)
 {

@@ -39,6 +39,14 @@ def _np_ptr(a: np.ndarray) -> int:
     return a.ctypes.data
 
 
+def _event_handle(e):
+    """A hipEvent_t as an int: a raw handle, a ctypes c_void_p, or an object with ``h``."""
+    if e is None:
+        return None
+    h = getattr(e, "h", e)
+    return h.value if hasattr(h, "value") else int(h)
+
+
 def _dev_ptr(t) -> int:
     """Device pointer of a torch tensor (or an int already)."""
     if isinstance(t, int):
@@ -194,12 +202,7 @@ class GpuPool:
     def set_launch_events(self, start, stop):
         """The next trace/render launch records these HIP events (raw hipEvent_t
         handles, or objects with an ``h`` handle) through its own dispatch."""
-        def handle(e):
-            if e is None:
-                return None
-            h = getattr(e, "h", e)
-            return h.value if hasattr(h, "value") else int(h)
-        call("och_gpu_set_launch_events", self._h, handle(start), handle(stop))
+        call("och_gpu_set_launch_events", self._h, _event_handle(start), _event_handle(stop))
 
     # -- tracing (reference signature)
     def sse_trace(self, ox, oy, oz, dx, dy, dz):
@@ -280,6 +283,28 @@ class GpuPool:
             row_chunk = cams[0].height
         call("och_gpu_render_views_dev", self._h, C.cast(arr, C.c_void_p), len(cams), _dev_ptr(rgba_slices),
              int(row_chunk), int(shard), int(n_shards))
+
+    def render_steps_dev(self, cams, frames, streams, n_steps: int, events=None, row_chunk: int | None = None,
+                         bounce: bool = False):
+        """n_steps whole frames of these cameras issued by the library's own loop
+        (och_gpu_render_steps_dev): frame k on streams[k % B] into frames[k % B],
+        B = len(frames) = len(streams); events = n_steps (start, stop) pairs of HIP
+        events (raw handles or objects with ``h``) recorded by each frame's dispatch."""
+        if len(frames) != len(streams) or not frames:
+            raise ValueError("one stream per frame buffer")
+        arr = (Camera * len(cams))(*cams)
+        if row_chunk is None:
+            row_chunk = cams[0].height
+        sp = (C.c_void_p * len(streams))(*[getattr(s_, "cuda_stream", s_) for s_ in streams])
+        fp = (C.c_void_p * len(frames))(*[_dev_ptr(f) for f in frames])
+        e0 = e1 = None
+        if events is not None:
+            if len(events) != n_steps:
+                raise ValueError("one event pair per step")
+            e0 = (C.c_void_p * n_steps)(*[_event_handle(a) for a, _ in events])
+            e1 = (C.c_void_p * n_steps)(*[_event_handle(b) for _, b in events])
+        call("och_gpu_render_steps_dev", self._h, C.cast(arr, C.c_void_p), len(cams), int(n_steps), sp, fp,
+             len(frames), e0, e1, int(row_chunk), int(bool(bounce)))
 
     def plan_views(self, cams, row_chunk: int | None = None, shard: int = 0, n_shards: int = 1):
         """Plan the launch order of frames of this geometry (och_gpu_plan_views); used with

@@ -55,3 +55,54 @@ def test_timing_modes_and_launch_events(ort, O, gpu_device):
     with pytest.raises(ort.OchError):
         pool.set_option("timing", 3)
     pool.close()
+
+
+def test_render_steps_native_loop(ort, O, gpu_device):
+    """och_gpu_render_steps_dev: the frame loop issued by the library -- frame k
+    on stream k % B into buffer k % B, its dispatch recording event pair k --
+    gives the oracle's frames in every buffer, primary and config 5, and leaves
+    the pool's stream as it was."""
+    import torch
+    from bench import FenceFreeEvent
+    tree = ort.build_terrain(8)
+    pal = ort.VoxelData().get_colours()
+    pool = ort.HOctree(tree.nodes, tree.root, 8, device=0)
+    pool.set_palette(pal)
+    cur = torch.cuda.current_stream()
+    pool.set_stream(cur)
+    W, H = 320, 180
+    cams = [ort.camera((1.5, 1.5, 1.5), 0.3, p, 1.25, W, H) for p in (0.0, -0.6)]
+    r = [O.trace_batch(O.OraclePool(tree.nodes, tree.root, 8, 1), O.Rcp(None), np.array([1.5, 1.5, 1.5], np.float32),
+                       O.raygen(0.3, p, 1.25, W, H)) for p in (0.0, -0.6)]
+    want = np.stack([O.shade(x["dir"], x["voxel"], pal).reshape(H, W) for x in r])
+    streams = [cur] + [torch.cuda.Stream() for _ in range(2)]
+    for n_steps in (7, 1, 0):
+        frames = [torch.zeros((2, H, W), dtype=torch.int32, device="cuda") for _ in streams]
+        events = [(FenceFreeEvent(), FenceFreeEvent()) for _ in range(n_steps)]
+        pool.render_steps_dev(cams, frames, streams, n_steps, events)
+        torch.cuda.synchronize()
+        for b, f in enumerate(frames):
+            got = f.cpu().numpy().view(np.uint32)
+            if b < n_steps:
+                assert np.array_equal(got, want), (n_steps, b)
+            else:
+                assert not got.any()                           # no frame went to this buffer
+        assert all(0.0 < x.elapsed_time(y) < 1000.0 for x, y in events)
+    # without events; config 5 through the same loop equals the single-launch render
+    frames = [torch.zeros((2, H, W), dtype=torch.int32, device="cuda") for _ in streams]
+    pool.render_steps_dev(cams, frames, streams, 4, bounce=True)
+    one = torch.zeros((2, H, W), dtype=torch.int32, device="cuda")
+    pool.render_bounce_views_dev(cams, one)
+    torch.cuda.synchronize()
+    for f in frames:
+        assert torch.equal(f, one)
+    # the pool's own stream is untouched: a plain launch after the loop runs on it
+    pool.set_option("timing", 1)
+    pool.render_views_dev(cams, one)
+    cur.synchronize()
+    assert np.array_equal(one.cpu().numpy().view(np.uint32), want)
+    with pytest.raises(ValueError):
+        pool.render_steps_dev(cams, frames[:2], streams, 3)
+    with pytest.raises(ValueError):
+        pool.render_steps_dev(cams, frames, streams, 3, [(FenceFreeEvent(), FenceFreeEvent())])
+    pool.close()
