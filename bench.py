@@ -478,6 +478,15 @@ def main():
     ap.add_argument("--inflight", type=int, default=None,
                     help="frames in flight: steps alternate over this many HIP streams, so one step's "
                          "slowest rays overlap the next step's bulk (1 = serialised); default 3, 6 at N >= 8")
+    ap.add_argument("--sharded", action="store_true",
+                    help="N = 1: the N > 1 step at world size 1 -- render colour codes, exchange them over RCCL "
+                         "(--exchange) and shade -- instead of the fused launch writing RGBA8 frames")
+    ap.add_argument("--exchange", choices=("rccl", "gather", "torch"), default="rccl",
+                    help="sharded steps (N > 1, or --sharded): 'rccl' = all-gather on the library's own RCCL "
+                         "communicator (och_comm_*, its id broadcast by torch.distributed), the window issued by "
+                         "one och_gpu_render_sharded_steps_dev call per rank; 'gather' = the same, but only rank 0 "
+                         "(the display) receives the slices; 'torch' = dist.all_gather_into_tensor per step from "
+                         "Python.  The gloo rehearsal backend always exchanges through torch")
     ap.add_argument("--hw-queues", type=int, default=None,
                     help="GPU_MAX_HW_QUEUES for this process (set before HIP starts); default the "
                          "environment's (4 on the box), 8 at N >= 8")
@@ -508,15 +517,17 @@ def main():
         log(f"warning: --gpus {a.gpus} but WORLD_SIZE {world}; using WORLD_SIZE")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    if world > 1:
+    sharded = world > 1 or a.sharded
+    if world > 1 or (a.sharded and a.exchange == "torch"):
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29517")
         if backend == "gloo":
-            dist.init_process_group("gloo")
+            dist.init_process_group("gloo", rank=rank, world_size=world)
         else:
-            dist.init_process_group("nccl", device_id=dev)
+            dist.init_process_group("nccl", device_id=dev, rank=rank, world_size=world)
 
     import octree_ray_tracing_amd as ort
-    from octree_ray_tracing_amd.frame import ShardedFrame, slice_row_map
+    from octree_ray_tracing_amd.frame import RcclComm, ShardedFrame, ShardedSteps, slice_row_map
 
     W, H = frame_size(world, a.width, a.height, a.scaling)
     nodes, root, tree_nodes, build_s = build_pool_nodes(a.depth, rank, world, dev)
@@ -530,7 +541,16 @@ def main():
     # Frames travel between ranks as 1-byte colour codes and are shaded after
     # the gather (same RGBA8 frames, a quarter of the bytes on xGMI).
     indexed = not a.rgba_frames and ort.VoxelData().get_colours().size // 6 <= pool.CODE_MAX_VOXELS
-    direct = world == 1 and not a.no_direct
+    direct = world == 1 and not a.no_direct and not a.sharded
+    # The library's own RCCL communicator for the exchange (N > 1 over nccl, or
+    # --sharded): rank 0's id broadcast by torch.distributed, ncclCommInitRank
+    # on every rank.  The gloo rehearsal (several ranks per GPU) keeps torch's.
+    comm = None
+    if sharded and indexed and backend == "nccl" and a.exchange in ("rccl", "gather"):
+        comm = RcclComm.from_process_group() if dist.is_initialized() else RcclComm.local(local)
+    exch_mode = "gather" if (comm is not None and a.exchange == "gather") else "all_gather"
+    if exch_mode == "gather" and a.shade != "display":
+        raise SystemExit("--exchange gather needs --shade display")
     cams = [ort.camera(ORIGIN, YAW, p, FOV, W, H) for p in PITCHES]
     # N > 1: which rank renders which row chunks.  Rank 0 times one render of
     # the whole frame per chunk and deals the chunks longest first onto the
@@ -559,7 +579,7 @@ def main():
     for s_ in streams:
         with torch.cuda.stream(s_):
             sfs.append(ShardedFrame(pool, W, H, a.row_chunk, n_views=len(PITCHES), indexed=indexed, shade=a.shade,
-                                    direct=direct, deal=deal))
+                                    direct=direct, deal=deal, comm=comm, sharded=sharded, exchange=exch_mode))
     pool.set_stream(stream)
     # Launch order: one planning render of these views times every tile, and
     # the costliest tiles go first (och_gpu_plan_views; dispatch order only,
@@ -670,7 +690,7 @@ def main():
     # N > 1 (colour codes): the render is issued the same way; the all-gather and
     # the display rank's shade stay in ShardedFrame.exchange, on the frame's stream.
     fast = None
-    if (direct or (indexed and world > 1)) and not a.no_fast_issue:
+    if (direct or (indexed and sharded)) and not a.no_fast_issue:
         from octree_ray_tracing_amd._lib import Camera, load as load_lib
         lib = load_lib()
         cam_arr = (Camera * len(cams))(*cams)
@@ -710,6 +730,26 @@ def main():
         return issue
 
     native_issue = fast is not None and fast["direct"] and a.issue == "native" and a.step_events == "dispatch"
+    # Sharded steps (N > 1, or --sharded) on the library's communicator: the
+    # window's frames -- render codes, exchange, display-rank shade, per
+    # frame on stream k % inflight -- issued by ONE och_gpu_render_sharded_steps_dev
+    # call per rank, as prepare_native does at N = 1.
+    sharded_steps = None
+    if comm is not None and a.issue == "native" and a.step_events == "dispatch" and not a.no_fast_issue:
+        sharded_steps = {b: ShardedSteps(sfs, streams, comm, cams, bounce=b) for b in (False, True)}
+        native_issue = True
+
+    def prepare_sharded(n, bounce, ev):
+        pairs = [ev_pool[(len(ev) + k) % len(ev_pool)] for k in range(n)] if ev is not None else []
+        issue_ = sharded_steps[bool(bounce)].prepare(
+            n, [x.h.value for x, _ in pairs] if ev is not None else None,
+            [y.h.value for _, y in pairs] if ev is not None else None)
+
+        def issue():
+            issue_()
+            if ev is not None:
+                ev.extend(pairs)
+        return issue
 
     def step_fast(k, ev, bounce):
         lib, (sa, ra) = fast["lib"], fast["args"][k % len(streams)]
@@ -814,7 +854,9 @@ def main():
         if world > 1:
             dist.barrier()
         drain()
-        issue = prepare_native(n, bounce, ev) if native_issue and not (marked and a.host_stamps) else None
+        issue = None
+        if native_issue and not (marked and a.host_stamps):
+            issue = prepare_sharded(n, bounce, ev) if sharded_steps is not None else prepare_native(n, bounce, ev)
         gc_was = gc.isenabled()
         gc.disable()                       # no collector pause inside the timed region (as timeit)
         if marked and a.host_stamps:
@@ -1029,19 +1071,36 @@ def main():
     # canonical algorithmic bytes, 24 B in + 12 B out + 4 B per PUSH per ray.
     step_s = elapsed / a.steps
     k_avg_ms = float(kms.mean()) if kms.size else latency_ms    # --no-step-events: the lone launch instead
-    canon_bytes = 36 * rays_rank + 4 * walk_push
+    # SURVEY §8(d)'s canonical count takes the reference's PUSHes of every ray
+    # (the walk without the cull); the walked figure counts what the timed,
+    # culled launch walks (proven misses read nothing).  Both per launch.
+    canon_bytes = 36 * rays_rank + 4 * push_total
+    walked_bytes = 36 * rays_rank + 4 * walk_push
+
+    def gbs(nbytes, ms):
+        return round(nbytes / (ms * 1e-3) / 1e9, 2) if ms else None
+
     hbm = {"bound": "hbm", "bytes_per_launch": int(canon_bytes),
-           "bytes_model": "SURVEY 8(d) canonical: 24 B ray in + 12 B hit record out per ray + 4 B per PUSH the "
-                          "launch walks (rays the occupied-box cull proves to miss walk none)",
-           "achieved": round(canon_bytes / (k_avg_ms * 1e-3) / 1e9, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+           "bytes_model": "SURVEY 8(d) canonical: 24 B ray in + 12 B hit record out per ray + 4 B per PUSH of the "
+                          "reference's walk (push_per_ray: every ray walks, as sse_trace does)",
+           "achieved": gbs(canon_bytes, k_avg_ms), "peak": HBM_PEAK_GBS, "unit": "GB/s",
            "frac": round(canon_bytes / (k_avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 5),
-           "achieved_per_step": round(canon_bytes / step_s / 1e9, 2),
-           "frac_per_step": round(canon_bytes / step_s / 1e9 / HBM_PEAK_GBS, 5)}
+           "achieved_per_step": gbs(canon_bytes, step_s * 1e3),
+           "frac_per_step": round(canon_bytes / step_s / 1e9 / HBM_PEAK_GBS, 5),
+           "walked_bytes_per_launch": int(walked_bytes),
+           "walked_bytes_model": "the same with the PUSHes the timed launch walks (walked_push_per_ray: rays the "
+                                 "occupied-box cull proves to miss walk none)",
+           "walked_achieved": gbs(walked_bytes, k_avg_ms),
+           "walked_frac_per_step": round(walked_bytes / step_s / 1e9 / HBM_PEAK_GBS, 5),
+           "note": "achieved / frac: per launch, over the launch's mean duration in the timed window (HIP events "
+                   "recorded by its dispatch; three frames overlap, so a launch lasts longer than a step); "
+                   "*_per_step: over the pipelined step time"}
     rgba_launch = direct or not indexed
     pmc, pmc_src = load_pmc("k_render_rgba" if rgba_launch else "k_render", f"d{a.depth}_{W}x{H}_n{world}")
     roof = {"kernel": f"k_trace_grid<CameraSource,{'FrameSink' if rgba_launch else 'CodeSink'}> (2 views per launch)",
             "kernel_ms": round(k_avg_ms, 4), "kernel_ms_serial": round(latency_ms, 4),
             "host_issue_ms": host_issue_ms,
+            "host_issue_ms_per_step": round(host_issue_ms / max(a.steps, 1), 5),
             "ms_per_step": round(step_s * 1e3, 4), "frames_in_flight": len(streams),
             "push_per_ray": round(push_total / rays_rank, 3), "rays_per_launch": rays_rank,
             "walked_push_per_ray": round(walk_push / rays_rank, 3), "culled_frac": round(culled / rays_rank, 4),
@@ -1052,20 +1111,31 @@ def main():
     if pmc and "SQ_INSTS_VALU" in pmc:
         insts = float(pmc["SQ_INSTS_VALU"])
         ach = insts / step_s / 1e9
-        prof_ms = float(pmc.get("mean_ms") or 0.0)
+        # the PMC passes' own launch duration: rocprofv3 serialises the
+        # dispatches of a counter pass, so this is one launch alone
+        prof_ms = float(pmc.get("pmc_mean_ms") or 0.0)
+        if prof_ms:
+            hbm["achieved_pmc_launch"] = gbs(canon_bytes, prof_ms)
+            hbm["frac_pmc_launch"] = round(canon_bytes / (prof_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 5)
+            hbm["walked_frac_pmc_launch"] = round(walked_bytes / (prof_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 5)
         roof.update({"bound": "valu-issue", "achieved": round(ach, 1), "peak": VALU_PEAK_GINST_S,
                      "unit": "G VALU wave-instructions/s", "frac": round(ach / VALU_PEAK_GINST_S, 4),
                      "valu_insts_per_launch": int(insts), "valu_insts_per_wave": pmc.get("valu_insts_per_wave"),
                      "valu_lane_utilization": pmc.get("valu_lane_utilization"),
                      "achieved_per_launch": round(insts / (k_avg_ms * 1e-3) / 1e9, 1),
-                     # per launch, from the profile alone: SQ_INSTS_VALU / that profile's mean launch duration
+                     # per launch, from the profile alone: SQ_INSTS_VALU / the PMC passes' mean (serialised)
+                     # launch duration, both in profiles/pmc_summary.json
                      "frac_profile": round(insts / (prof_ms * 1e-3) / 1e9 / VALU_PEAK_GINST_S, 4) if prof_ms else None,
                      "profile_mean_ms": prof_ms or None,
+                     "profile_mean_ms_basis": "pmc_mean_ms: the PMC passes' mean launch duration (dispatches "
+                                              "serialised by the profiler)",
+                     "frac_serial_launch": round(insts / (latency_ms * 1e-3) / 1e9 / VALU_PEAK_GINST_S, 4),
                      "effective_clock_ghz": pmc.get("effective_clock_ghz"),
                      "note": "frac = issue rate over the pipelined step (three frames overlap, so a launch lasts "
                              "longer than a step: window_profile shows the overlap); frac_profile = the same "
-                             "instructions over one launch's mean duration under the profiler; the DAG is "
-                             "L2/MALL-resident, so HBM is far from binding (see hbm)"})
+                             "instructions over one serialised launch under the profiler (pmc_mean_ms); "
+                             "frac_serial_launch = over kernel_ms_serial, one launch on an idle GPU timed here; "
+                             "the DAG is L2/MALL-resident, so HBM is far from binding (see hbm)"})
     else:
         roof.update({k: hbm[k] for k in ("bound", "achieved", "peak", "unit", "frac")})
 
@@ -1086,7 +1156,8 @@ def main():
 
     if rank == 0:
         if world == 1:
-            workload = "configs[2]: 4096^3 depth-12 och_h_octree DAG, 1920x1080 primary rays, 1 MI355X"
+            workload = "configs[2]: 4096^3 depth-12 och_h_octree DAG, 1920x1080 primary rays, 1 MI355X" + (
+                " (the sharded N > 1 step at world size 1: codes, RCCL exchange, shade)" if sharded else "")
         elif a.scaling == "strong" and (W, H) == (3840, 2160):
             workload = (f"configs[3]: 4096^3 depth-12, 3840x2160 primary rays tiled across {world} MI355X "
                         "with RCCL framebuffer all-gather")
@@ -1115,9 +1186,16 @@ def main():
                        "parallelism": f"rows{world}",
                        "frames_in_flight": len(streams),
                        "hw_queues": int(os.environ.get("GPU_MAX_HW_QUEUES", "4")),
-                       "issue": ("one och_gpu_render_steps_dev call per timed window (the library issues each "
+                       "issue": ("one och_gpu_render_sharded_steps_dev call per timed window and rank (the "
+                                 "library issues each step's render, RCCL exchange and shade)" if sharded_steps
+                                 else "one och_gpu_render_steps_dev call per timed window (the library issues each "
                                  "step's launch)" if native_issue else "one C-ABI render call per step"
                                  if fast is not None else "Python wrappers per step"),
+                       "exchange": (None if not sharded else
+                                    f"RCCL {'gather to rank 0 (ncclSend/ncclRecv)' if exch_mode == 'gather' else 'all-gather'} "
+                                    "on the library's communicator (och_comm_*)" if comm is not None else
+                                    "torch.distributed all_gather_into_tensor" if backend == "nccl" else
+                                    "torch.distributed gloo all_gather through the host (rehearsal)"),
                        "row_deal": (None if world == 1 else
                                     "round-robin 8-row chunks" if deal is None else
                                     f"row chunks dealt by {a.deal} (och_deal_chunks), rank 0 weight "
@@ -1148,8 +1226,11 @@ def main():
             "other_configs": others,
         }
         print(json.dumps(line), flush=True)
+    if comm is not None:
+        torch.cuda.synchronize()
+        comm.close()
     pool.close()
-    if world > 1:
+    if dist.is_initialized():
         dist.destroy_process_group()
 
 

@@ -383,6 +383,57 @@ OCH_API int och_frame_group_frames_dev(och_frame_group *group, int rank, uint32_
 /* Copy device `rank`'s frames to a host buffer of n_views*H*W words (synchronous). */
 OCH_API int och_frame_group_download(och_frame_group *group, int rank, uint32_t *rgba);
 OCH_API int och_frame_group_synchronize(och_frame_group *group);
+/* n_steps frames of the same cameras issued natively: frame k renders,
+ * exchanges and shades into buffer set k % n_buffers of every device, on
+ * that set's stream, so up to n_buffers frames are in flight (n_buffers
+ * 1..8).  Asynchronous.  och_frame_group_frames_dev / _download then give
+ * buffer set (n_steps - 1) % n_buffers: the last frame. */
+OCH_API int och_frame_group_render_steps(och_frame_group *group, const och_camera *cams, int n_views, int n_steps,
+                                         int n_buffers, int row_chunk, int bounce);
+
+/* ------------------------------------------------------------ multi-GPU frames, one process per GPU */
+/* SURVEY §8(e) with one process per GPU (the driver's torch.distributed
+ * launch, MPI, ...): the library's own RCCL communicator over the ranks.
+ * Rank 0 calls och_comm_unique_id; the caller hands the OCH_COMM_ID_BYTES
+ * bytes to every rank by its own means (torch.distributed broadcast, MPI_Bcast,
+ * a file); every rank then calls och_comm_create with its device (collective:
+ * returns once all ranks joined).  RCCL is loaded on first use, as for the
+ * frame group; OCH_E_NODEV when it cannot be. */
+#define OCH_COMM_ID_BYTES 128
+typedef struct och_comm och_comm;
+OCH_API int och_comm_unique_id(uint8_t *id);
+OCH_API int och_comm_create(const uint8_t *id, int n_ranks, int rank, int device, och_comm **out);
+OCH_API int och_comm_destroy(och_comm *comm);
+OCH_API int och_comm_info(const och_comm *comm, int *n_ranks, int *rank, int *device);
+/* recv = [n_ranks][bytes]: every rank's `bytes` (ncclAllGather), enqueued on stream. */
+OCH_API int och_comm_all_gather(och_comm *comm, const void *send, void *recv, size_t bytes, void *stream);
+/* Only rank `root` receives recv = [n_ranks][bytes]; the others send (recv may be NULL there). */
+OCH_API int och_comm_gather(och_comm *comm, const void *send, void *recv, size_t bytes, int root, void *stream);
+
+/* Exchange of a sharded frame (och_gpu_render_sharded_steps_dev). */
+enum {
+    OCH_EXCHANGE_ALL_GATHER = 0,   /* every rank receives every slice (ncclAllGather), every rank shades */
+    OCH_EXCHANGE_DISPLAY = 1,      /* every rank receives every slice, only rank 0 (the display) shades */
+    OCH_EXCHANGE_GATHER = 2        /* only rank 0 receives the slices (ncclSend / ncclRecv) and shades */
+};
+/* The sharded frame loop of update_image (ORT/test_och_h_octree.cpp:437-457)
+ * on one rank, issued natively: n_steps frames of the same cameras, frame k on
+ * streams[k % n_buffers]:
+ *   1. this rank's row chunks of the n_views cameras as colour codes
+ *      (och_gpu_render_codes_views_dev, shard = the comm's rank, n_shards = its
+ *      size) into slices[b]: [n_views][rows][W] bytes, rows = och_gpu_slice_rows;
+ *   2. the exchange into gathered[b]: [n_ranks][n_views][rows][W] bytes;
+ *   3. where this rank shades (`exchange` above): shade + unshard into frames[b],
+ *      [n_views][H][W] RGBA8 -- the frames och_gpu_render_views_dev writes.
+ * gathered / frames may be NULL (or hold NULL entries) on ranks that do not
+ * receive / shade.  start_events / stop_events (n_steps each, or both NULL):
+ * recorded by frame k's render dispatch.  Every rank must issue the same
+ * n_steps.  Asynchronous; the pool's stream is left as it was. */
+OCH_API int och_gpu_render_sharded_steps_dev(och_gpu_pool *pool, och_comm *comm, const och_camera *cams, int n_views,
+                                             int n_steps, void *const *streams, uint8_t *const *slices,
+                                             uint8_t *const *gathered, uint32_t *const *frames, int n_buffers,
+                                             void *const *start_events, void *const *stop_events, int row_chunk,
+                                             int bounce, int exchange);
 
 /* ------------------------------------------------------------ builder */
 /* The demo terrain (ORT/test_och_h_octree.cpp:561-787) built in parallel

@@ -126,7 +126,20 @@ PROTOTYPES = {
     "och_frame_group_frames_dev": (C.c_int, [_P, C.c_int, C.POINTER(_P)]),
     "och_frame_group_download": (C.c_int, [_P, C.c_int, _P]),
     "och_frame_group_synchronize": (C.c_int, [_P]),
+    "och_frame_group_render_steps": (C.c_int, [_P, _P, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int]),
+    "och_comm_unique_id": (C.c_int, [_P]),
+    "och_comm_create": (C.c_int, [_P, C.c_int, C.c_int, C.c_int, C.POINTER(_P)]),
+    "och_comm_destroy": (C.c_int, [_P]),
+    "och_comm_info": (C.c_int, [_P, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int)]),
+    "och_comm_all_gather": (C.c_int, [_P, _P, _P, C.c_size_t, _P]),
+    "och_comm_gather": (C.c_int, [_P, _P, _P, C.c_size_t, C.c_int, _P]),
+    "och_gpu_render_sharded_steps_dev": (C.c_int, [_P, _P, _P, C.c_int, C.c_int, _P, _P, _P, _P, C.c_int, _P, _P,
+                                                   C.c_int, C.c_int, C.c_int]),
 }
+
+# och_gpu_render_sharded_steps_dev's exchange (include/och_gpu.h OCH_EXCHANGE_*)
+EXCHANGE = {"all_gather": 0, "display": 1, "gather": 2}
+COMM_ID_BYTES = 128
 
 # Functions whose int return value is data, not a status.
 _NOT_STATUS = {"och_abi_version", "och_shard_rows"}

@@ -1436,38 +1436,54 @@ OCH_API int och_gpu_set_row_deal(och_gpu_pool *p, int height, int row_chunk, int
     if (chunk_shard && p->deal_for(height, row_chunk, n_shards) && row_chunk > 0 &&
         std::equal(p->deal_table.begin(), p->deal_table.end(), chunk_shard))
         return OCH_OK;                                                  // this deal already (plans stay valid)
+    // Validate the new deal and build its tables on the host first: a bad
+    // call leaves the pool's current deal in place.
+    std::vector<int32_t> map, owner;
+    int n_chunks = 0, max_chunks = 1;
+    if (chunk_shard) {
+        if (height <= 0 || row_chunk <= 0 || n_shards <= 0 || n_shards > 32767)
+            return fail(OCH_E_INVALID, "bad row deal geometry (%d, %d, %d)", height, row_chunk, n_shards);
+        n_chunks = (height + row_chunk - 1) / row_chunk;
+        std::vector<std::vector<int32_t>> mine(n_shards);
+        for (int c = 0; c < n_chunks; ++c) {
+            if (chunk_shard[c] < 0 || chunk_shard[c] >= n_shards)
+                return fail(OCH_E_INVALID, "chunk %d dealt to shard %d of %d", c, chunk_shard[c], n_shards);
+            mine[chunk_shard[c]].push_back(c);
+        }
+        for (const auto &m : mine) max_chunks = std::max(max_chunks, (int)m.size());
+        if (max_chunks > 65535) return fail(OCH_E_INVALID, "more than 65535 chunks for one shard");
+        map.assign((size_t)n_shards * max_chunks, -1);
+        owner.assign(n_chunks, 0);
+        for (int sh = 0; sh < n_shards; ++sh)
+            for (size_t l = 0; l < mine[sh].size(); ++l) {
+                map[(size_t)sh * max_chunks + l] = mine[sh][l];
+                owner[mine[sh][l]] = (sh << 16) | (int32_t)l;
+            }
+    }
     DeviceGuard g(p->device);
+    int32_t *d_map = nullptr, *d_own = nullptr;
+    if (chunk_shard) {
+        hipError_t e = hipMalloc(&d_map, map.size() * 4);
+        if (e == hipSuccess) e = hipMalloc(&d_own, owner.size() * 4);
+        if (e == hipSuccess) e = hipMemcpy(d_map, map.data(), map.size() * 4, hipMemcpyHostToDevice);
+        if (e == hipSuccess) e = hipMemcpy(d_own, owner.data(), owner.size() * 4, hipMemcpyHostToDevice);
+        if (e != hipSuccess) {
+            if (d_map) (void)hipFree(d_map);
+            if (d_own) (void)hipFree(d_own);
+            return fail(OCH_E_HIP, "row deal tables: %s", hipGetErrorString(e));
+        }
+    }
     OCH_HIP(hipDeviceSynchronize());          // frames in flight may still read the old tables
     if (p->d_chunk_map) OCH_HIP(hipFree(p->d_chunk_map));
     if (p->d_owner) OCH_HIP(hipFree(p->d_owner));
-    p->d_chunk_map = nullptr;
-    p->d_owner = nullptr;
-    p->deal_n = p->deal_h = p->deal_chunk = p->deal_max = 0;
-    p->deal_table.clear();
+    p->d_chunk_map = d_map;
+    p->d_owner = d_own;
     ++p->deal_serial;
-    if (!chunk_shard) return OCH_OK;           // back to round-robin
-    if (height <= 0 || row_chunk <= 0 || n_shards <= 0 || n_shards > 32767)
-        return fail(OCH_E_INVALID, "bad row deal geometry (%d, %d, %d)", height, row_chunk, n_shards);
-    const int n_chunks = (height + row_chunk - 1) / row_chunk;
-    std::vector<std::vector<int32_t>> mine(n_shards);
-    for (int c = 0; c < n_chunks; ++c) {
-        if (chunk_shard[c] < 0 || chunk_shard[c] >= n_shards)
-            return fail(OCH_E_INVALID, "chunk %d dealt to shard %d of %d", c, chunk_shard[c], n_shards);
-        mine[chunk_shard[c]].push_back(c);
+    if (!chunk_shard) {                        // back to round-robin
+        p->deal_n = p->deal_h = p->deal_chunk = p->deal_max = 0;
+        p->deal_table.clear();
+        return OCH_OK;
     }
-    int max_chunks = 1;
-    for (const auto &m : mine) max_chunks = std::max(max_chunks, (int)m.size());
-    if (max_chunks > 65535) return fail(OCH_E_INVALID, "more than 65535 chunks for one shard");
-    std::vector<int32_t> map((size_t)n_shards * max_chunks, -1), owner(n_chunks);
-    for (int sh = 0; sh < n_shards; ++sh)
-        for (size_t l = 0; l < mine[sh].size(); ++l) {
-            map[(size_t)sh * max_chunks + l] = mine[sh][l];
-            owner[mine[sh][l]] = (sh << 16) | (int32_t)l;
-        }
-    OCH_HIP(hipMalloc(&p->d_chunk_map, map.size() * 4));
-    OCH_HIP(hipMalloc(&p->d_owner, owner.size() * 4));
-    OCH_HIP(hipMemcpy(p->d_chunk_map, map.data(), map.size() * 4, hipMemcpyHostToDevice));
-    OCH_HIP(hipMemcpy(p->d_owner, owner.data(), owner.size() * 4, hipMemcpyHostToDevice));
     p->deal_h = height;
     p->deal_chunk = row_chunk;
     p->deal_n = n_shards;
@@ -1495,7 +1511,9 @@ OCH_API int och_gpu_chunk_costs(och_gpu_pool *p, const och_camera *cams, int n_v
     // one whole-frame render, natural 8x8-tile order, every workgroup timed
     const int W = cams[0].width, H = cams[0].height;
     const uint32_t tiles_x = (uint32_t)(W + 7) / 8, tiles_y = (uint32_t)(H + 7) / 8;
-    const uint32_t tiles = (uint32_t)n_views * tiles_x * tiles_y, per_block = (uint32_t)p->opt_block / 64;
+    // tiles per workgroup exactly as launch_as sizes the grid kernel's grid
+    const uint32_t tiles = (uint32_t)n_views * tiles_x * tiles_y,
+                   per_block = (uint32_t)p->opt_block / 64 * (och::kDualRays ? 2u : 1u);
     const uint32_t n_blocks = (tiles + per_block - 1) / per_block;
     const size_t frame_bytes = ((size_t)n_views * H * W * 4 + 255) & ~(size_t)255;
     int st = ensure_scratch(p, frame_bytes + (size_t)n_blocks * 4);
@@ -1513,14 +1531,22 @@ OCH_API int och_gpu_chunk_costs(och_gpu_pool *p, const och_camera *cams, int n_v
     f.n_shards = 1;
     f.slice_rows = H;
     f.chunk_map = nullptr;
+    // The plain grid kernel writes the costs (the merging kernel writes none,
+    // ADVICE r3): every launched workgroup overwrites its 0xFFFFFFFF, so a
+    // block the launch did not cover is caught below instead of being read as
+    // uninitialised scratch.
     och::Schedule sc = p->schedule();
     sc.kind = 0;
     sc.tile_order = 0;
     sc.cost = cost;
+    sc.merge_k = 0;
+    OCH_HIP(hipMemsetAsync(cost, 0xFF, (size_t)n_blocks * 4, p->stream()));
     OCH_HIP(och::launch_render(p->dev(), f, sc, p->stream()));
     std::vector<uint32_t> c(n_blocks);
     OCH_HIP(hipMemcpyAsync(c.data(), cost, (size_t)n_blocks * 4, hipMemcpyDeviceToHost, p->stream()));
     OCH_HIP(hipStreamSynchronize(p->stream()));
+    for (uint32_t b = 0; b < n_blocks; ++b)
+        if (c[b] == 0xFFFFFFFFu) return fail(OCH_E_INVALID, "chunk-cost render left workgroup %u untimed", b);
     // a workgroup's time spread over its tiles, a tile's over its 8 rows
     const int n_chunks = (H + row_chunk - 1) / row_chunk;
     std::vector<double> acc(n_chunks, 0.0);
@@ -1608,6 +1634,61 @@ OCH_API int och_gpu_render_steps_dev(och_gpu_pool *p, const och_camera *cams, in
             p->next_ev_stop = static_cast<hipEvent_t>(stop_events[k]);
         }
         st = render_views(p, cams, n_views, frames[b], row_chunk, 0, 1, bounce != 0);
+    }
+    p->next_ev_start = p->next_ev_stop = nullptr;
+    p->ext_stream = prev;
+    p->use_ext = had_ext;
+    return st;
+}
+
+OCH_API int och_gpu_render_sharded_steps_dev(och_gpu_pool *p, och_comm *comm, const och_camera *cams, int n_views,
+                                             int n_steps, void *const *streams, uint8_t *const *slices,
+                                             uint8_t *const *gathered, uint32_t *const *frames, int n_buffers,
+                                             void *const *start_events, void *const *stop_events, int row_chunk,
+                                             int bounce, int exchange)
+{
+    if (!p || !comm || !cams || !streams || !slices) return fail(OCH_E_INVALID, "NULL argument");
+    if (n_steps < 0 || n_buffers < 1) return fail(OCH_E_INVALID, "n_steps %d / n_buffers %d", n_steps, n_buffers);
+    if (n_views < 1 || n_views > OCH_MAX_VIEWS || row_chunk <= 0) return fail(OCH_E_INVALID, "bad views / row_chunk");
+    if (exchange < OCH_EXCHANGE_ALL_GATHER || exchange > OCH_EXCHANGE_GATHER)
+        return fail(OCH_E_INVALID, "unknown exchange %d", exchange);
+    if ((start_events == nullptr) != (stop_events == nullptr))
+        return fail(OCH_E_INVALID, "start_events and stop_events: both or neither");
+    int n_ranks = 0, rank = 0, device = -1;
+    if (int cs = och::comm_ranks(comm, &n_ranks, &rank, &device)) return cs;
+    if (device != p->device) return fail(OCH_E_INVALID, "communicator on device %d, pool on device %d", device, p->device);
+    const bool receives = exchange != OCH_EXCHANGE_GATHER || rank == 0;
+    const bool shades = exchange == OCH_EXCHANGE_ALL_GATHER || rank == 0;
+    for (int b = 0; b < n_buffers; ++b) {
+        if (!slices[b]) return fail(OCH_E_INVALID, "slices[%d] is NULL", b);
+        if (receives && (!gathered || !gathered[b])) return fail(OCH_E_INVALID, "rank %d needs gathered[%d]", rank, b);
+        if (shades && (!frames || !frames[b])) return fail(OCH_E_INVALID, "rank %d needs frames[%d]", rank, b);
+    }
+    const int W = cams[0].width, H = cams[0].height;
+    const size_t count = (size_t)n_views * p->slice_rows(H, row_chunk, n_ranks) * W;
+    DeviceGuard g(p->device);
+    // Per frame: render -> exchange -> shade, all on the frame's stream, so
+    // the three are ordered on the device and the host never waits.  A
+    // buffer set is reused only behind the previous frame on its stream.
+    const bool had_ext = p->use_ext;
+    const hipStream_t prev = p->ext_stream;
+    int st = OCH_OK;
+    for (int k = 0; k < n_steps && st == OCH_OK; ++k) {
+        const int b = k % n_buffers;
+        const hipStream_t s = static_cast<hipStream_t>(streams[b]);
+        p->ext_stream = s;
+        p->use_ext = true;
+        if (start_events) {
+            p->next_ev_start = static_cast<hipEvent_t>(start_events[k]);
+            p->next_ev_stop = static_cast<hipEvent_t>(stop_events[k]);
+        }
+        st = render_views(p, cams, n_views, nullptr, row_chunk, rank, n_ranks, bounce != 0, slices[b]);
+        if (st == OCH_OK)
+            st = exchange == OCH_EXCHANGE_GATHER
+                     ? och::comm_gather(comm, slices[b], receives ? gathered[b] : nullptr, count, 0, s)
+                     : och::comm_all_gather(comm, slices[b], gathered[b], count, s);
+        if (st == OCH_OK && shades)
+            st = och_gpu_shade_unshard_views_dev(p, gathered[b], frames[b], W, H, row_chunk, n_ranks, n_views);
     }
     p->next_ev_start = p->next_ev_stop = nullptr;
     p->ext_stream = prev;

@@ -100,6 +100,14 @@ void *pool_stream(const och_gpu_pool *pool);
 int pool_palette_size(const och_gpu_pool *pool, int *n_voxels);
 uint64_t pool_last_writer(const och_gpu_pool *pool);
 
+// The library's RCCL communicator (och_comm.cpp), for the sharded frame loop
+// in och_api.cpp.  comm_all_gather: recv = [n_ranks][bytes]; comm_gather:
+// only rank `root` receives (recv may be null elsewhere).  Both enqueue on
+// `stream`; the caller has the communicator's device current.
+int comm_ranks(const och_comm *comm, int *n_ranks, int *rank, int *device);
+int comm_all_gather(och_comm *comm, const void *send, void *recv, size_t bytes, hipStream_t stream);
+int comm_gather(och_comm *comm, const void *send, void *recv, size_t bytes, int root, hipStream_t stream);
+
 struct DevFrame {
     och_camera cams[OCH_MAX_VIEWS];   // equal width / height
     int32_t n_views;
@@ -110,6 +118,13 @@ struct DevFrame {
     int32_t row_chunk, shard, n_shards, slice_rows;
     const int32_t *chunk_map; // row deal: this shard's global chunk per local chunk (-1 = padding), or null
 };
+
+// OCH_DUAL builds: the grid kernel walks two rays per lane (two 8x8 tiles per
+// wave), so a workgroup covers twice the tiles (och_gpu_chunk_costs).
+#ifndef OCH_DUAL
+#define OCH_DUAL 0
+#endif
+constexpr bool kDualRays = OCH_DUAL != 0;
 
 // Threads per workgroup of the config-5 (bounce) kernels: compaction spans
 // the block's 4 waves.

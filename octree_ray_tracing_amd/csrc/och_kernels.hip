@@ -459,11 +459,21 @@ __device__ __forceinline__ void ray_descend(Ray &r, const DevPool &P, uint32_t s
 #endif
 // The grid and bounce kernels (one ray per lane, straight-line use of cur)
 // take it; the refill and persistent schedules keep the compiler's loads.
+// The build checks the compiler's output for what this relies on
+// (tools/isa_check.py, run by `make` and __graft_entry__.build()): in every
+// kernel that issues the load, the load and every wait name one register,
+// and on every path from a load to the next vmcnt(0) wait no instruction
+// reads that register before writing it (a read there would see the word
+// before the load lands -- a copy of cur at a join, a spill, a full-wave
+// select).  Writes there are the lane-disjoint temporaries of the STEP
+// phase described above.
 constexpr bool kAsmLoad = OCH_ASM_LOAD != 0;
 template <bool kAsm>
 __device__ __forceinline__ void wait_cur(Ray &r)
 {
-    if (kAsm) asm volatile("s_waitcnt vmcnt(0)" : "+v"(r.cur) : : "memory");
+    // the comment names cur's register in the compiler's assembly, for the
+    // build's ISA check (tools/isa_check.py)
+    if (kAsm) asm volatile("s_waitcnt vmcnt(0) ; och_cur_wait %0" : "+v"(r.cur) : : "memory");
 }
 
 template <bool kCount, bool kAsm>
@@ -489,7 +499,7 @@ __device__ __forceinline__ void ray_push_descend(Ray &r, const DevPool &P, uint3
     *r.sp = r.cur;                          // the parent, before its register takes the child's word
     r.sp += stride;
     if (OCH_LOAD_INTO_CUR && kAsm && !OCH_LDS_TOP)
-        asm volatile("global_load_dword %0, %1, %2 offset:-96"     // src = P.nodes - 96 B + off
+        asm volatile("global_load_dword %0, %1, %2 offset:-96 ; och_cur_load"   // src = P.nodes - 96 B + off
                      : "+v"(r.cur)
                      : "v"(off), "s"(P.nodes)
                      : "memory");
@@ -1305,7 +1315,7 @@ __global__ void k_trace_grid_merge(DevPool P, Src S, Sink K, int merge_k, const 
     }
 }
 
-// Config 5: primary rays, then wavefront compaction -- the block's hit// Config 5: primary rays, then wavefront compaction -- the block's hit
+// Config 5: primary rays, then wavefront compaction -- the block's hit
 // lanes (ballot + popcount per wave, wave offsets through LDS) write their
 // secondary rays into an LDS queue, and the first lanes of the block trace
 // them, so waves whose tiles mostly missed retire instead of idling beside

@@ -15,7 +15,7 @@ import math
 
 import numpy as np
 
-from ._lib import Camera, call
+from ._lib import COMM_ID_BYTES, EXCHANGE, Camera, call, load
 from .tracer import GpuPool, shard_rows
 
 
@@ -53,6 +53,83 @@ def unshard_host(gathered: np.ndarray, height: int, row_chunk: int, deal=None) -
     return frame
 
 
+class RcclComm:
+    """The library's own RCCL communicator (och_comm_*): one rank per process
+    and GPU, as the driver's torch.distributed launch runs them.  Rank 0 makes
+    the id, torch.distributed broadcasts it, every rank joins
+    (ncclCommInitRank).  The sharded frame loop (och_gpu_render_sharded_steps_dev)
+    exchanges its slices over it, so a frame's render, all-gather and shade
+    are issued by one library call with no interpreter between them."""
+
+    def __init__(self, uid: bytes, n_ranks: int, rank: int, device: int):
+        if len(uid) != COMM_ID_BYTES:
+            raise ValueError(f"an RCCL id has {COMM_ID_BYTES} bytes")
+        buf = (C.c_uint8 * COMM_ID_BYTES).from_buffer_copy(uid)
+        self._h = C.c_void_p()
+        call("och_comm_create", C.cast(buf, C.c_void_p), int(n_ranks), int(rank), int(device), C.byref(self._h))
+        self.n_ranks, self.rank, self.device = int(n_ranks), int(rank), int(device)
+
+    @staticmethod
+    def unique_id() -> bytes:
+        buf = (C.c_uint8 * COMM_ID_BYTES)()
+        call("och_comm_unique_id", C.cast(buf, C.c_void_p))
+        return bytes(buf)
+
+    @classmethod
+    def local(cls, device: int):
+        """A communicator of one rank (world size 1): the exchange is RCCL's
+        copy of the one slice."""
+        return cls(cls.unique_id(), 1, 0, device)
+
+    @classmethod
+    def from_process_group(cls, group=None, device: int | None = None):
+        """Every rank of `group` (default: the default group) calls this
+        together: rank 0's id goes to the others over torch.distributed."""
+        import torch
+        import torch.distributed as dist
+
+        rank, world = dist.get_rank(group), dist.get_world_size(group)
+        if device is None:
+            device = torch.cuda.current_device()
+        ids = torch.zeros(COMM_ID_BYTES, dtype=torch.uint8)
+        if rank == 0:
+            ids.copy_(torch.frombuffer(bytearray(cls.unique_id()), dtype=torch.uint8))
+        src = dist.get_global_rank(group, 0) if group is not None else 0
+        if dist.get_backend(group) == "gloo":
+            dist.broadcast(ids, src=src, group=group)
+        else:
+            dev_ids = ids.to(torch.device("cuda", device))
+            dist.broadcast(dev_ids, src=src, group=group)
+            ids = dev_ids.cpu()
+        return cls(bytes(ids.numpy().tobytes()), world, rank, device)
+
+    @property
+    def handle(self):
+        return self._h
+
+    def all_gather(self, send, recv, stream):
+        """recv = [n_ranks][send.numel() bytes], enqueued on `stream` (a torch stream)."""
+        call("och_comm_all_gather", self._h, C.c_void_p(send.data_ptr()), C.c_void_p(recv.data_ptr()),
+             send.numel() * send.element_size(), C.c_void_p(stream.cuda_stream))
+
+    def gather(self, send, recv, stream, root: int = 0):
+        """Only `root` receives recv = [n_ranks][bytes]; recv may be None elsewhere."""
+        call("och_comm_gather", self._h, C.c_void_p(send.data_ptr()),
+             C.c_void_p(recv.data_ptr() if recv is not None else 0), send.numel() * send.element_size(), int(root),
+             C.c_void_p(stream.cuda_stream))
+
+    def close(self):
+        if getattr(self, "_h", None) and self._h.value:
+            call("och_comm_destroy", self._h)
+            self._h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 class ShardedFrame:
     """Renders frames of one or more equal-size views across the ranks of the
     default process group.
@@ -62,11 +139,19 @@ class ShardedFrame:
     all-gather -> unshard are ordered without host synchronisation.  Views
     are rendered by one launch (och_gpu_render_views_dev), gathered by one
     collective and unsharded by one kernel.
+
+    comm: an RcclComm -- the exchange runs on the library's own communicator
+    instead of torch.distributed's (the path och_gpu_render_sharded_steps_dev
+    issues natively); sharded=True keeps the codes + exchange + shade path at
+    world size 1 (the exchange is then the collective's copy), so it runs on a
+    one-GPU box.  exchange="gather": only rank 0 (the display) receives the
+    slices (ncclSend / ncclRecv through comm); needs comm and shade="display".
     """
 
     def __init__(self, pool: GpuPool, width: int, height: int, row_chunk: int = 8, n_views: int = 1, group=None,
                  indexed: bool = False, shard: tuple[int, int] | None = None, shade: str = "all",
-                 direct: bool = False, deal=None, shade_stream=None):
+                 direct: bool = False, deal=None, shade_stream=None, comm: RcclComm | None = None,
+                 sharded: bool = False, exchange: str = "all_gather"):
         import torch
         import torch.distributed as dist
 
@@ -102,7 +187,16 @@ class ShardedFrame:
         # direct=True on a single rank: the fused launch writes the RGBA8 frames
         # themselves (update_image's framebuffer, ORT/test_och_h_octree.cpp:
         # 448-450) -- no slice, no exchange, no shade pass
-        self.direct = bool(direct) and self.world == 1 and not self.proxy
+        self.comm = comm
+        if comm is not None and (comm.n_ranks, comm.rank) != (self.world, self.rank):
+            raise ValueError(f"communicator rank {comm.rank} of {comm.n_ranks}, frame rank {self.rank} of {self.world}")
+        if exchange not in EXCHANGE:
+            raise ValueError(f"exchange must be one of {sorted(EXCHANGE)}")
+        if exchange == "gather" and (comm is None or shade != "display"):
+            raise ValueError("exchange='gather' needs an RcclComm and shade='display'")
+        self.exchange_mode = exchange
+        self.sharded = bool(sharded) or self.world > 1
+        self.direct = bool(direct) and self.world == 1 and not self.proxy and not self.sharded
         dev = torch.device("cuda", torch.cuda.current_device())
         dt = torch.uint8 if indexed else torch.int32
         self.slice = torch.empty((n_views, self.rows, width), dtype=dt, device=dev)
@@ -150,7 +244,14 @@ class ShardedFrame:
             # device (every slot gets this rank's slice; no xGMI time)
             self.gathered.copy_(self.slice.unsqueeze(0).expand_as(self.gathered))
             src = self.gathered
-        elif self.world > 1:
+        elif self.comm is not None:                         # the library's own RCCL communicator
+            cur = torch.cuda.current_stream()
+            if self.exchange_mode == "gather":
+                self.comm.gather(self.slice, self.gathered if self.rank == 0 else None, cur)
+            else:
+                self.comm.all_gather(self.slice, self.gathered, cur)
+            src = self.gathered
+        elif self.sharded and (self.world > 1 or dist.is_initialized()):
             if dist.get_backend(self.group) == "gloo":      # host-staged (CPU tests, rehearsal runs)
                 host = self.gathered.new_empty(self.gathered.shape, device="cpu")
                 dist.all_gather(list(host.unbind(0)), self.slice.cpu(), group=self.group)
@@ -171,8 +272,30 @@ class ShardedFrame:
                 self._shade_pending = True
             finally:
                 self.pool.set_stream(cur)
+            # the frames are still being written on shade_stream: a consumer
+            # calls ready() (or waits on shaded_event) before reading them
             return self.frames
         self._shade(src)
+        return self.frames
+
+    @property
+    def shaded_event(self):
+        """With a shade_stream: the event the last shade recorded (None before
+        the first one, or without a shade_stream)."""
+        if self.shade_stream is None or not self._shade_pending:
+            return None
+        return self._shaded
+
+    def ready(self, stream=None):
+        """Make `stream` (default: the current stream) wait until the frames
+        of the last exchange are written.  Needed only with a shade_stream,
+        whose shade exchange() leaves in flight; otherwise the frames are
+        written on the stream the exchange ran on."""
+        import torch
+
+        ev = self.shaded_event
+        if ev is not None:
+            (stream or torch.cuda.current_stream()).wait_event(ev)
         return self.frames
 
     def _shade(self, src):
@@ -242,6 +365,15 @@ class FrameGroup:
         call("och_frame_group_render", self._h, C.cast(arr, C.c_void_p), len(cams), int(row_chunk), int(bool(bounce)))
         self._shape = (len(cams), cams[0].height, cams[0].width)
 
+    def render_steps(self, cams, n_steps: int, n_buffers: int = 3, row_chunk: int = 8, bounce: bool = False):
+        """n_steps frames issued by the devices' own threads, up to n_buffers
+        in flight (och_frame_group_render_steps); download() gives the last."""
+        cams = list(cams) if isinstance(cams, (list, tuple)) else [cams]
+        arr = (Camera * len(cams))(*cams)
+        call("och_frame_group_render_steps", self._h, C.cast(arr, C.c_void_p), len(cams), int(n_steps),
+             int(n_buffers), int(row_chunk), int(bool(bounce)))
+        self._shape = (len(cams), cams[0].height, cams[0].width)
+
     def synchronize(self):
         call("och_frame_group_synchronize", self._h)
 
@@ -249,3 +381,57 @@ class FrameGroup:
         out = np.empty(self._shape, np.uint32)
         call("och_frame_group_download", self._h, int(rank), out.ctypes.data)
         return out
+
+
+class ShardedSteps:
+    """A window of sharded frames issued natively (och_gpu_render_sharded_steps_dev):
+    frame k renders this rank's rows as colour codes, exchanges them over the
+    library's RCCL communicator and (where this rank shades) shades them, all
+    on streams[k % B] into frames[k % B]'s buffers -- the work of
+    ShardedFrame.render on that stream, with no interpreter between a frame's
+    launches.  frames: one ShardedFrame per stream, indexed, sharing one pool
+    and made with this comm."""
+
+    def __init__(self, frames, streams, comm: RcclComm, cams, bounce: bool = False):
+        f0 = frames[0]
+        if len(frames) != len(streams) or not all(f.comm is comm and f.indexed and not f.direct for f in frames):
+            raise ValueError("one indexed, sharded ShardedFrame per stream, all on this comm")
+        self.lib = load()
+        self.pool = f0.pool
+        self.frames, self.streams, self.comm = list(frames), list(streams), comm
+        cams = list(cams) if isinstance(cams, (list, tuple)) else [cams]
+        self.cams = (Camera * len(cams))(*cams)
+        self.n_views = len(cams)
+        B = len(frames)
+        mode = f0.exchange_mode
+        if mode == "all_gather" and f0.shade == "display":
+            mode = "display"
+        self.exchange = EXCHANGE[mode]
+        receives = mode != "gather" or f0.rank == 0
+        shades = mode == "all_gather" or f0.rank == 0
+        self._streams = (C.c_void_p * B)(*[s.cuda_stream for s in streams])
+        self._slices = (C.c_void_p * B)(*[f.slice.data_ptr() for f in frames])
+        self._gathered = (C.c_void_p * B)(*[f.gathered.data_ptr() if receives else 0 for f in frames])
+        self._frames = (C.c_void_p * B)(*[f.frames.data_ptr() if shades else 0 for f in frames])
+        self.row_chunk = f0.row_chunk
+        self.bounce = int(bool(bounce))
+
+    def prepare(self, n_steps: int, start_events=None, stop_events=None):
+        """The window's call with its arguments built now; returns issue()."""
+        fn = self.lib.och_gpu_render_sharded_steps_dev
+        e0 = e1 = None
+        if start_events is not None:
+            e0 = (C.c_void_p * n_steps)(*start_events)
+            e1 = (C.c_void_p * n_steps)(*stop_events)
+        args = (self.pool._h, self.comm.handle, C.cast(self.cams, C.c_void_p), self.n_views, int(n_steps),
+                self._streams, self._slices, self._gathered, self._frames, len(self.frames), e0, e1,
+                self.row_chunk, self.bounce, self.exchange)
+
+        def issue():
+            if fn(*args):
+                raise RuntimeError(f"sharded steps: {self.lib.och_last_error().decode()}")
+        return issue
+
+    def run(self, n_steps: int):
+        self.prepare(n_steps)()
+        return self.frames[(n_steps - 1) % len(self.frames)]

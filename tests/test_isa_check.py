@@ -1,0 +1,80 @@
+"""tools/isa_check.py: the build-time check of the descent's asm load
+(OCH_ASM_LOAD) passes on the product kernels and catches the
+compiler outputs it exists to refuse."""
+import subprocess
+import sys
+
+from conftest import ROOT
+
+sys.path.insert(0, str(ROOT / "tools"))
+import isa_check  # noqa: E402
+
+HEAD = "\t.text\n_Z4kern:\n"
+TAIL = "\ts_endpgm\n.Lfunc_end0:\n"
+
+
+def check(body: str):
+    return isa_check.check_function("kern", isa_check.functions(HEAD + body + TAIL)["_Z4kern"])
+
+
+def test_product_kernels_pass():
+    r = subprocess.run([sys.executable, str(ROOT / "tools" / "isa_check.py")], capture_output=True, text=True)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert '"problems": 0' in r.stdout and '"asm_load_enabled": true' in r.stdout
+
+
+def test_clean_loop_passes():
+    body = """.LBB0_1:
+\ts_waitcnt vmcnt(0) ; och_cur_wait v13
+\tv_bfe_u32 v23, v13, v22, 1
+\tds_write_b32 v15, v13
+\tglobal_load_dword v13, v19, s[28:29] offset:-96 ; och_cur_load
+\tv_fma_f32 v19, v18, v5, v3
+\ts_cbranch_execz .LBB0_2
+\tv_max3_u32 v13, v22, v23, v24
+\tv_cmp_gt_i32_e64 s[6:7], 0, v13
+\tds_read_b32 v13, v15
+.LBB0_2:
+\ts_branch .LBB0_1
+"""
+    problems, n = check(body)
+    assert n == 1 and problems == []
+
+
+def test_copy_of_cur_in_flight_fails():
+    body = """\tglobal_load_dword v13, v19, s[28:29] offset:-96 ; och_cur_load
+\tv_mov_b32_e32 v22, v13
+\ts_waitcnt vmcnt(0) ; och_cur_wait v22
+"""
+    problems, _ = check(body)
+    assert problems and "reads v13" in problems[0]
+
+
+def test_wait_on_other_register_fails():
+    body = """\tglobal_load_dword v13, v19, s[28:29] offset:-96 ; och_cur_load
+\tv_mov_b32_e32 v22, 0
+\ts_waitcnt vmcnt(0) ; och_cur_wait v22
+"""
+    problems, _ = check(body)
+    assert problems and "copied while in flight" in problems[0]
+
+
+def test_read_on_one_branch_path_fails():
+    body = """\tglobal_load_dword v13, v19, s[28:29] offset:-96 ; och_cur_load
+\ts_cbranch_execz .LBB0_3
+\tv_mov_b32_e32 v13, 0
+.LBB0_3:
+\tv_add_u32_e32 v1, v13, v2
+\ts_waitcnt vmcnt(0) ; och_cur_wait v13
+"""
+    problems, _ = check(body)
+    assert problems and "v_add_u32" in problems[0]
+
+
+def test_store_of_cur_in_flight_fails():
+    body = """\tglobal_load_dword v[12:13], v19, s[28:29] offset:-96 ; och_cur_load
+\tglobal_store_dword v1, v13, s[2:3]
+\ts_waitcnt vmcnt(0) ; och_cur_wait v[12:13]
+"""
+    problems, _ = check(body)
+    assert problems

@@ -1,0 +1,208 @@
+"""Build-time ISA check of the descent's asm load (OCH_ASM_LOAD, och_kernels.hip).
+
+The grid and bounce kernels issue the child's slot-word load into the ray's
+current-node register `cur` by inline asm, outside the compiler's waitcnt
+view, and wait for it with an explicit `s_waitcnt vmcnt(0)` that takes `cur`
+as an operand (nothing else guarantees the compiler never touches
+`cur` while the load is in flight).  This compiles the kernels to assembly
+with the product's flags and checks, in every function that issues the load:
+  1. the first vmcnt(0) wait on every path from a load, if it is cur's own
+     wait, names the register the load wrote (a compiler copy of cur at a
+     join would make the wait hand a stale register to the next PUSH);
+  2. on every control-flow path from a load to the next vmcnt(0) wait, no
+     instruction reads that register before an instruction on the same path
+     has written it.  Such a read would take the word before the load lands
+     (a copy, a spill, a full-wave select).  Writes there are allowed: they are
+     the STEP phase's temporaries in lanes that issued no load (exec-masked,
+     so the load's return and they never meet, och_kernels.hip OCH_ASM_LOAD).
+Exit status 0 and a one-line summary when every kernel passes; 1 with the
+offending instruction otherwise.  Run by the csrc Makefile (`make isa-check`),
+__graft_entry__.build() and tests/test_isa_check.py.
+
+Usage: python tools/isa_check.py [--source och_kernels.hip] [--asm file.s] [-D NAME=VALUE ...]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import re
+import subprocess
+import sys
+import tempfile
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[1]
+CSRC = ROOT / "octree_ray_tracing_amd" / "csrc"
+HIPCC = "/opt/rocm/bin/hipcc"
+# the product's flags (csrc/Makefile FLAGS + DEVFLAGS), device code only
+FLAGS = ["-std=c++17", "-O3", "-ffp-contract=off", "-fno-fast-math", "--offload-arch=gfx950",
+         "-fno-gpu-flush-denormals-to-zero", "-munsafe-fp-atomics", "--cuda-device-only", "-S"]
+
+REG_RE = re.compile(r"\bv(\d+)\b|\bv\[(\d+):(\d+)\]")
+LABEL_RE = re.compile(r"^(\.LBB\d+_\d+|[A-Za-z_.$][\w.$]*):")
+# instructions without a VGPR destination: every vector operand is a source
+NO_VDST = re.compile(r"^(s_|v_cmp|v_cmpx|v_readfirstlane|v_readlane|global_store|buffer_store|flat_store|"
+                     r"scratch_store|ds_write|ds_store|exp\b|global_atomic(?!.*\bsc0\b)|ds_add_u32|ds_gws)")
+# instructions whose destination is also read (partial writes)
+PARTIAL_DST = re.compile(r"(_sdwa|_d16|_hi\b|_dpp\b|v_writelane|v_mac_|v_fmac_)")
+
+
+def compile_asm(source: Path, defines: list[str]) -> str:
+    with tempfile.TemporaryDirectory() as d:
+        out = Path(d) / "k.s"
+        cmd = [HIPCC, *FLAGS, *[f"-D{x}" for x in defines], str(source), "-o", str(out)]
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise SystemExit(f"isa_check: compile failed:\n{r.stderr[-2000:]}")
+        return out.read_text()
+
+
+def regs(text: str) -> set[int]:
+    out = set()
+    for m in REG_RE.finditer(text):
+        if m.group(1) is not None:
+            out.add(int(m.group(1)))
+        else:
+            out.update(range(int(m.group(2)), int(m.group(3)) + 1))
+    return out
+
+
+def split_operands(ins: str):
+    """(mnemonic, [operand strings]) of one instruction, comment stripped."""
+    body = ins.split(";")[0].split("//")[0].strip()
+    if not body:
+        return "", []
+    parts = body.split(None, 1)
+    mn = parts[0]
+    ops = [o.strip() for o in re.split(r",(?![^\[]*\])", parts[1])] if len(parts) > 1 else []
+    return mn, ops
+
+
+def reads_writes(ins: str):
+    """(VGPRs read, VGPRs fully written) by one instruction."""
+    mn, ops = split_operands(ins)
+    if not mn or not ops:
+        return set(), set()
+    if NO_VDST.match(mn):
+        return set().union(*(regs(o) for o in ops)), set()
+    dst = regs(ops[0])
+    src = set().union(*(regs(o) for o in ops[1:])) if len(ops) > 1 else set()
+    if PARTIAL_DST.search(mn):
+        src |= dst
+    return src, dst
+
+
+def functions(asm: str):
+    """{name: [lines]} of every function body in the assembly text."""
+    out, cur, name = {}, None, None
+    for line in asm.splitlines():
+        if cur is None:
+            m = re.match(r"^([_A-Za-z][\w.$]*):\s*(;.*)?$", line)
+            if m and not line.startswith(".L"):
+                name, cur = m.group(1), []
+            continue
+        if re.match(r"^\.Lfunc_end\d+:", line):
+            out[name] = cur
+            cur = None
+            continue
+        cur.append(line)
+    return out
+
+
+def check_function(name: str, lines: list[str]):
+    """Problems of one function (empty list = passes), and its load count."""
+    ins, labels = [], {}
+    for line in lines:
+        m = LABEL_RE.match(line)
+        if m:
+            labels[m.group(1)] = len(ins)
+            continue
+        t = line.strip()
+        if not t or t.startswith((".", ";")):
+            continue
+        ins.append(t)
+    loads = [i for i, t in enumerate(ins) if "och_cur_load" in t]
+    waits = [i for i, t in enumerate(ins) if "och_cur_wait" in t]
+    if not loads:
+        return [], 0
+    problems = []
+    del waits
+
+    def successors(pc: int):
+        mn, ops = split_operands(ins[pc])
+        if mn == "s_branch":
+            return [labels[ops[0]]] if ops and ops[0] in labels else []
+        if mn.startswith("s_cbranch"):
+            tgt = [labels[ops[0]]] if ops and ops[0] in labels else []
+            return tgt + [pc + 1]
+        if mn in ("s_endpgm", "s_setpc_b64", "s_trap"):
+            return []
+        return [pc + 1]
+
+    for start in loads:
+        creg_text = split_operands(ins[start])[1][0]
+        creg = regs(creg_text)
+        seen = set()
+        stack = [(start + 1, False)]
+        while stack:
+            pc, written = stack.pop()
+            if pc >= len(ins) or (pc, written) in seen:
+                continue
+            seen.add((pc, written))
+            t = ins[pc]
+            mn, _ = split_operands(t)
+            if mn in ("s_swappc_b64", "s_setpc_b64"):
+                problems.append(f"{name}: call with a cur load in flight: {t}")
+                continue
+            if mn == "s_waitcnt" and "vmcnt(0)" in t:
+                # the load has landed; if this is cur's own wait, it must hand
+                # on the register the load wrote (no copy of cur in between)
+                if "och_cur_wait" in t and t.split("och_cur_wait", 1)[1].strip() != creg_text:
+                    problems.append(f"{name}: the load into {creg_text} (instruction {start}) is waited for as "
+                                    f"{t.split('och_cur_wait', 1)[1].strip()}: cur was copied while in flight")
+                continue
+            rd, wr = reads_writes(t)
+            if rd & creg and not written:
+                problems.append(f"{name}: reads {creg_text} while the asm load may be in flight "
+                                f"(load at instruction {start}): {t}")
+                continue
+            if wr & creg:
+                written = True
+            for nxt in successors(pc):
+                stack.append((nxt, written))
+    return problems, len(loads)
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--source", default=str(CSRC / "och_kernels.hip"))
+    ap.add_argument("--asm", default=None, help="check this assembly file instead of compiling")
+    ap.add_argument("-D", dest="defines", action="append", default=[])
+    a = ap.parse_args(argv)
+    asm = Path(a.asm).read_text() if a.asm else compile_asm(Path(a.source), a.defines)
+    fns = functions(asm)
+    checked, problems, loads = [], [], 0
+    for name, lines in fns.items():
+        p, n = check_function(name, lines)
+        if n:
+            checked.append(name)
+            loads += n
+        problems += p
+    want = ("k_trace_grid", "k_trace_bounce")
+    missing = [w for w in want if not any(w in c for c in checked)]
+    asm_on = "och_cur_load" in asm
+    summary = {"functions": len(fns), "checked": len(checked), "asm_loads": loads, "problems": len(problems),
+               "asm_load_enabled": asm_on}
+    if asm_on and missing:
+        problems.append(f"no asm load found in {missing}")
+    if problems:
+        print("isa_check: FAILED " + json.dumps(summary))
+        for p in problems[:20]:
+            print("  " + p)
+        return 1
+    print("isa_check: ok " + json.dumps(summary))
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

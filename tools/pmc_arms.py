@@ -1,4 +1,4 @@
-"""Per-kernel PMC means of the A/B arms of tools/r03m_run.sh (rocprofv3 CSVs under
+"""Per-kernel PMC means of the A/B arms of profiles/r03/scripts/r03m_run.sh (rocprofv3 CSVs under
 gpurun_out/r03m/pmc_<arm>_<group>/): the render kernels only (k_trace_grid /
 k_trace_grid_merge over CameraSource), per dispatch, with the derived VALU lane
 utilisation, VALU per wave and wait fraction."""
