@@ -1038,14 +1038,22 @@ def main():
                 els.append(timed(n, bounce=True, ev=bev))
                 kms_.append(float(np.mean([x.elapsed_time(y) for x, y in bev])))
             return statistics.median(els), statistics.median(kms_)
+        # the pool's compaction mode (OCH_OPT_BOUNCE_COMPACT, default or --opt)
+        # is the line's value; the other two modes are timed beside it
+        mode0 = pool.get_option("bounce_compact")
         b_el, b_kms = bounce_run(a.steps)
         if rank == 0:
             bounce_host = sfs[(a.steps - 1) % len(sfs)].frames.cpu().numpy()
-        pool.set_option("bounce_compact", 0)
-        if pool.get_option("tile_order") >= 2:
-            pool.plan_views(cams, a.row_chunk, rank, world)       # the plan is per compaction setting
-        nc_el, nc_kms = bounce_run(max(a.steps // 2, 3))
-        pool.set_option("bounce_compact", 1)
+        modes = {}
+        for m in (0, 1, 2):
+            if m == mode0:
+                continue
+            pool.set_option("bounce_compact", m)
+            if pool.get_option("tile_order") >= 2:
+                pool.plan_views(cams, a.row_chunk, rank, world)       # the plan is per compaction setting
+            m_el, m_kms = bounce_run(max(a.steps // 2, 3))
+            modes[m] = (m_el / max(a.steps // 2, 3), m_kms)
+        pool.set_option("bounce_compact", mode0)
         if pool.get_option("tile_order") >= 2:
             pool.plan_views(cams, a.row_chunk, rank, world)
         pool.set_stream(stream)
@@ -1060,8 +1068,15 @@ def main():
                   "primary_mrays_s": round(primary * a.steps / b_el / 1e6, 2),
                   "ms_per_step": round(b_el / a.steps * 1e3, 4), "secondary_rays_per_step": secondary,
                   "kernel_ms": round(b_kms, 4),
-                  "compaction_off_ms_per_step": round(nc_el / max(a.steps // 2, 3) * 1e3, 4),
-                  "compaction_off_kernel_ms": round(nc_kms, 4)}
+                  "compaction_mode": {0: "in place, secondary walk started on the primary's stack",
+                                      1: "every block's secondary rays through its LDS queue",
+                                      2: "per block: the queue when it frees a wave, else in place"}[mode0],
+                  "other_modes": {("in_place", "queue", "per_block")[m]: {"ms_per_step": round(t * 1e3, 4),
+                                                                          "kernel_ms": round(k, 4)}
+                                  for m, (t, k) in modes.items()}}
+        if 0 in modes:        # round 3's names: "compaction off" = in place
+            bounce["compaction_off_ms_per_step"] = round(modes[0][0] * 1e3, 4)
+            bounce["compaction_off_kernel_ms"] = round(modes[0][1], 4)
 
     # Roofline of the dominant kernel (the render launch, both views, this
     # rank's rows).  Binding limit: VALU issue -- VALU

@@ -161,8 +161,10 @@ typedef enum och_option {
                                   each handed to one XCD so neighbouring rays share that XCD's L2; 2 = the launch
                                   order planned by och_gpu_plan_views (costliest tiles first) for frames of the
                                   planned geometry, else 0.  Dispatch order only: frames are identical */
-    OCH_OPT_BOUNCE_COMPACT = 6,/* config 5: 1 (default) = compact each block's secondary rays into its first lanes
-                                  (wave ballot/popcount + LDS queue) before tracing them; 0 = trace in place */
+    OCH_OPT_BOUNCE_COMPACT = 6,/* config 5: 1 = compact each block's secondary rays into its first lanes (wave
+                                  ballot/popcount + LDS queue) before tracing them; 0 = trace each in place, the
+                                  walk started on its primary's LDS stack; 2 = per block, compact when that packs
+                                  the block's secondary rays into fewer waves than hold them, else in place */
     OCH_OPT_CHUNK_TILES = 7,   /* schedule 2: 64-ray tiles per wave, a power of two in 1..64 (default 4) */
     OCH_OPT_CULL = 8,          /* 1 (default) = a ray whose walk provably never enters the bounding box of the
                                   pool's voxels (och_pool_occupied_box) is recorded as the miss it would end in,

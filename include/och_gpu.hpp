@@ -10,6 +10,7 @@
 #include <cstdint>
 #include <stdexcept>
 #include <string>
+#include <array>
 #include <vector>
 
 #include "och_gpu.h"
@@ -182,6 +183,15 @@ public:
         check(och_frame_group_render(g_, cams.data(), static_cast<int>(cams.size()), row_chunk, bounce ? 1 : 0),
               "och_frame_group_render");
     }
+    // n_steps frames, up to n_buffers in flight, each device's issued by its own
+    // thread; frames() / download() then give the last one.
+    void render_steps(const std::vector<och_camera> &cams, int n_steps, int n_buffers = 3, int row_chunk = 8,
+                      bool bounce = false)
+    {
+        check(och_frame_group_render_steps(g_, cams.data(), static_cast<int>(cams.size()), n_steps, n_buffers,
+                                           row_chunk, bounce ? 1 : 0),
+              "och_frame_group_render_steps");
+    }
     uint32_t *frames(int rank) const
     {
         uint32_t *p = nullptr;
@@ -193,6 +203,31 @@ public:
 
 private:
     och_frame_group *g_ = nullptr;
+};
+
+// The library's RCCL communicator for one process per GPU: rank 0 makes the
+// id (unique_id()), the launcher hands it to every rank (MPI_Bcast, a file,
+// torch.distributed), every rank constructs comm(id, n_ranks, rank, device).
+class comm {
+public:
+    using id_t = std::array<uint8_t, OCH_COMM_ID_BYTES>;
+    static id_t unique_id()
+    {
+        id_t id{};
+        check(och_comm_unique_id(id.data()), "och_comm_unique_id");
+        return id;
+    }
+    comm(const id_t &id, int n_ranks, int rank, int device)
+    {
+        check(och_comm_create(id.data(), n_ranks, rank, device, &c_), "och_comm_create");
+    }
+    comm(const comm &) = delete;
+    comm &operator=(const comm &) = delete;
+    ~comm() { och_comm_destroy(c_); }
+    och_comm *handle() const { return c_; }
+
+private:
+    och_comm *c_ = nullptr;
 };
 
 // tree_camera's per-frame state (pos :55, dir :53, fov :95).

@@ -891,7 +891,7 @@ OCH_API int och_gpu_set_option(och_gpu_pool *p, int option, int value)
         p->opt_tile_order = value;
         return OCH_OK;
     case OCH_OPT_BOUNCE_COMPACT:
-        if (value != 0 && value != 1) return fail(OCH_E_INVALID, "bounce compaction must be 0 or 1");
+        if (value < 0 || value > 2) return fail(OCH_E_INVALID, "bounce compaction must be 0, 1 or 2");
         p->opt_bounce_compact = value;
         return OCH_OK;
     case OCH_OPT_CHUNK_TILES:

@@ -206,9 +206,26 @@ __device__ __forceinline__ bool ray_cull(const Ray &r, const DevPool &P, const f
 // before iterating.  Launches that count PUSHes cull only at OCH_OPT_CULL = 2
 // (a diagnostic: how many PUSHes the culled launch walks), so their counts
 // stay the reference's.
+template <bool kCount, bool kCull>
+__device__ __forceinline__ bool ray_setup(Ray &r, const DevPool &P, const float *o, const float *d, uint32_t *stack,
+                                          uint32_t stride);
+
 template <bool kPacked, bool kCount, bool kCull = false, bool kAsm = false>
 __device__ __forceinline__ void ray_init(Ray &r, const DevPool &P, const float *o, const float *d, uint32_t *stack,
                                          uint32_t stride)
+{
+    if (!ray_setup<kCount, kCull>(r, P, o, d, stack, stride)) return;
+    if (kPacked && OCH_MERGED_DESCEND)
+        ray_push_descend<true, kAsm>(r, P, stride);
+    else
+        ray_push<kPacked, true>(r, P);
+}
+
+// ray_init's setup (:294-338) up to, not including, the root PUSH.  false:
+// the ray is culled (recorded as the MISS, 0 PUSHes, ray_active false).
+template <bool kCount, bool kCull>
+__device__ __forceinline__ bool ray_setup(Ray &r, const DevPool &P, const float *o, const float *d, uint32_t *stack,
+                                          uint32_t stride)
 {
     r.inv = 24;
     r.idx = 0;
@@ -252,12 +269,9 @@ __device__ __forceinline__ void ray_init(Ray &r, const DevPool &P, const float *
         r.dim = 1u << 23;                                                   // finished: the MISS
         set_mode(r, kStepping);
         if (!OCH_DIM_LEVEL) r.level = 0;
-        return;
+        return false;
     }
-    if (kPacked && OCH_MERGED_DESCEND)
-        ray_push_descend<true, kAsm>(r, P, stride);
-    else
-        ray_push<kPacked, true>(r, P);
+    return true;
 }
 
 // The PUSH / STEP / POP machine (ORT/och_h_octree.h:342-446,
@@ -529,6 +543,65 @@ __device__ __forceinline__ void ray_push_descend(Ray &r, const DevPool &P, uint3
     }
 #endif
     r.idx = nidx;
+}
+
+// OCH_BOUNCE_RESTART: a config-5 secondary ray walked by the lane that
+// walked its primary starts on the primary's LDS stack instead of loading
+// its way down from the root.  The reference traces the secondary from the
+// root (sse_trace(o2, d2), ORT/och_h_octree.h:292-447): setup, then PUSH and
+// descend (:342-376) with t_min = +0 until a PUSH finds its child empty or
+// the leaf level is reached.  Which child each of those PUSHes tests follows
+// from the ray alone (setup's idx, then fma(mid, c, b) >= t_min per level);
+// only the node words come from memory.  As long as the tested child is the
+// one the primary descended into at that level, the node is the primary's
+// ancestor, whose word the primary's walk left in this lane's stack slot of
+// the next level (a descent writes the parent's word at its level; at the
+// primary's HIT, slots 1..depth hold its ancestors).  So those descents read
+// the word from LDS -- no dependent global load -- and everything else
+// (geometry, PUSH count, stack contents) is the from-root walk's, bit for
+// bit.  The first PUSH off the primary's path, or at the leaf level, is the
+// ordinary ray_push_descend.  Children are compared as slot indices (idx ^
+// the sign mask), since the mirrored axis reflects the two rays' frames
+// differently: prim_p / prim_inv are the primary's position bits and sign
+// mask at its HIT (packed merged layout only).
+// Measured and not kept on: the descents it saves are L1 hits
+// (the primary walked those nodes an instant earlier), an LDS read costs
+// about as much, and the on-path loop runs its wave in lockstep -- in place,
+// 0.211 -> 0.219 ms per config-5 step.  Build option only.
+#ifndef OCH_BOUNCE_RESTART
+#define OCH_BOUNCE_RESTART 0
+#endif
+template <bool kCount, bool kAsm>
+__device__ __forceinline__ void ray_init_on_primary(Ray &r, const DevPool &P, const float *o, const float *d,
+                                                    uint32_t *stack, uint32_t stride, const uint32_t prim_p[3],
+                                                    uint32_t prim_inv)
+{
+    if (!ray_setup<kCount, true>(r, P, o, d, stack, stride)) return;
+    // target position bits: the primary's slot bits in this ray's frame
+    const uint32_t flip = prim_inv ^ r.inv;
+    const uint32_t t0 = prim_p[0] ^ (0u - (flip & 1u));
+    const uint32_t t1 = prim_p[1] ^ (0u - ((flip >> 1) & 1u));
+    const uint32_t t2 = prim_p[2] ^ (0u - ((flip >> 2) & 1u));
+    for (;;) {
+        const uint32_t present = __builtin_amdgcn_ubfe(r.cur, r.idx ^ r.inv, 1u);
+        const bool on_path = (((r.p[0] ^ t0) | (r.p[1] ^ t1) | (r.p[2] ^ t2)) & r.dim) == 0;
+        if (!present || !on_path || r.dim == P.dim_lo) break;
+        if (kCount) ++r.push;                                               // PUSH :342-344
+        r.sp += stride;                                                     // :357 (the slot holds this word)
+        r.cur = *r.sp;                                                      // the primary's next ancestor
+        r.dim >>= 1;                                                        // :361
+        const float tm = ffrom(r.t_min);
+        uint32_t nidx = 0;
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {                                       // :363-373
+            const uint32_t mid = r.p[a] | r.dim;
+            const bool upper = __builtin_fmaf(ffrom(mid), r.c[a], r.b[a]) >= tm;
+            nidx |= (uint32_t)upper << a;
+            r.p[a] = upper ? mid : r.p[a];
+        }
+        r.idx = nidx;
+    }
+    ray_push_descend<kCount, kAsm>(r, P, stride);                           // the PUSH off the primary's path
 }
 
 template <bool kPacked, bool kCount, bool kAsm = false>
@@ -984,11 +1057,27 @@ __device__ __forceinline__ uint32_t pixel_colour(const Hit &h, const uint32_t *p
     return palette[6u * (h.voxel - 1u) + (uint32_t)h.dir];
 }
 
+// OCH_NT_FRAME: the RGBA8 frame words are stored non-temporally (streamed
+// past L2 / MALL, which hold the DAG), as k_shade_unshard4 stores its frames.
+#ifndef OCH_NT_FRAME
+#define OCH_NT_FRAME 0
+#endif
+__device__ __forceinline__ void frame_store(uint32_t *out, uint32_t i, uint32_t c)
+{
+    if (OCH_NT_FRAME)
+        __builtin_nontemporal_store(c, out + i);
+    else
+        out[i] = c;
+}
+
 struct FrameSink {
     uint32_t *out;
     const uint32_t *palette;
     uint32_t n_voxels;
-    __device__ __forceinline__ void put(uint32_t i, const Hit &h) const { out[i] = pixel_colour(h, palette, n_voxels); }
+    __device__ __forceinline__ void put(uint32_t i, const Hit &h) const
+    {
+        frame_store(out, i, pixel_colour(h, palette, n_voxels));
+    }
 };
 
 // Config 5 sinks.  put_primary stores what is final for a ray without a
@@ -1001,12 +1090,12 @@ struct BounceFrameSink {
     __device__ __forceinline__ uint32_t put_primary(uint32_t i, const Hit &h, bool bounced) const
     {
         const uint32_t c = pixel_colour(h, f.palette, f.n_voxels);
-        if (!bounced) f.out[i] = c;
+        if (!bounced) frame_store(f.out, i, c);
         return c;
     }
     __device__ __forceinline__ void put_secondary(uint32_t i, uint32_t c, const Hit &h2) const
     {
-        f.out[i] = h2.dir == OCH_EXIT ? c : (((c >> 1) & 0x007F7F7Fu) | (c & 0xFF000000u));
+        frame_store(f.out, i, h2.dir == OCH_EXIT ? c : (((c >> 1) & 0x007F7F7Fu) | (c & 0xFF000000u)));
     }
 };
 
@@ -1321,6 +1410,27 @@ __global__ void k_trace_grid_merge(DevPool P, Src S, Sink K, int merge_k, const 
 // them, so waves whose tiles mostly missed retire instead of idling beside
 // a few bounced lanes.  The queue (8 words per thread, SoA) reuses the
 // parent stacks' LDS between the passes.
+// compact (OCH_OPT_BOUNCE_COMPACT): 0 = every secondary ray in place (by the
+// lane that walked its primary; started on the primary's stack with
+// OCH_BOUNCE_RESTART); 1 = always through the queue; 2 = per block: through
+// the queue when it packs the block's secondary rays into fewer waves than
+// hold them in place, else in place.  On the bench's terrain 98.7 % of the
+// secondary rays sit in waves whose 64 lanes all bounce, so the queue frees
+// few waves; it is still the fastest of the three.
+template <bool kPacked, bool kCount, class Sink>
+__device__ __forceinline__ void bounce_in_place(const DevPool &P, const Sink &K, uint32_t *stack, uint32_t nb,
+                                                const float *o2, const float *d2, uint32_t out, uint32_t payload,
+                                                const uint32_t prim_p[3], uint32_t prim_inv)
+{
+    Ray r;
+    if (kPacked && OCH_MERGED_DESCEND && OCH_LOAD_INTO_CUR && OCH_BOUNCE_RESTART && !OCH_LDS_TOP)
+        ray_init_on_primary<kCount, kAsmLoad>(r, P, o2, d2, stack, nb, prim_p, prim_inv);
+    else
+        ray_init<kPacked, kCount, true, kAsmLoad>(r, P, o2, d2, stack, nb);
+    ray_run<kPacked, kCount, kAsmLoad>(r, P, nb);
+    K.put_secondary(out, payload, ray_result<kPacked, kAsmLoad>(r, P));
+}
+
 template <class Src, class Sink, bool kPacked, bool kCount>
 __global__ void k_trace_bounce(DevPool P, Src S, Sink K, int compact, const uint32_t *__restrict__ order,
                                uint32_t *__restrict__ cost, uint64_t *stamps, uint32_t stamp_cap)
@@ -1335,7 +1445,7 @@ __global__ void k_trace_bounce(DevPool P, Src S, Sink K, int compact, const uint
     const uint32_t nb = blockDim.x;
     const uint32_t wave_base = blk * nb + (threadIdx.x & ~63u);
     float o[3], d[3], o2[3], d2[3];
-    uint32_t out = 0, payload = 0;
+    uint32_t out = 0, payload = 0, prim_p[3] = {0u, 0u, 0u}, prim_inv = 0;
     bool want = false;
     bool miss;
     if (wave_base + (threadIdx.x & 63u) < S.count() &&
@@ -1350,14 +1460,15 @@ __global__ void k_trace_bounce(DevPool P, Src S, Sink K, int compact, const uint
             want = h1.dir < OCH_EXIT;
             if (want) bounce_ray(o, d, h1, P.half_voxel, o2, d2);
             payload = K.put_primary(out, h1, want);
-            if (want && !compact) {                                         // in place, no compaction
-                ray_init<kPacked, kCount, true, kAsmLoad>(r, P, o2, d2, stack, nb);
-                ray_run<kPacked, kCount, kAsmLoad>(r, P, nb);
-                K.put_secondary(out, payload, ray_result<kPacked, kAsmLoad>(r, P));
-            }
+            prim_p[0] = r.p[0];
+            prim_p[1] = r.p[1];
+            prim_p[2] = r.p[2];
+            prim_inv = r.inv;
+            if (want && compact == 0)                                       // in place, no compaction
+                bounce_in_place<kPacked, kCount>(P, K, stack, nb, o2, d2, out, payload, prim_p, prim_inv);
         }
     }
-    if (!compact) {
+    if (compact == 0) {
         if (cost && threadIdx.x == 0) cost[blk] = (uint32_t)(__builtin_amdgcn_s_memtime() - c0);
         if (stamps) stamp(stamps, stamp_cap, t0, 0);
         return;
@@ -1366,11 +1477,19 @@ __global__ void k_trace_bounce(DevPool P, Src S, Sink K, int compact, const uint
     const uint64_t bal = __ballot(want);
     if (lane == 0) wave_count[wave] = (uint32_t)__popcll(bal);
     __syncthreads();
-    uint32_t base = 0, total = 0;
+    uint32_t base = 0, total = 0, holding = 0;
     for (uint32_t w = 0; w < (nb >> 6); ++w) {
         const uint32_t cnt = wave_count[w];
         base += w < wave ? cnt : 0u;
         total += cnt;
+        holding += cnt != 0u;
+    }
+    if (compact == 2 && (total + 63u) / 64u >= holding) {
+        // the queue would not free a wave (block-uniform): in place
+        if (want) bounce_in_place<kPacked, kCount>(P, K, stack, nb, o2, d2, out, payload, prim_p, prim_inv);
+        if (cost && threadIdx.x == 0) cost[blk] = (uint32_t)(__builtin_amdgcn_s_memtime() - c0);
+        if (stamps) stamp(stamps, stamp_cap, t0, 0);
+        return;
     }
     if (want) {
         const uint32_t q = base + (uint32_t)__popcll(bal & ((1ull << lane) - 1ull));

@@ -156,7 +156,7 @@ def test_config4_2160p_as_8_shards(ort, O, gpu_device, d12, d12_ref, pal, deal):
     pool.close()
 
 
-@pytest.mark.parametrize("compact", [1, 0])
+@pytest.mark.parametrize("compact", [1, 0, 2])
 def test_config5_d12_records(ort, O, gpu_device, d12, d12_ref, compact):
     """configs[4]: primary + secondary hit records at depth 12, camera frame and random rays."""
     from test_gpu_parity import assert_same_bounce, gpu_trace_bounce_dev
@@ -173,9 +173,10 @@ def test_config5_d12_records(ort, O, gpu_device, d12, d12_ref, compact):
     pool.close()
 
 
-@pytest.mark.parametrize("compact", [1, 0])
+@pytest.mark.parametrize("compact", [1, 0, 2])
 def test_config5_d12_frames(ort, O, gpu_device, d12, d12_ref, pal, compact):
-    """configs[4] frames through the bench's path (indexed codes, bounce=1), compaction on / off."""
+    """configs[4] frames through the bench's path (indexed codes, bounce=1): compaction on, off (the
+    secondary walk restarted on the primary's stack) and per block."""
     import torch
     from octree_ray_tracing_amd.frame import ShardedFrame
     W, H = 1920, 1080

@@ -153,6 +153,13 @@ def test_deep_sparse_trees(ort, O, gpu_device, depth):
     for layout in (0, 1):
         pool.set_option("layout", layout)
         assert_same(gpu_trace_dev(pool, o, d), ref)
+    # config 5's secondary rays at these depths: the in-place walk restarts on
+    # stacks up to 23 levels deep (OCH_BOUNCE_RESTART)
+    refb = O.trace_bounce_batch(ref_pool, O.Rcp(None), o, d, nthreads=16, want_push=True)
+    pool.set_option("layout", 1)
+    for compact in (0, 1, 2):
+        pool.set_option("bounce_compact", compact)
+        assert_same_bounce(gpu_trace_bounce_dev(pool, o, d), refb)
     pool.close()
 
 
@@ -406,11 +413,15 @@ def test_bounce_records(ort, O, gpu_device, depth):
     ro = rng.uniform(1.01, 1.99, (100000, 3)).astype(np.float32)
     rd = rng.uniform(-1, 1, (100000, 3)).astype(np.float32)
     rd /= np.linalg.norm(rd, axis=1, keepdims=True)
-    for layout in (1, 0):
-        pool.set_option("layout", layout)
-        for origins, dirs in ((ORIGIN, rays), (ro, rd)):
-            ref = O.trace_bounce_batch(ref_pool, O.Rcp(None), origins, dirs, nthreads=16, want_push=True)
-            assert_same_bounce(gpu_trace_bounce_dev(pool, origins, dirs), ref)
+    # the secondary walk: in place on the primary's stack (0), through the
+    # block's queue from the root (1), per block (2); every mode, both layouts
+    for origins, dirs in ((ORIGIN, rays), (ro, rd)):
+        ref = O.trace_bounce_batch(ref_pool, O.Rcp(None), origins, dirs, nthreads=16, want_push=True)
+        for layout in (1, 0):
+            pool.set_option("layout", layout)
+            for compact in (0, 1, 2):
+                pool.set_option("bounce_compact", compact)
+                assert_same_bounce(gpu_trace_bounce_dev(pool, origins, dirs), ref)
     pool.close()
 
 

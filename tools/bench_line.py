@@ -16,7 +16,7 @@ def main(path: str) -> None:
     print(f"{path}: value {d['value']} Mrays/s, {d['ms_per_step']} ms/step, sustained {s.get('value')}, "
           f"kernel {r.get('kernel_ms')} (serial {r.get('kernel_ms_serial')}), host issue/step "
           f"{r.get('host_issue_ms_per_step')}, cull off {d.get('value_cull_off')}, bounce {b.get('value')} "
-          f"({b.get('ms_per_step')} ms, off {b.get('compaction_off_ms_per_step')}), parity {p.get('mismatches')} "
+          f"({b.get('ms_per_step')} ms, mode {str(b.get('compaction_mode'))[:12]}, others {json.dumps(b.get('other_modes'))}), parity {p.get('mismatches')} "
           f"/ {p.get('pixels')}, issue: {d['config'].get('issue', '')[:40]}")
 
 

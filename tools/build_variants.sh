@@ -16,7 +16,8 @@ for spec in "$@"; do
     name=${spec%%:*}
     $HIPCC -shared -fPIC --offload-arch=gfx950 -o build_variants/liboch_gpu_$name.so build_variants/k_$name.o \
         octree_ray_tracing_amd/csrc/build/och_api.o octree_ray_tracing_amd/csrc/build/och_builder.o \
-        octree_ray_tracing_amd/csrc/build/och_editor.o octree_ray_tracing_amd/csrc/build/och_group.o -pthread -ldl
+        octree_ray_tracing_amd/csrc/build/och_editor.o octree_ray_tracing_amd/csrc/build/och_group.o \
+        octree_ray_tracing_amd/csrc/build/och_comm.o -pthread -ldl
     rm -f build_variants/k_$name.o
 done
 ls -la build_variants

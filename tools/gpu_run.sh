@@ -16,6 +16,13 @@
 #   profile                 tools/profile.sh TAG (PMC passes + window trace)
 #   py[:LABEL]=ARGS         python -u tools/ARGS                -> py_LABEL.log
 #   rehearse_n2             tools/rehearse_n2.sh (2 gloo ranks on one GPU)
+#   lib=NAME                later steps load build_variants/liboch_gpu_NAME.so (tools/build_variants.sh);
+#                           lib=default goes back to the in-tree library
+#   pmc:LABEL=COUNTERS      one rocprofv3 --pmc pass (quote the counter list) over the bench's 20-step
+#                           window (BENCH_PMC_ARGS adds bench args) -> pmc_LABEL/, summarised into
+#                           pmc_LABEL.json (tools/pmc_summary.py --window); passes of one LABEL accumulate
+#   pmcpy:LABEL=COUNTERS@SCRIPT ARGS   the same pass over python -u tools/SCRIPT ARGS, every dispatch
+#                           summarised (no window) -> pmc_LABEL.json
 # Example:
 #   bash tools/gpu_run.sh r04a pytest=tests/test_gpu_comm.py "bench:sharded=--sharded --no-cpu-baseline" nccl_host
 set -o pipefail
@@ -64,6 +71,23 @@ for step in "$@"; do
     py)
       timeout -k 10 600 python -u tools/$args > "$O/py_$label.log" 2>&1 || { tail -20 "$O/py_$label.log"; exit $i; }
       tail -3 "$O/py_$label.log" ;;
+    lib)
+      if [[ "$args" == "default" ]]; then unset OCH_GPU_LIB; else export OCH_GPU_LIB=build_variants/liboch_gpu_$args.so; fi
+      [[ -z "$OCH_GPU_LIB" || -f "$OCH_GPU_LIB" ]] || { echo "missing $OCH_GPU_LIB" >&2; exit $i; } ;;
+    pmc)
+      export TMPDIR=/tmp
+      export OCH_TREE_CACHE=${OCH_TREE_CACHE:-/tmp/och_tree_d12.npz}
+      timeout -s KILL 240 rocprofv3 --pmc $args --output-format csv -d "$O/pmc_$label/pmc_pass$i" -o run -- \
+        python -u bench.py --steps 20 --no-cpu-baseline --no-parity --sustain 0 --no-other-configs --no-bounce \
+        --no-cull-off --moving-steps 0 $BENCH_PMC_ARGS > "$O/pmc_${label}_$i.json" 2> "$O/pmc_${label}_$i.err" \
+        || { tail -20 "$O/pmc_${label}_$i.err"; exit $i; }
+      python tools/pmc_summary.py "$O/pmc_$label" --window > "$O/pmc_$label.json" || exit $i ;;
+    pmcpy)
+      export TMPDIR=/tmp
+      counters=${args%%@*}; script=${args#*@}
+      timeout -s KILL 240 rocprofv3 --pmc $counters --output-format csv -d "$O/pmc_$label/pmc_pass$i" -o run -- \
+        python -u tools/$script > "$O/pmc_${label}_$i.log" 2>&1 || { tail -20 "$O/pmc_${label}_$i.log"; exit $i; }
+      python tools/pmc_summary.py "$O/pmc_$label" > "$O/pmc_$label.json" || exit $i ;;
     rehearse_n2)
       bash tools/rehearse_n2.sh > "$O/rehearse_n2.txt" 2>&1 || { tail -20 "$O/rehearse_n2.txt"; exit $i; }
       cp gpurun_out/rehearse_n2.json "$O/" 2>/dev/null ;;
