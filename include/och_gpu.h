@@ -180,9 +180,14 @@ typedef enum och_option {
                                   1 (default) = recorded by the kernel's own dispatch (hipExtLaunchKernel: no
                                   packets between two launches of a stream); 2 = hipEventRecord before and
                                   after the launch; 0 = not timed */
-    OCH_OPT_PLAN = 11          /* shape of och_gpu_plan_views' launch order (set before planning): 0 =
+    OCH_OPT_PLAN = 11,         /* shape of och_gpu_plan_views' launch order (set before planning): 0 =
                                   costliest first; P in 1..99 = the costliest P % first, the rest in natural
                                   order (default 10); 100 = costliest and cheapest alternating */
+    OCH_OPT_SKIP = 12          /* 1 (default) = per-node voxel-box skip: a walk that descends into a node
+                                  whose voxels' bounding box (precomputed per child slot of the packed layout)
+                                  it provably never enters steps out of it at once, as the cull ends a ray
+                                  missing every voxel's box; exact, for launches that do not
+                                  count PUSHes; 2 = counting launches too (diagnostic); 0 = off */
 } och_option;
 OCH_API int och_gpu_set_option(och_gpu_pool *pool, int option, int value);
 OCH_API int och_gpu_get_option(const och_gpu_pool *pool, int option, int *value);
@@ -476,6 +481,15 @@ OCH_API void och_host_pool_free(och_host_pool *pool);
  * root_id | root_mask << 24.  out = NULL only reports *out_nodes. */
 OCH_API int och_pool_pack(const uint32_t *nodes, uint32_t n_nodes, uint32_t root, int depth, int index_base,
                           uint32_t *out, uint32_t out_capacity, uint32_t *out_nodes, uint32_t *out_root);
+/* The per-node skip's boxes (OCH_OPT_SKIP) of a packed pool (och_pool_pack's
+ * output): out[8 * id + k] describes the child in slot k of node id -- the
+ * bounding box of the voxels under it in its own cell, world orientation,
+ * quantised outwards: bits 0-1 x lo and 2-3 (4 - x hi) in quarters, 4-7 the
+ * same for y, 8-11 z lo and 12-15 (16 - z hi) in sixteenths; 0 = the whole
+ * cell, 0xFFFF = no voxel.  Leaf-level and empty slots hold 0.  out holds
+ * n_nodes * 8 entries.  OCH_E_INVALID above depth 20. */
+OCH_API int och_pool_slot_boxes(const uint32_t *packed, uint32_t n_nodes, uint32_t packed_root, int depth,
+                                uint16_t *out);
 /* Bounding box of every non-empty leaf voxel reachable from root, in voxel
  * units: voxel (x, y, z) lies in it iff lo <= (x, y, z) < hi per axis.
  * Returns OCH_OK with lo = hi = {0, 0, 0} for a pool without voxels. */

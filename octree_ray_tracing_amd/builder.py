@@ -122,6 +122,14 @@ def occupied_box(nodes: np.ndarray, root: int, depth: int, index_base: int = 1):
     return tuple(lo), tuple(hi)
 
 
+def slot_boxes(packed: np.ndarray, packed_root: int, depth: int) -> np.ndarray:
+    """The per-node skip's boxes of a packed pool (och_pool_slot_boxes): uint16 (n, 8)."""
+    packed = np.ascontiguousarray(packed, np.uint32).reshape(-1, 8)
+    out = np.zeros(packed.shape, np.uint16)
+    call("och_pool_slot_boxes", packed.ctypes.data, packed.shape[0], int(packed_root), int(depth), out.ctypes.data)
+    return out
+
+
 def pack_pool(nodes: np.ndarray, root: int, depth: int, index_base: int = 1):
     """The packed device layout of a pool (och_pool_pack): (packed nodes, packed root)."""
     nodes = np.ascontiguousarray(nodes, np.uint32).reshape(-1, 8)

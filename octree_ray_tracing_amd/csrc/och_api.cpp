@@ -19,6 +19,7 @@
 namespace {
 
 constexpr uint32_t kIdLimit = 1u << 24;   // packed ids are 24 bits
+constexpr uint32_t kIdLimitMask = kIdLimit - 1;
 
 thread_local std::string g_error;
 
@@ -145,6 +146,7 @@ struct och_gpu_pool {
     std::vector<uint32_t> mirror;
     // packed layout (see och_internal.h DevPool)
     uint32_t *d_packed = nullptr;
+    uint16_t *d_boxes = nullptr;    // per packed slot: the child's voxel box (och::pool_slot_boxes), or none
     uint32_t packed_root = 0;
     uint32_t packed_nodes = 0;
     uint32_t packed_top_ids[5] = {1, 1, 1, 1, 1};   // first id past levels 1..T
@@ -159,6 +161,7 @@ struct och_gpu_pool {
     int opt_merge = 0;
     int opt_timing = 1;                        // OCH_OPT_TIMING
     int opt_plan = 10;                         // OCH_OPT_PLAN (shape of och_gpu_plan_views' order)
+    int opt_skip = 1;                          // OCH_OPT_SKIP (per-node voxel-box skip)
     hipEvent_t next_ev_start = nullptr;        // och_gpu_set_launch_events: the next launch's events
     hipEvent_t next_ev_stop = nullptr;
     // bounding box of the pool's voxels (voxel units, [lo, hi)), for the cull
@@ -234,6 +237,14 @@ struct och_gpu_pool {
         // 1 + k / 2^depth is an exact float for depth <= 22
         p.cull = box_any ? opt_cull : 0;
         p.cam_cull = lut_error <= och::kCameraCullRcpError ? 1 : 0;
+        // the boxes describe the breadth-first packed layout only (an editor's
+        // slot-numbered layout has none)
+        p.boxes = pk && !packed_by_slot ? d_boxes : nullptr;
+        p.skip = p.boxes ? opt_skip : 0;
+        // without boxes the kernel still issues its box load (branch-free):
+        // aim it at the node array, which spans more than 16 B per node, and
+        // skip = 0 keeps every ray's skipmask 0
+        p.box_base = p.boxes ? p.boxes : reinterpret_cast<const uint16_t *>(p.nodes);
         for (int a = 0; a < 3; ++a) {
             p.cull_lo[a] = 1.0F + std::ldexp((float)box_lo[a], -depth);
             p.cull_hi[a] = 1.0F + std::ldexp((float)box_hi[a], -depth);
@@ -441,12 +452,85 @@ bool pack_pool(const uint32_t *nodes, uint32_t n_nodes, uint32_t root, int depth
     return true;
 }
 
+}  // namespace
+
+// Per-slot voxel boxes of a packed pool (the per-node skip, och_internal.h
+// DevPool::boxes): for every interior slot holding child C, the bounding box
+// of the voxels under C in C's own cell, world orientation, quantised
+// outwards to quarters on x and y and sixteenths on z.
+bool och::pool_slot_boxes(const uint32_t *packed, uint32_t n_nodes, uint32_t packed_root, int depth,
+                          std::vector<uint16_t> &out)
+{
+    if (depth < 2 || depth > kSkipMaxDepth || n_nodes < 2) return false;
+    const uint32_t root = packed_root & kIdLimitMask;
+    std::vector<uint8_t> level(n_nodes, 0);
+    level[root] = 1;
+    // breadth-first ids: a parent's id is below its children's
+    for (uint32_t v = 1; v < n_nodes; ++v) {
+        if (!level[v] || level[v] >= depth) continue;
+        for (int k = 0; k < 8; ++k) {
+            const uint32_t w = packed[(size_t)v * 8 + k];
+            if (!w) continue;
+            const uint32_t c = w & kIdLimitMask;
+            if (c <= v || c >= n_nodes) return false;
+            level[c] = (uint8_t)(level[v] + 1);
+        }
+    }
+    // voxel units relative to the node's corner: [lo, hi) per axis
+    std::vector<int32_t> box((size_t)n_nodes * 6, 0);
+    for (uint32_t v = n_nodes - 1; v >= 1; --v) {
+        if (!level[v]) continue;
+        int32_t *b = &box[(size_t)v * 6];
+        b[0] = b[1] = b[2] = INT32_MAX;
+        b[3] = b[4] = b[5] = INT32_MIN;
+        const int32_t half = 1 << (depth - level[v]);           // child size in voxels
+        for (int k = 0; k < 8; ++k) {
+            const uint32_t w = packed[(size_t)v * 8 + k];
+            if (!w) continue;
+            const int32_t *cb = level[v] == depth ? nullptr : &box[(size_t)(w & kIdLimitMask) * 6];
+            if (cb && cb[0] > cb[3]) continue;                   // an empty node holds no voxel
+            for (int a = 0; a < 3; ++a) {
+                const int32_t off = ((k >> a) & 1) * half;
+                b[a] = std::min(b[a], cb ? off + cb[a] : off);
+                b[3 + a] = std::max(b[3 + a], cb ? off + cb[3 + a] : off + 1);
+            }
+        }
+    }
+    out.assign((size_t)n_nodes * 8, 0);
+    for (uint32_t v = 1; v < n_nodes; ++v) {
+        if (!level[v] || level[v] >= depth) continue;
+        const int64_t size = int64_t(1) << (depth - level[v]);   // the child's cell, voxels
+        for (int k = 0; k < 8; ++k) {
+            const uint32_t w = packed[(size_t)v * 8 + k];
+            if (!w) continue;
+            const int32_t *b = &box[(size_t)(w & kIdLimitMask) * 6];
+            if (b[0] > b[3]) {                  // no voxel under the child: an empty box, the walk skips it
+                out[(size_t)v * 8 + k] = kSkipEmptyBox;
+                continue;
+            }
+            uint32_t code = 0;
+            for (int a = 0; a < 3; ++a) {
+                const int64_t q = a < 2 ? 4 : 16, bits = a < 2 ? 2 : 4;
+                const int64_t lo = (int64_t)b[a] * q / size;                  // floor (b >= 0)
+                const int64_t hi = ((int64_t)b[3 + a] * q + size - 1) / size; // ceil
+                code |= (uint32_t)lo << (4 * a) | (uint32_t)(q - hi) << (4 * a + bits);
+            }
+            out[(size_t)v * 8 + k] = (uint16_t)code;
+        }
+    }
+    return true;
+}
+
+namespace {
+
 int upload_packed(och_gpu_pool *p, const uint32_t *nodes, uint32_t n_nodes)
 {
     std::vector<uint32_t> packed;
     uint32_t proot = 0;
     if (p->d_packed) OCH_HIP(hipFree(p->d_packed));
+    if (p->d_boxes) OCH_HIP(hipFree(p->d_boxes));
     p->d_packed = nullptr;
+    p->d_boxes = nullptr;
     p->packed_nodes = 0;
     p->packed_by_slot = false;
     if (!pack_pool(nodes, n_nodes, p->root, p->depth, p->index_base, packed, proot, p->packed_top_ids))
@@ -455,6 +539,11 @@ int upload_packed(och_gpu_pool *p, const uint32_t *nodes, uint32_t n_nodes)
     OCH_HIP(hipMemcpy(p->d_packed, packed.data(), packed.size() * 4, hipMemcpyHostToDevice));
     p->packed_root = proot;
     p->packed_nodes = (uint32_t)(packed.size() / 8);
+    std::vector<uint16_t> boxes;
+    if (och::pool_slot_boxes(packed.data(), p->packed_nodes, proot, p->depth, boxes)) {
+        OCH_HIP(hipMalloc(&p->d_boxes, boxes.size() * 2));
+        OCH_HIP(hipMemcpy(p->d_boxes, boxes.data(), boxes.size() * 2, hipMemcpyHostToDevice));
+    }
     return OCH_OK;
 }
 
@@ -609,6 +698,7 @@ OCH_API int och_gpu_pool_destroy(och_gpu_pool *p)
     if (p->use_ext) (void)hipStreamSynchronize(p->ext_stream);
     if (p->d_nodes) (void)hipFree(p->d_nodes);
     if (p->d_packed) (void)hipFree(p->d_packed);
+    if (p->d_boxes) (void)hipFree(p->d_boxes);
     if (p->d_lut) (void)hipFree(p->d_lut);
     if (p->d_palette) (void)hipFree(p->d_palette);
     if (p->d_code_table) (void)hipFree(p->d_code_table);
@@ -915,6 +1005,10 @@ OCH_API int och_gpu_set_option(och_gpu_pool *p, int option, int value)
         if (value < 0 || value > 100) return fail(OCH_E_INVALID, "plan shape must be 0..100");
         p->opt_plan = value;
         return OCH_OK;
+    case OCH_OPT_SKIP:
+        if (value < 0 || value > 2) return fail(OCH_E_INVALID, "skip must be 0, 1 or 2");
+        p->opt_skip = value;
+        return OCH_OK;
     default:
         return fail(OCH_E_INVALID, "unknown option %d", option);
     }
@@ -936,6 +1030,7 @@ OCH_API int och_gpu_get_option(const och_gpu_pool *p, int option, int *value)
     case OCH_OPT_MERGE: *value = p->opt_merge; return OCH_OK;
     case OCH_OPT_TIMING: *value = p->opt_timing; return OCH_OK;
     case OCH_OPT_PLAN: *value = p->opt_plan; return OCH_OK;
+    case OCH_OPT_SKIP: *value = p->opt_skip; return OCH_OK;
     default: return fail(OCH_E_INVALID, "unknown option %d", option);
     }
 }
@@ -1772,6 +1867,18 @@ OCH_API int och_pool_pack(const uint32_t *nodes, uint32_t n_nodes, uint32_t root
         if (out_capacity < *out_nodes) return fail(OCH_E_CAPACITY, "output holds %u nodes, %u needed", out_capacity, *out_nodes);
         std::memcpy(out, packed.data(), packed.size() * 4);
     }
+    return OCH_OK;
+}
+
+OCH_API int och_pool_slot_boxes(const uint32_t *packed, uint32_t n_nodes, uint32_t packed_root, int depth,
+                                uint16_t *out)
+{
+    if (!packed || !out || n_nodes < 2) return fail(OCH_E_INVALID, "bad slot-box arguments");
+    std::vector<uint16_t> boxes;
+    if (!och::pool_slot_boxes(packed, n_nodes, packed_root, depth, boxes))
+        return fail(OCH_E_INVALID, "no slot boxes for this pool (depth %d above %d, or not a breadth-first packed pool)",
+                    depth, och::kSkipMaxDepth);
+    std::memcpy(out, boxes.data(), boxes.size() * 2);
     return OCH_OK;
 }
 

@@ -4,6 +4,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <vector>
+
 #include "../../include/och_gpu.h"
 
 namespace och {
@@ -38,7 +40,23 @@ struct DevPool {
     // budgets the RCPPS table's relative error: 1 only when the uploaded
     // table's maximum error is within kCameraCullRcpError (och_api.cpp).
     int32_t cam_cull;
+    // Per-node voxel-box skip (OCH_OPT_SKIP; och_kernels.hip ray_skip_node):
+    // per packed slot, the voxel box of its child (och::pool_slot_boxes), or
+    // null; skip as OCH_OPT_SKIP (0 when boxes is null).
+    const uint16_t *boxes;
+    int32_t skip;
+    const uint16_t *box_base;   // boxes, or the node array when there are none (the load's address)
 };
+
+// Per-slot voxel boxes (DevPool::boxes): x and y in quarters of the child's
+// cell, z in sixteenths, each as lo and (Q - hi): bits 0-1 x lo, 2-3 x, 4-5 y
+// lo, 6-7 y, 8-11 z lo, 12-15 z.  0 = the whole cell; kSkipEmptyBox = no voxel.
+// Depths above kSkipMaxDepth carry none (a sixteenth of the leaf-parent cell
+// must be whole mantissa bits).
+constexpr int kSkipMaxDepth = 20;
+constexpr uint16_t kSkipEmptyBox = 0xFFFF;
+bool pool_slot_boxes(const uint32_t *packed, uint32_t n_nodes, uint32_t packed_root, int depth,
+                     std::vector<uint16_t> &out);
 
 // Largest RCPPS-table relative error for which camera_proven_miss is sound
 // (och_kernels.hip has the budget: per-axis factors within 2^-9 of 1 against

@@ -92,6 +92,8 @@ struct Ray {
     int level;            // 1..depth while walking; 0 after a miss, depth + 1 after a hit
     uint32_t mode;        // kAtPush (or finished), kStepping, kPending
     uint32_t push;
+    uint32_t box;         // the voxel box of the node the last descent entered (OCH_NODE_SKIP), else 0
+    uint32_t skipmask;    // 0xFFFF when the per-node skip is exact for this ray, else 0
 };
 
 // Ray phase: due to PUSH (or finished), due to STEP (after a failed PUSH or a
@@ -111,6 +113,14 @@ __device__ __forceinline__ bool in_mode(Ray &r, uint32_t m)
 {
     asm volatile("" : "+v"(r.mode));
     return r.mode == m;
+}
+
+#ifndef OCH_NODE_SKIP
+#define OCH_NODE_SKIP 1
+#endif
+__device__ __forceinline__ bool skip_on(const DevPool &P, bool count)
+{
+    return OCH_NODE_SKIP && (count ? P.skip == 2 : P.skip != 0);
 }
 
 constexpr uint32_t kIdMask = 0x00FFFFFFu;
@@ -165,7 +175,7 @@ __device__ __forceinline__ void ray_push(Ray &r, const DevPool &P)
 #ifndef OCH_DUAL
 #define OCH_DUAL 0
 #endif
-template <bool kCount, bool kAsm = false>
+template <bool kCount, bool kAsm = false, bool kBox = true>
 __device__ __forceinline__ void ray_push_descend(Ray &r, const DevPool &P, uint32_t stride,
                                                  const uint32_t *top = nullptr);
 
@@ -216,9 +226,9 @@ __device__ __forceinline__ void ray_init(Ray &r, const DevPool &P, const float *
 {
     if (!ray_setup<kCount, kCull>(r, P, o, d, stack, stride)) return;
     if (kPacked && OCH_MERGED_DESCEND)
-        ray_push_descend<true, kAsm>(r, P, stride);
+        ray_push_descend<kCount, kAsm>(r, P, stride);
     else
-        ray_push<kPacked, true>(r, P);
+        ray_push<kPacked, kCount>(r, P);
 }
 
 // ray_init's setup (:294-338) up to, not including, the root PUSH.  false:
@@ -265,6 +275,14 @@ __device__ __forceinline__ bool ray_setup(Ray &r, const DevPool &P, const float 
     set_mode(r, kAtPush);
     r.child = 0;
     r.push = 0;
+    r.box = 0;
+    bool exact = true;                                  // the per-node skip's precondition (ray_skip_node)
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        exact &= ((fbits(r.c[a]) >> 23) & 0xFFu) - 1u < 251u;
+        exact &= o[a] > 1.0F && o[a] < 2.0F;
+    }
+    r.skipmask = exact && P.boxes && skip_on(P, kCount) ? 0xFFFFu : 0u;
     if (kCull && (kCount ? P.cull == 2 : P.cull != 0) && ray_cull(r, P, o)) {
         r.dim = 1u << 23;                                                   // finished: the MISS
         set_mode(r, kStepping);
@@ -286,9 +304,16 @@ __device__ __forceinline__ bool ray_setup(Ray &r, const DevPool &P, const float 
 // load every PUSH's slot to test it, so it resolves the slot first (descend,
 // step, push): an empty child then STEPs in the same iteration.
 // stride: words between two levels of one lane's LDS stack.
+constexpr uint32_t kUndoDescent = 0x10000u;   // Ray::box: back out of the node just entered (OCH_NODE_SKIP)
+__device__ __forceinline__ void ray_undo_descent(Ray &r, uint32_t stride);
+
 template <bool kPacked>
 __device__ __forceinline__ void ray_phase_step(Ray &r, uint32_t stride)
 {
+    if (OCH_NODE_SKIP && kPacked && r.box == kUndoDescent) {
+        ray_undo_descent(r, stride);                    // the per-node skip's POP (ray_push_descend)
+        r.box = 0;
+    }
     // STEP :378-419.  The reference's cascade (x if tx <= ty && tx <= tz,
     // else y if ty < tx && ty <= tz, else z) picks the first axis holding
     // the unsigned minimum.
@@ -490,10 +515,83 @@ __device__ __forceinline__ void wait_cur(Ray &r)
     if (kAsm) asm volatile("s_waitcnt vmcnt(0) ; och_cur_wait %0" : "+v"(r.cur) : : "memory");
 }
 
-template <bool kCount, bool kAsm>
+// OCH_NODE_SKIP: the per-node voxel-box skip (OCH_OPT_SKIP; DESIGN.md §4c has
+// the proof).  The occupied-box cull's invariant holds for every cell the walk
+// enters: max_a t_a(hi_a) <= t_min <= min_a t_a(lo_a), t_a(q) = fma(q, c_a,
+// b_a) non-increasing in q.  So a ray for which a box B holding every voxel
+// under node C fails  max_a t_a(B.hi_a) <= min_a t_a(B.lo_a) >= t_min  enters
+// no cell of C that holds a voxel, and cannot hit inside C.  Its excursion
+// through C ends by leaving C through C's exit plane at C's exit t -- the
+// plane and t the STEP right after treating C as empty picks (the POP
+// chain's argument: with every t a non-negative float the exit axis and
+// t_min repeat at each level on the way out).  So the walk that descends
+// into C, reads C's box (loaded with C's word) and steps straight back out
+// (ray_undo_descent: the parent's word from the stack, the level's bits
+// cleared -- one POP) is in the state the full excursion ends in, and every
+// record is the reference's.  Exact for rays with every c_a a negative
+// normal below 2^125 (finite t) and the origin inside (1, 2)^3 (skipmask);
+// launches that count PUSHes skip only at OCH_OPT_SKIP = 2 (a diagnostic).
+
+// bx: the box of the node the last descent entered (och_internal.h
+// DevPool::boxes): x, y in quarters of its cell, z in sixteenths, world
+// orientation, each as lo and Q - hi.  True when the ray provably enters no
+// cell of that box.
+__device__ __forceinline__ bool ray_skip_node(const Ray &r, uint32_t bx)
+{
+    const uint32_t size = r.dim << 1;                    // the node's cell, mantissa units
+    const float tm = ffrom(r.t_min);
+    float enter = -INFINITY, leave = INFINITY;
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        const uint32_t bits = a < 2 ? 2u : 4u, q = 1u << bits;
+        const uint32_t lo = __builtin_amdgcn_ubfe(bx, 4u * a, bits);
+        const uint32_t hc = __builtin_amdgcn_ubfe(bx, 4u * a + bits, bits);
+        const bool refl = (r.inv >> a) & 1u;             // reflected axis: [Q - hi, Q - lo)
+        const uint32_t rlo = refl ? hc : lo, rhi = q - (refl ? lo : hc);
+        const uint32_t step = size >> bits, corner = r.p[a] & ~r.dim;
+        const float tlo = __builtin_fmaf(ffrom(corner + rlo * step), r.c[a], r.b[a]);
+        const float thi = __builtin_fmaf(ffrom(corner + rhi * step), r.c[a], r.b[a]);
+        enter = fmaxf(enter, thi);                       // the near planes: the larger position
+        leave = fminf(leave, tlo);
+    }
+    return enter > leave || leave < tm;
+}
+
+// Back out of the node the last descent entered, as a POP does (:434-444).
+__device__ __forceinline__ void ray_undo_descent(Ray &r, uint32_t stride)
+{
+    r.sp -= stride;
+    r.cur = *r.sp;                                       // the parent's word, written by the descent
+    const uint32_t keep = ~r.dim;
+    r.p[0] &= keep;
+    r.p[1] &= keep;
+    r.p[2] &= keep;
+    r.dim <<= 1;
+    const uint32_t k = __builtin_ctz(r.dim);
+    uint32_t zy = (__builtin_amdgcn_ubfe(r.p[2], k, 1) << 1) | __builtin_amdgcn_ubfe(r.p[1], k, 1);
+    asm volatile("" : "+v"(zy));
+    r.idx = (zy << 1) | __builtin_amdgcn_ubfe(r.p[0], k, 1);
+    set_mode(r, kStepping);
+}
+
+template <bool kCount, bool kAsm, bool kBox>
 __device__ __forceinline__ void ray_push_descend(Ray &r, const DevPool &P, uint32_t stride, const uint32_t *top)
 {
     wait_cur<kAsm>(r);
+    if (OCH_NODE_SKIP) {
+        // skipmask is 0 unless this launch skips and the skip is exact for the ray
+        const uint32_t bx = r.box & r.skipmask;
+        r.box = 0;
+        if (bx && ray_skip_node(r, bx)) {               // the node just entered holds nothing on this ray
+            // back out at the start of the next STEP phase (ray_phase_step):
+            // undone here, the new definition of cur made the compiler copy
+            // cur's register at the loop's latch while other lanes' loads into
+            // it were in flight (tools/isa_check.py)
+            r.box = kUndoDescent;
+            set_mode(r, kStepping);
+            return;
+        }
+    }
     if (!OCH_LOAD_INTO_CUR) r.cur = in_mode(r, kPending) ? r.child : r.cur;
     if (kCount) ++r.push;
     const uint32_t c24 = r.idx ^ r.inv;                                     // 24 + child index
@@ -512,6 +610,14 @@ __device__ __forceinline__ void ray_push_descend(Ray &r, const DevPool &P, uint3
     if (!OCH_DIM_LEVEL) ++r.level;
     *r.sp = r.cur;                          // the parent, before its register takes the child's word
     r.sp += stride;
+    // the child's voxel box (per-node skip), loaded beside its word: boxes
+    // - 48 B + off / 2 = boxes + 2 * (8 * id + child).  Issued whether or not
+    // the launch skips (the host points boxes at the node array when there
+    // are none, and skipmask masks the word): a load under a branch made the
+    // compiler copy the registers of loads in flight at the join (the build's
+    // ISA check, tools/isa_check.py, caught it).
+    if (OCH_NODE_SKIP && kBox)            // the compiler's own load: it waits for it before the box is read
+        r.box = *reinterpret_cast<const uint16_t *>(reinterpret_cast<const char *>(P.box_base) - 48 + (off >> 1));
     if (OCH_LOAD_INTO_CUR && kAsm && !OCH_LDS_TOP)
         asm volatile("global_load_dword %0, %1, %2 offset:-96 ; och_cur_load"   // src = P.nodes - 96 B + off
                      : "+v"(r.cur)

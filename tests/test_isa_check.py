@@ -25,7 +25,7 @@ def test_product_kernels_pass():
 
 def test_clean_loop_passes():
     body = """.LBB0_1:
-\ts_waitcnt vmcnt(0) ; och_cur_wait v13
+\ts_waitcnt vmcnt(0) ; och_cur_wait v13 v30
 \tv_bfe_u32 v23, v13, v22, 1
 \tds_write_b32 v15, v13
 \tglobal_load_dword v13, v19, s[28:29] offset:-96 ; och_cur_load
@@ -54,6 +54,24 @@ def test_wait_on_other_register_fails():
     body = """\tglobal_load_dword v13, v19, s[28:29] offset:-96 ; och_cur_load
 \tv_mov_b32_e32 v22, 0
 \ts_waitcnt vmcnt(0) ; och_cur_wait v22
+"""
+    problems, _ = check(body)
+    assert problems and "copied while in flight" in problems[0]
+
+
+def test_box_load_read_in_flight_fails():
+    body = """\tglobal_load_ushort v30, v19, s[30:31] offset:-48 ; och_box_load
+\tglobal_load_dword v13, v19, s[28:29] offset:-96 ; och_cur_load
+\tv_and_b32_e32 v31, v30, v29
+\ts_waitcnt vmcnt(0) ; och_cur_wait v13 v30
+"""
+    problems, n = check(body)
+    assert n == 2 and problems and "reads v30" in problems[0]
+
+
+def test_box_load_waited_under_other_register_fails():
+    body = """\tglobal_load_ushort v30, v19, s[30:31] offset:-48 ; och_box_load
+\ts_waitcnt vmcnt(0) ; och_cur_wait v13 v31
 """
     problems, _ = check(body)
     assert problems and "copied while in flight" in problems[0]

@@ -6,6 +6,8 @@ view, and wait for it with an explicit `s_waitcnt vmcnt(0)` that takes `cur`
 as an operand (nothing else guarantees the compiler never touches
 `cur` while the load is in flight).  This compiles the kernels to assembly
 with the product's flags and checks, in every function that issues the load:
+  (and the same for the child's voxel-box load of the per-node skip, whose
+  register the wait names second)
   1. the first vmcnt(0) wait on every path from a load, if it is cur's own
      wait, names the register the load wrote (a compiler copy of cur at a
      join would make the wait hand a stale register to the next PUSH);
@@ -121,7 +123,10 @@ def check_function(name: str, lines: list[str]):
         if not t or t.startswith((".", ";")):
             continue
         ins.append(t)
-    loads = [i for i, t in enumerate(ins) if "och_cur_load" in t]
+    # the descent's asm loads: the child's word into cur (och_cur_load) and its
+    # voxel box (och_box_load, the per-node skip); cur's wait names both
+    # registers, in that order ("och_cur_wait <cur> <box>")
+    loads = [i for i, t in enumerate(ins) if "och_cur_load" in t or "och_box_load" in t]
     waits = [i for i, t in enumerate(ins) if "och_cur_wait" in t]
     if not loads:
         return [], 0
@@ -142,6 +147,7 @@ def check_function(name: str, lines: list[str]):
     for start in loads:
         creg_text = split_operands(ins[start])[1][0]
         creg = regs(creg_text)
+        slot = 1 if "och_box_load" in ins[start] else 0
         seen = set()
         stack = [(start + 1, False)]
         while stack:
@@ -157,9 +163,10 @@ def check_function(name: str, lines: list[str]):
             if mn == "s_waitcnt" and "vmcnt(0)" in t:
                 # the load has landed; if this is cur's own wait, it must hand
                 # on the register the load wrote (no copy of cur in between)
-                if "och_cur_wait" in t and t.split("och_cur_wait", 1)[1].strip() != creg_text:
+                named = t.split("och_cur_wait", 1)[1].split() if "och_cur_wait" in t else None
+                if named is not None and (len(named) <= slot or named[slot] != creg_text):
                     problems.append(f"{name}: the load into {creg_text} (instruction {start}) is waited for as "
-                                    f"{t.split('och_cur_wait', 1)[1].strip()}: cur was copied while in flight")
+                                    f"{' '.join(named)}: the register was copied while in flight")
                 continue
             rd, wr = reads_writes(t)
             if rd & creg and not written:
@@ -189,10 +196,11 @@ def main(argv=None) -> int:
             loads += n
         problems += p
     want = ("k_trace_grid", "k_trace_bounce")
+    box_on = "och_box_load" in asm
     missing = [w for w in want if not any(w in c for c in checked)]
     asm_on = "och_cur_load" in asm
     summary = {"functions": len(fns), "checked": len(checked), "asm_loads": loads, "problems": len(problems),
-               "asm_load_enabled": asm_on}
+               "asm_load_enabled": asm_on, "box_load_enabled": box_on}
     if asm_on and missing:
         problems.append(f"no asm load found in {missing}")
     if problems:

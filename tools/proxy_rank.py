@@ -52,6 +52,9 @@ def main():
     ap.add_argument("--deal", choices=("cost", "count", "rr"), default="count", help="as bench.py")
     ap.add_argument("--display-weight", type=float, default=None, help="as bench.py (default 1 - 0.05 N)")
     ap.add_argument("--shade-stream", action="store_true", help="as bench.py: the display rank shades on its own stream")
+    ap.add_argument("--exchange", choices=("all_gather", "gather"), default="all_gather",
+                    help="as bench.py --exchange: 'gather' = only rank 0 receives the slices, so the other ranks' "
+                         "step has no receive (no gathered-buffer write)")
     a = ap.parse_args()
 
     import torch
@@ -154,7 +157,7 @@ def arm(a, torch, pool, streams, cams, W, H, world, shard, nf, opts, deal=None, 
                 if evs is not None:                 # as bench.py: recorded by the render's own dispatch
                     pool.set_launch_events(*evs[k % len(evs)])
                 f_.render_local(cams)
-                if not a.no_exchange:
+                if not a.no_exchange and (a.exchange == "all_gather" or shard == 0):
                     f_.exchange()
         drain()
         return time.perf_counter() - t0
@@ -163,7 +166,7 @@ def arm(a, torch, pool, streams, cams, W, H, world, shard, nf, opts, deal=None, 
     wins = [run(a.steps) for _ in range(a.windows)]
     sus = [run(a.sustain_steps) for _ in range(3)]
     row = {"world": world, "shard": shard, "frame": f"{W}x{H}", "inflight": nf, "opts": opts,
-           "exchange": not a.no_exchange, "shade": a.shade, "shades": a.shade == "all" or shard == 0,
+           "exchange": (a.exchange if not a.no_exchange else None), "shade": a.shade, "shades": a.shade == "all" or shard == 0,
            "deal": a.deal, "shade_stream": a.shade_stream,
            "events": a.events, "rays_per_step_rank": rays_rank, "slice_rows": rows,
            "ms_per_step_20": round(statistics.median(wins) / a.steps * 1e3, 4),
