@@ -161,7 +161,7 @@ struct och_gpu_pool {
     int opt_merge = 0;
     int opt_timing = 1;                        // OCH_OPT_TIMING
     int opt_plan = 10;                         // OCH_OPT_PLAN (shape of och_gpu_plan_views' order)
-    int opt_skip = 1;                          // OCH_OPT_SKIP (per-node voxel-box skip)
+    int opt_skip = 0;                          // OCH_OPT_SKIP (per-node voxel-box skip; boxes built on first use)
     hipEvent_t next_ev_start = nullptr;        // och_gpu_set_launch_events: the next launch's events
     hipEvent_t next_ev_stop = nullptr;
     // bounding box of the pool's voxels (voxel units, [lo, hi)), for the cull
@@ -523,6 +523,26 @@ bool och::pool_slot_boxes(const uint32_t *packed, uint32_t n_nodes, uint32_t pac
 
 namespace {
 
+// The per-node skip's boxes (OCH_OPT_SKIP) of the packed pool, built when the
+// skip is first switched on: 2 B per slot, 80 MB at depth 12, that a pool
+// which never skips does not carry.
+int upload_boxes(och_gpu_pool *p, const std::vector<uint32_t> &packed)
+{
+    std::vector<uint16_t> boxes;
+    if (!och::pool_slot_boxes(packed.data(), p->packed_nodes, p->packed_root, p->depth, boxes)) return OCH_OK;
+    OCH_HIP(hipMalloc(&p->d_boxes, boxes.size() * 2));
+    OCH_HIP(hipMemcpy(p->d_boxes, boxes.data(), boxes.size() * 2, hipMemcpyHostToDevice));
+    return OCH_OK;
+}
+
+int ensure_boxes(och_gpu_pool *p)
+{
+    if (p->d_boxes || !p->d_packed || p->packed_by_slot) return OCH_OK;
+    std::vector<uint32_t> packed((size_t)p->packed_nodes * 8);
+    OCH_HIP(hipMemcpy(packed.data(), p->d_packed, packed.size() * 4, hipMemcpyDeviceToHost));
+    return upload_boxes(p, packed);
+}
+
 int upload_packed(och_gpu_pool *p, const uint32_t *nodes, uint32_t n_nodes)
 {
     std::vector<uint32_t> packed;
@@ -539,12 +559,7 @@ int upload_packed(och_gpu_pool *p, const uint32_t *nodes, uint32_t n_nodes)
     OCH_HIP(hipMemcpy(p->d_packed, packed.data(), packed.size() * 4, hipMemcpyHostToDevice));
     p->packed_root = proot;
     p->packed_nodes = (uint32_t)(packed.size() / 8);
-    std::vector<uint16_t> boxes;
-    if (och::pool_slot_boxes(packed.data(), p->packed_nodes, proot, p->depth, boxes)) {
-        OCH_HIP(hipMalloc(&p->d_boxes, boxes.size() * 2));
-        OCH_HIP(hipMemcpy(p->d_boxes, boxes.data(), boxes.size() * 2, hipMemcpyHostToDevice));
-    }
-    return OCH_OK;
+    return p->opt_skip ? upload_boxes(p, packed) : OCH_OK;
 }
 
 // Largest relative error |r * x - 1| of the table model over x in [-2, -1):
@@ -1008,6 +1023,10 @@ OCH_API int och_gpu_set_option(och_gpu_pool *p, int option, int value)
     case OCH_OPT_SKIP:
         if (value < 0 || value > 2) return fail(OCH_E_INVALID, "skip must be 0, 1 or 2");
         p->opt_skip = value;
+        if (value) {
+            DeviceGuard g(p->device);
+            return ensure_boxes(p);
+        }
         return OCH_OK;
     default:
         return fail(OCH_E_INVALID, "unknown option %d", option);

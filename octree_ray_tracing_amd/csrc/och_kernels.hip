@@ -118,10 +118,16 @@ __device__ __forceinline__ bool in_mode(Ray &r, uint32_t m)
 #ifndef OCH_NODE_SKIP
 #define OCH_NODE_SKIP 1
 #endif
-__device__ __forceinline__ bool skip_on(const DevPool &P, bool count)
+__host__ __device__ __forceinline__ bool skip_on(const DevPool &P, bool count)
 {
-    return OCH_NODE_SKIP && (count ? P.skip == 2 : P.skip != 0);
+    return OCH_NODE_SKIP && P.boxes && (count ? P.skip == 2 : P.skip != 0);
 }
+// The walk's layout template argument (kPacked): 0 the pointer pool, 1 the
+// packed pool, kPackedSkip the packed pool with the per-node skip.  The skip
+// is its own instantiation: its box load, test and back-out cost about 11 %
+// of the packed walk's rate when merely present (measured), so
+// the launch that does not skip runs code without them.
+constexpr int kPackedSkip = 2;
 
 constexpr uint32_t kIdMask = 0x00FFFFFFu;
 
@@ -129,7 +135,7 @@ constexpr uint32_t kIdMask = 0x00FFFFFFu;
 // layout tests presence with the child mask held in the node's slot word and
 // loads only present children; the raw layout loads every slot and tests it
 // when the load has landed (ray_phase_descend).
-template <bool kPacked, bool kCount>
+template <int kPacked, bool kCount>
 __device__ __forceinline__ void ray_push(Ray &r, const DevPool &P)
 {
     if (kCount) ++r.push;
@@ -175,7 +181,7 @@ __device__ __forceinline__ void ray_push(Ray &r, const DevPool &P)
 #ifndef OCH_DUAL
 #define OCH_DUAL 0
 #endif
-template <bool kCount, bool kAsm = false, bool kBox = true>
+template <bool kCount, bool kAsm, bool kBox>
 __device__ __forceinline__ void ray_push_descend(Ray &r, const DevPool &P, uint32_t stride,
                                                  const uint32_t *top = nullptr);
 
@@ -220,13 +226,13 @@ template <bool kCount, bool kCull>
 __device__ __forceinline__ bool ray_setup(Ray &r, const DevPool &P, const float *o, const float *d, uint32_t *stack,
                                           uint32_t stride);
 
-template <bool kPacked, bool kCount, bool kCull = false, bool kAsm = false>
+template <int kPacked, bool kCount, bool kCull = false, bool kAsm = false>
 __device__ __forceinline__ void ray_init(Ray &r, const DevPool &P, const float *o, const float *d, uint32_t *stack,
                                          uint32_t stride)
 {
     if (!ray_setup<kCount, kCull>(r, P, o, d, stack, stride)) return;
     if (kPacked && OCH_MERGED_DESCEND)
-        ray_push_descend<kCount, kAsm>(r, P, stride);
+        ray_push_descend<kCount, kAsm, kPacked == kPackedSkip>(r, P, stride);
     else
         ray_push<kPacked, kCount>(r, P);
 }
@@ -304,16 +310,26 @@ __device__ __forceinline__ bool ray_setup(Ray &r, const DevPool &P, const float 
 // load every PUSH's slot to test it, so it resolves the slot first (descend,
 // step, push): an empty child then STEPs in the same iteration.
 // stride: words between two levels of one lane's LDS stack.
-constexpr uint32_t kUndoDescent = 0x10000u;   // Ray::box: back out of the node just entered (OCH_NODE_SKIP)
+// Ray::mode of a lane that backs out of the node it just entered (the
+// per-node skip, ray_push_descend), then STEPs: negative, so the STEP phase's
+// test (mode <= 0, signed) takes it with the lanes due to STEP.  In the mode
+// register rather than in box: a test of box in the STEP phase made the
+// compiler wait for every lane's box load there (vmcnt(0) at each STEP
+// phase), which undid the loads' overlap with the STEP phase.
+constexpr uint32_t kUndoDescent = 0x80000000u;
 __device__ __forceinline__ void ray_undo_descent(Ray &r, uint32_t stride);
 
-template <bool kPacked>
+__device__ __forceinline__ bool due_to_step(Ray &r)
+{
+    asm volatile("" : "+v"(r.mode));
+    return (int32_t)r.mode <= 0;
+}
+
+template <int kPacked>
 __device__ __forceinline__ void ray_phase_step(Ray &r, uint32_t stride)
 {
-    if (OCH_NODE_SKIP && kPacked && r.box == kUndoDescent) {
+    if (OCH_NODE_SKIP && kPacked == kPackedSkip && r.mode == kUndoDescent)
         ray_undo_descent(r, stride);                    // the per-node skip's POP (ray_push_descend)
-        r.box = 0;
-    }
     // STEP :378-419.  The reference's cascade (x if tx <= ty && tx <= tz,
     // else y if ty < tx && ty <= tz, else z) picks the first axis holding
     // the unsigned minimum.
@@ -412,7 +428,7 @@ __device__ __forceinline__ void ray_phase_step(Ray &r, uint32_t stride)
     r.idx = (zy << 1) | __builtin_amdgcn_ubfe(r.p[0], k, 1);
 }
 
-template <bool kPacked>
+template <int kPacked>
 __device__ __forceinline__ void ray_phase_descend(Ray &r, const DevPool &P, uint32_t stride)
 {
     set_mode(r, kAtPush);
@@ -549,8 +565,9 @@ __device__ __forceinline__ bool ray_skip_node(const Ray &r, uint32_t bx)
         const bool refl = (r.inv >> a) & 1u;             // reflected axis: [Q - hi, Q - lo)
         const uint32_t rlo = refl ? hc : lo, rhi = q - (refl ? lo : hc);
         const uint32_t step = size >> bits, corner = r.p[a] & ~r.dim;
-        const float tlo = __builtin_fmaf(ffrom(corner + rlo * step), r.c[a], r.b[a]);
-        const float thi = __builtin_fmaf(ffrom(corner + rhi * step), r.c[a], r.b[a]);
+        // plane positions: corner + k * step, k <= 16, step < 2^22 -- a 24-bit multiply-add
+        const float tlo = __builtin_fmaf(ffrom(corner + __umul24(rlo, step)), r.c[a], r.b[a]);
+        const float thi = __builtin_fmaf(ffrom(corner + __umul24(rhi, step)), r.c[a], r.b[a]);
         enter = fmaxf(enter, thi);                       // the near planes: the larger position
         leave = fminf(leave, tlo);
     }
@@ -587,8 +604,7 @@ __device__ __forceinline__ void ray_push_descend(Ray &r, const DevPool &P, uint3
             // undone here, the new definition of cur made the compiler copy
             // cur's register at the loop's latch while other lanes' loads into
             // it were in flight (tools/isa_check.py)
-            r.box = kUndoDescent;
-            set_mode(r, kStepping);
+            set_mode(r, kUndoDescent);
             return;
         }
     }
@@ -677,7 +693,7 @@ __device__ __forceinline__ void ray_push_descend(Ray &r, const DevPool &P, uint3
 #ifndef OCH_BOUNCE_RESTART
 #define OCH_BOUNCE_RESTART 0
 #endif
-template <bool kCount, bool kAsm>
+template <bool kCount, bool kAsm, bool kBox>
 __device__ __forceinline__ void ray_init_on_primary(Ray &r, const DevPool &P, const float *o, const float *d,
                                                     uint32_t *stack, uint32_t stride, const uint32_t prim_p[3],
                                                     uint32_t prim_inv)
@@ -707,18 +723,18 @@ __device__ __forceinline__ void ray_init_on_primary(Ray &r, const DevPool &P, co
         }
         r.idx = nidx;
     }
-    ray_push_descend<kCount, kAsm>(r, P, stride);                           // the PUSH off the primary's path
+    ray_push_descend<kCount, kAsm, kBox>(r, P, stride);                     // the PUSH off the primary's path
 }
 
-template <bool kPacked, bool kCount, bool kAsm = false>
+template <int kPacked, bool kCount, bool kAsm = false>
 __device__ __forceinline__ void ray_iterate(Ray &r, const DevPool &P, uint32_t stride, const uint32_t *top = nullptr)
 {
     if (kPacked && OCH_MERGED_DESCEND) {
-        if (in_mode(r, kStepping)) ray_phase_step<kPacked>(r, stride);
+        if (due_to_step(r)) ray_phase_step<kPacked>(r, stride);
         // no activity test: a miss leaves the lane kStepping, a HIT ends in this phase
         uint32_t m = r.mode;                  // tested through an opaque copy, so the skipping
         asm volatile("" : "+v"(m));           // lanes' r.mode is not re-materialised as kStepping
-        if (m != kStepping) ray_push_descend<kCount, kAsm>(r, P, stride, top);
+        if (m != kStepping) ray_push_descend<kCount, kAsm, kPacked == kPackedSkip>(r, P, stride, top);
         return;
     }
     if (!kPacked && in_mode(r, kPending)) ray_phase_descend<kPacked>(r, P, stride);
@@ -761,7 +777,7 @@ __device__ __forceinline__ void ray_walk_packed(Ray &r, const DevPool &P, uint32
 }
 
 // Walk an initialised ray to its HIT or MISS.
-template <bool kPacked, bool kCount, bool kAsm = false>
+template <int kPacked, bool kCount, bool kAsm = false>
 __device__ __forceinline__ void ray_run(Ray &r, const DevPool &P, uint32_t stride, const uint32_t *top = nullptr)
 {
     if (kPacked && OCH_STEP_RUN && OCH_MERGED_DESCEND && OCH_LOAD_INTO_CUR && OCH_POP_CHAIN && !OCH_LDS_TOP) {
@@ -775,7 +791,7 @@ __device__ __forceinline__ void ray_run(Ray &r, const DevPool &P, uint32_t strid
 
 // The hit record of a finished ray (:346-355 hit, :423-431 miss).  The
 // merged loop (OCH_LOAD_INTO_CUR) leaves a HIT's voxel id in cur.
-template <bool kPacked, bool kAsm = false>
+template <int kPacked, bool kAsm = false>
 __device__ __forceinline__ Hit ray_result(Ray &r, const DevPool &P)
 {
     Hit h;
@@ -1312,7 +1328,7 @@ __device__ __forceinline__ uint32_t xcd_block(uint32_t b, uint32_t nb, uint32_t 
 // most expensive workgroups of the planning frame first, so the frame does not
 // end on a few late grazing tiles); cost: optional per-block duration in
 // shader clocks (the planning launch).  Placement only: results are the same.
-template <class Src, class Sink, bool kPacked, bool kCount>
+template <class Src, class Sink, int kPacked, bool kCount>
 __global__ void k_trace_grid(DevPool P, Src S, Sink K, uint32_t xcd_group, const uint32_t *__restrict__ order,
                              uint32_t *__restrict__ cost, uint64_t *stamps, uint32_t stamp_cap)
 {
@@ -1422,9 +1438,11 @@ __device__ __forceinline__ void merge_unpack(Ray &r, uint32_t &out, const uint32
     r.mode = (m >> 15) & 15u;
     r.sp23 = lds + (m >> 19) + 23u * stride;
     r.sp = r.sp23 - k * stride;
+    r.box = 0;                  // a moved ray walks on without the per-node skip
+    r.skipmask = 0;
 }
 
-template <class Src, class Sink>
+template <class Src, class Sink, int kPacked>
 __global__ void k_trace_grid_merge(DevPool P, Src S, Sink K, int merge_k, const uint32_t *__restrict__ order)
 {
     extern __shared__ uint32_t lds_stack[];
@@ -1444,7 +1462,7 @@ __global__ void k_trace_grid_merge(DevPool P, Src S, Sink K, int merge_k, const 
         if (miss) {
             K.put(out, Hit{OCH_EXIT, 0u, P.miss_bits, 0u});
         } else {
-            ray_init<true, false, true, kAsmLoad>(r, P, o, d, lds_stack + threadIdx.x, nb);
+            ray_init<kPacked, false, true, kAsmLoad>(r, P, o, d, lds_stack + threadIdx.x, nb);
             has = true;
         }
     }
@@ -1453,7 +1471,7 @@ __global__ void k_trace_grid_merge(DevPool P, Src S, Sink K, int merge_k, const 
         for (int k = 0; k < merge_k; ++k) {                     // one round of walking
             const bool walking = has && ray_active(r, P);
             if (__ballot(walking) == 0) break;
-            if (walking) ray_iterate<true, false, kAsmLoad>(r, P, nb);
+            if (walking) ray_iterate<kPacked, false, kAsmLoad>(r, P, nb);
         }
         if (has && !ray_active(r, P)) {                         // retire
             K.put(out, ray_result<true, kAsmLoad>(r, P));
@@ -1478,6 +1496,8 @@ __global__ void k_trace_grid_merge(DevPool P, Src S, Sink K, int merge_k, const 
                 uint32_t rank = (uint32_t)__popcll(bal & below);
                 for (uint32_t w = keep; w < wave; ++w) rank += wave_count[w];
                 wait_cur<kAsmLoad>(r);
+                if (kPacked == kPackedSkip && r.mode == kUndoDescent)
+                    ray_undo_descent(r, nb);                    // the mode field has 4 bits
                 uint32_t st[kMergeWords];
                 // the ray's own stack column (not this lane's: a ray adopted
                 // earlier walks on the column it started in)
@@ -1523,21 +1543,21 @@ __global__ void k_trace_grid_merge(DevPool P, Src S, Sink K, int merge_k, const 
 // hold them in place, else in place.  On the bench's terrain 98.7 % of the
 // secondary rays sit in waves whose 64 lanes all bounce, so the queue frees
 // few waves; it is still the fastest of the three.
-template <bool kPacked, bool kCount, class Sink>
+template <int kPacked, bool kCount, class Sink>
 __device__ __forceinline__ void bounce_in_place(const DevPool &P, const Sink &K, uint32_t *stack, uint32_t nb,
                                                 const float *o2, const float *d2, uint32_t out, uint32_t payload,
                                                 const uint32_t prim_p[3], uint32_t prim_inv)
 {
     Ray r;
     if (kPacked && OCH_MERGED_DESCEND && OCH_LOAD_INTO_CUR && OCH_BOUNCE_RESTART && !OCH_LDS_TOP)
-        ray_init_on_primary<kCount, kAsmLoad>(r, P, o2, d2, stack, nb, prim_p, prim_inv);
+        ray_init_on_primary<kCount, kAsmLoad, kPacked == kPackedSkip>(r, P, o2, d2, stack, nb, prim_p, prim_inv);
     else
         ray_init<kPacked, kCount, true, kAsmLoad>(r, P, o2, d2, stack, nb);
     ray_run<kPacked, kCount, kAsmLoad>(r, P, nb);
     K.put_secondary(out, payload, ray_result<kPacked, kAsmLoad>(r, P));
 }
 
-template <class Src, class Sink, bool kPacked, bool kCount>
+template <class Src, class Sink, int kPacked, bool kCount>
 __global__ void k_trace_bounce(DevPool P, Src S, Sink K, int compact, const uint32_t *__restrict__ order,
                                uint32_t *__restrict__ cost, uint64_t *stamps, uint32_t stamp_cap)
 {
@@ -1641,7 +1661,7 @@ __global__ void k_trace_bounce(DevPool P, Src S, Sink K, int compact, const uint
 // tile arithmetic of a refill is wave-uniform (get_refill).
 constexpr uint32_t kNoRay = 0xFFFFFFFFu;
 
-template <class Src, class Sink, bool kPacked, bool kCount>
+template <class Src, class Sink, int kPacked, bool kCount>
 __global__ void k_trace_refill(DevPool P, Src S, Sink K, uint32_t chunk_rays, int refill_min, uint64_t *stamps,
                                uint32_t stamp_cap)
 {
@@ -1691,7 +1711,7 @@ __global__ void k_trace_refill(DevPool P, Src S, Sink K, uint32_t chunk_rays, in
     if (stamps) stamp(stamps, stamp_cap, t0, finished);
 }
 
-template <class Src, class Sink, bool kPacked, bool kCount>
+template <class Src, class Sink, int kPacked, bool kCount>
 __global__ void k_trace_persistent(DevPool P, Src S, Sink K, uint32_t *counter, int refill_min, uint64_t *stamps,
                                    uint32_t stamp_cap)
 {
@@ -1842,7 +1862,7 @@ __global__ __launch_bounds__(256) void k_scatter_slots(const uint32_t *__restric
 // slot below (the miss POP's read) and above (the hit descent's write).
 size_t stack_bytes(int depth, int block) { return (size_t)(depth + 1) * block * sizeof(uint32_t); }
 
-template <class Src, class Sink, bool kPacked, bool kCount>
+template <class Src, class Sink, int kPacked, bool kCount>
 hipError_t launch_as(const DevPool &p, const Src &s, const Sink &k, uint32_t n, const Schedule &sc, hipStream_t stream,
                      uint32_t supertile_rays = 0)
 {
@@ -1869,7 +1889,7 @@ hipError_t launch_as(const DevPool &p, const Src &s, const Sink &k, uint32_t n, 
                            k, sc.counter, sc.refill_min, sc.stamps, sc.stamp_cap);
     } else if (sc.merge_k > 0 && kPacked && !kCount && block >= 128 && block <= 1024) {
         const uint32_t grid = (n + block - 1) / block;
-        OCH_LAUNCH_TIMED(sc, (k_trace_grid_merge<Src, Sink>), dim3(grid), dim3(block),
+        OCH_LAUNCH_TIMED(sc, (k_trace_grid_merge<Src, Sink, kPacked ? kPacked : 1>), dim3(grid), dim3(block),
                            lds > kMergeWords * 4u * (size_t)block ? lds : kMergeWords * 4u * (size_t)block, stream, p,
                            s, k, sc.merge_k, sc.order_n == grid ? sc.order : nullptr);
     } else {
@@ -1889,8 +1909,9 @@ template <class Src, class Sink, bool kCount>
 hipError_t launch(const DevPool &p, const Src &s, const Sink &k, uint32_t n, const Schedule &sc, hipStream_t stream,
                   uint32_t supertile_rays = 0)
 {
-    return p.packed ? launch_as<Src, Sink, true, kCount>(p, s, k, n, sc, stream, supertile_rays)
-                    : launch_as<Src, Sink, false, kCount>(p, s, k, n, sc, stream, supertile_rays);
+    if (!p.packed) return launch_as<Src, Sink, 0, kCount>(p, s, k, n, sc, stream, supertile_rays);
+    return skip_on(p, kCount) ? launch_as<Src, Sink, kPackedSkip, kCount>(p, s, k, n, sc, stream, supertile_rays)
+                              : launch_as<Src, Sink, 1, kCount>(p, s, k, n, sc, stream, supertile_rays);
 }
 
 
@@ -1903,11 +1924,14 @@ hipError_t launch_bounce(const DevPool &p, const Src &s, const Sink &k, uint32_t
     const size_t lds = stack_bytes(p.depth, block) > queue ? stack_bytes(p.depth, block) : queue;
     const dim3 grid((n + block - 1) / block);
     const uint32_t *order = sc.order_n == grid.x ? sc.order : nullptr;   // a plan of exactly this grid
-    if (p.packed)
-        OCH_LAUNCH_TIMED(sc, (k_trace_bounce<Src, Sink, true, kCount>), grid, dim3(block), lds, stream, p, s, k,
+    if (p.packed && skip_on(p, kCount))
+        OCH_LAUNCH_TIMED(sc, (k_trace_bounce<Src, Sink, kPackedSkip, kCount>), grid, dim3(block), lds, stream, p, s, k,
+                           sc.bounce_compact, order, sc.cost, sc.stamps, sc.stamp_cap);
+    else if (p.packed)
+        OCH_LAUNCH_TIMED(sc, (k_trace_bounce<Src, Sink, 1, kCount>), grid, dim3(block), lds, stream, p, s, k,
                            sc.bounce_compact, order, sc.cost, sc.stamps, sc.stamp_cap);
     else
-        OCH_LAUNCH_TIMED(sc, (k_trace_bounce<Src, Sink, false, kCount>), grid, dim3(block), lds, stream, p, s, k,
+        OCH_LAUNCH_TIMED(sc, (k_trace_bounce<Src, Sink, 0, kCount>), grid, dim3(block), lds, stream, p, s, k,
                            sc.bounce_compact, order, sc.cost, sc.stamps, sc.stamp_cap);
     return hipGetLastError();
 }

@@ -1,13 +1,15 @@
 """The per-node voxel-box skip (OCH_OPT_SKIP) against the oracle.
 
-Launches that count PUSHes keep the reference's walk (the skip is off there
-unless OCH_OPT_SKIP = 2), so the record-level parity tests elsewhere run the
-skip only in their frames.  Here every comparison uses launches WITHOUT PUSH
-counts -- the product's -- on the bench's depth-12 terrain and on deep sparse
-trees: camera rays of both views, random rays from inside the tree, rays with
-zero and denormal components (where the skip must stand aside), config 5's
-secondary rays, the tiled batch, and the pointer octree with empty nodes.
-Records (direction, voxel id, t bits) must equal the reference's walk
+The skip is off by default (measured slower on the bench's terrain) and runs
+as its own kernel instantiation (layout argument kPackedSkip), so every test
+here switches it on.  Launches that count PUSHes keep the reference's walk
+unless OCH_OPT_SKIP = 2, so every comparison uses launches WITHOUT PUSH counts
+-- the product's -- on the bench's depth-12 terrain and on deep sparse trees:
+camera rays of both views, random rays from inside the tree, rays with zero and
+denormal components (where the skip must stand aside), config 5's secondary
+rays, the tiled batch, the bench's frame kernels (fused RGBA8, indexed codes,
+the merge schedule), and the pointer octree with empty nodes.  Records
+(direction, voxel id, t bits) and frames must equal the reference's walk
 (oracle/och_oracle.c), bit for bit, with the skip on and off.  The diagnostic
 OCH_OPT_SKIP = 2 shows what the skip saves: the same records with fewer PUSHes."""
 import numpy as np
@@ -52,7 +54,7 @@ def ray_sets(O, n=200000, seed=4):
 @pytest.mark.parametrize("skip", [1, 0])
 def test_d12_records_without_counts(ort, O, gpu_device, d12, d12_ref, skip):
     pool = ort.HOctree(d12.nodes, d12.root, 12, device=0)
-    assert pool.get_option("skip") == 1, "the skip is on by default"
+    assert pool.get_option("skip") == 0, "the skip is off by default"
     pool.set_option("skip", skip)
     for origins, dirs in ray_sets(O):
         ref = O.trace_batch(d12_ref, O.Rcp(None), origins, dirs, nthreads=16)
@@ -82,6 +84,7 @@ def test_d12_skip_saves_pushes(ort, O, gpu_device, d12, d12_ref):
 @pytest.mark.parametrize("compact", [1, 0])
 def test_d12_bounce_records_without_counts(ort, O, gpu_device, d12, d12_ref, compact):
     pool = ort.HOctree(d12.nodes, d12.root, 12, device=0)
+    pool.set_option("skip", 1)
     pool.set_option("bounce_compact", compact)
     for origins, dirs in ray_sets(O, n=100000)[:3]:
         ref = O.trace_bounce_batch(d12_ref, O.Rcp(None), origins, dirs, nthreads=16)
@@ -92,6 +95,7 @@ def test_d12_bounce_records_without_counts(ort, O, gpu_device, d12, d12_ref, com
 def test_d12_tiled_batch_without_counts(ort, O, gpu_device, d12, d12_ref):
     import torch
     pool = ort.HOctree(d12.nodes, d12.root, 12, device=0)
+    pool.set_option("skip", 1)
     W, H = 1920, 1080
     rays = O.raygen(0.3, -0.6, 1.25, W, H)
     ref = O.trace_batch(d12_ref, O.Rcp(None), ORIGIN, rays, nthreads=16)
@@ -137,6 +141,7 @@ def test_deep_sparse_trees_without_counts(ort, O, gpu_device, depth):
     o = o.astype(np.float32)
     ref = O.trace_batch(ref_pool, O.Rcp(None), o, d, nthreads=16)
     pool = ort.HOctree(nodes, root, depth, device=0)
+    pool.set_option("skip", 1)
     assert_same(gpu_trace_dev(pool, o, d, want_push=False), ref, push=False)
     refb = O.trace_bounce_batch(ref_pool, O.Rcp(None), o, d, nthreads=16)
     assert_same_bounce(gpu_trace_bounce_dev(pool, o, d, want_push=False), refb)
@@ -153,5 +158,33 @@ def test_octree_table_with_empty_nodes(ort, O, gpu_device):
     rays = O.raygen(0.3, -0.6, 1.25, 512, 512)
     ref = O.trace_batch(ref_pool, O.Rcp(None), ORIGIN, rays, nthreads=16)
     pool = ort.Octree(nodes, 8, device=0)
+    pool.set_option("skip", 1)
     assert_same(gpu_trace_dev(pool, ORIGIN, rays, want_push=False), ref, push=False)
+    pool.close()
+
+
+def test_d12_frames_with_skip(ort, O, gpu_device, d12, d12_ref):
+    """The bench's frame kernels in the skip instantiation: the fused RGBA8
+    launch, indexed codes + shade, and the merge schedule; config 5's frames."""
+    import torch
+    from octree_ray_tracing_amd.frame import ShardedFrame
+    from test_gpu_configs import FOV, YAW, assert_frames, oracle_frames
+    W, H = 1920, 1080
+    pal = ort.VoxelData().get_colours()
+    pool = ort.HOctree(d12.nodes, d12.root, 12, device=0)
+    pool.set_palette(pal)
+    pool.set_option("skip", 1)
+    cams = [ort.camera(tuple(ORIGIN), YAW, p, FOV, W, H) for p in PITCHES]
+    want = oracle_frames(O, d12_ref, pal, W, H)
+    for direct, merge in ((True, 0), (False, 0), (False, 4)):
+        pool.set_option("merge", merge)
+        sf = ShardedFrame(pool, W, H, 8, n_views=2, indexed=True, direct=direct)
+        sf.render(cams)
+        torch.cuda.synchronize()
+        assert_frames(sf.frames, want)
+    pool.set_option("merge", 0)
+    sf = ShardedFrame(pool, W, H, 8, n_views=2, indexed=True)
+    sf.render(cams, bounce=True)
+    torch.cuda.synchronize()
+    assert_frames(sf.frames, oracle_frames(O, d12_ref, pal, W, H, bounce=True))
     pool.close()

@@ -16,6 +16,7 @@
 #   profile                 tools/profile.sh TAG (PMC passes + window trace)
 #   py[:LABEL]=ARGS         python -u tools/ARGS                -> py_LABEL.log
 #   rehearse_n2             tools/rehearse_n2.sh (2 gloo ranks on one GPU)
+#   env=NAME=VALUE          export NAME=VALUE for later steps
 #   lib=NAME                later steps load build_variants/liboch_gpu_NAME.so (tools/build_variants.sh);
 #                           lib=default goes back to the in-tree library
 #   pmc:LABEL=COUNTERS      one rocprofv3 --pmc pass (quote the counter list) over the bench's 20-step
@@ -71,6 +72,8 @@ for step in "$@"; do
     py)
       timeout -k 10 600 python -u tools/$args > "$O/py_$label.log" 2>&1 || { tail -20 "$O/py_$label.log"; exit $i; }
       tail -3 "$O/py_$label.log" ;;
+    env)
+      export "$args" ;;
     lib)
       if [[ "$args" == "default" ]]; then unset OCH_GPU_LIB; else export OCH_GPU_LIB=build_variants/liboch_gpu_$args.so; fi
       [[ -z "$OCH_GPU_LIB" || -f "$OCH_GPU_LIB" ]] || { echo "missing $OCH_GPU_LIB" >&2; exit $i; } ;;
