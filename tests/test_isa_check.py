@@ -59,24 +59,6 @@ def test_wait_on_other_register_fails():
     assert problems and "copied while in flight" in problems[0]
 
 
-def test_box_load_read_in_flight_fails():
-    body = """\tglobal_load_ushort v30, v19, s[30:31] offset:-48 ; och_box_load
-\tglobal_load_dword v13, v19, s[28:29] offset:-96 ; och_cur_load
-\tv_and_b32_e32 v31, v30, v29
-\ts_waitcnt vmcnt(0) ; och_cur_wait v13 v30
-"""
-    problems, n = check(body)
-    assert n == 2 and problems and "reads v30" in problems[0]
-
-
-def test_box_load_waited_under_other_register_fails():
-    body = """\tglobal_load_ushort v30, v19, s[30:31] offset:-48 ; och_box_load
-\ts_waitcnt vmcnt(0) ; och_cur_wait v13 v31
-"""
-    problems, _ = check(body)
-    assert problems and "copied while in flight" in problems[0]
-
-
 def test_read_on_one_branch_path_fails():
     body = """\tglobal_load_dword v13, v19, s[28:29] offset:-96 ; och_cur_load
 \ts_cbranch_execz .LBB0_3

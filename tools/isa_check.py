@@ -5,9 +5,8 @@ current-node register `cur` by inline asm, outside the compiler's waitcnt
 view, and wait for it with an explicit `s_waitcnt vmcnt(0)` that takes `cur`
 as an operand (nothing else guarantees the compiler never touches
 `cur` while the load is in flight).  This compiles the kernels to assembly
-with the product's flags and checks, in every function that issues the load:
-  (and the same for the child's voxel-box load of the per-node skip, whose
-  register the wait names second)
+with the product's flags and checks, in every function that issues the load
+(the per-node skip's box load is the compiler's own and needs no check):
   1. the first vmcnt(0) wait on every path from a load, if it is cur's own
      wait, names the register the load wrote (a compiler copy of cur at a
      join would make the wait hand a stale register to the next PUSH);
@@ -123,15 +122,11 @@ def check_function(name: str, lines: list[str]):
         if not t or t.startswith((".", ";")):
             continue
         ins.append(t)
-    # the descent's asm loads: the child's word into cur (och_cur_load) and its
-    # voxel box (och_box_load, the per-node skip); cur's wait names both
-    # registers, in that order ("och_cur_wait <cur> <box>")
-    loads = [i for i, t in enumerate(ins) if "och_cur_load" in t or "och_box_load" in t]
-    waits = [i for i, t in enumerate(ins) if "och_cur_wait" in t]
+    # the descent's asm loads of the child's word into cur (och_cur_load)
+    loads = [i for i, t in enumerate(ins) if "och_cur_load" in t]
     if not loads:
         return [], 0
     problems = []
-    del waits
 
     def successors(pc: int):
         mn, ops = split_operands(ins[pc])
@@ -147,7 +142,6 @@ def check_function(name: str, lines: list[str]):
     for start in loads:
         creg_text = split_operands(ins[start])[1][0]
         creg = regs(creg_text)
-        slot = 1 if "och_box_load" in ins[start] else 0
         seen = set()
         stack = [(start + 1, False)]
         while stack:
@@ -164,7 +158,7 @@ def check_function(name: str, lines: list[str]):
                 # the load has landed; if this is cur's own wait, it must hand
                 # on the register the load wrote (no copy of cur in between)
                 named = t.split("och_cur_wait", 1)[1].split() if "och_cur_wait" in t else None
-                if named is not None and (len(named) <= slot or named[slot] != creg_text):
+                if named is not None and (not named or named[0] != creg_text):
                     problems.append(f"{name}: the load into {creg_text} (instruction {start}) is waited for as "
                                     f"{' '.join(named)}: the register was copied while in flight")
                 continue
@@ -196,11 +190,10 @@ def main(argv=None) -> int:
             loads += n
         problems += p
     want = ("k_trace_grid", "k_trace_bounce")
-    box_on = "och_box_load" in asm
     missing = [w for w in want if not any(w in c for c in checked)]
     asm_on = "och_cur_load" in asm
     summary = {"functions": len(fns), "checked": len(checked), "asm_loads": loads, "problems": len(problems),
-               "asm_load_enabled": asm_on, "box_load_enabled": box_on}
+               "asm_load_enabled": asm_on}
     if asm_on and missing:
         problems.append(f"no asm load found in {missing}")
     if problems:
