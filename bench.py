@@ -470,8 +470,8 @@ def main():
                          "+ och_deal_chunks), by count (rank 0 at --display-weight), or round-robin")
     ap.add_argument("--display-weight", type=float, default=None,
                     help="N > 1 with --shade display: rank 0's share of the row chunks relative to the other ranks "
-                         "(it also shades the whole frame); default 1 - 0.05 N, from tools/proxy_rank.py sweeps "
-                         "(DESIGN.md §5)")
+                         "(it also shades the whole frame); default ort.display_weight(N, exchange): 0.9 / 0.7 / "
+                         "0.5 at N = 2 / 4 / 8 with the gather, from tools/proxy_rank.py sweeps (DESIGN.md §5)")
     ap.add_argument("--no-direct", action="store_true",
                     help="N = 1: render codes and shade them in a second pass, as ranks do at N > 1, instead of "
                          "the fused launch writing the RGBA8 frames directly")
@@ -481,12 +481,13 @@ def main():
     ap.add_argument("--sharded", action="store_true",
                     help="N = 1: the N > 1 step at world size 1 -- render colour codes, exchange them over RCCL "
                          "(--exchange) and shade -- instead of the fused launch writing RGBA8 frames")
-    ap.add_argument("--exchange", choices=("rccl", "gather", "torch"), default="rccl",
-                    help="sharded steps (N > 1, or --sharded): 'rccl' = all-gather on the library's own RCCL "
-                         "communicator (och_comm_*, its id broadcast by torch.distributed), the window issued by "
-                         "one och_gpu_render_sharded_steps_dev call per rank; 'gather' = the same, but only rank 0 "
-                         "(the display) receives the slices; 'torch' = dist.all_gather_into_tensor per step from "
-                         "Python.  The gloo rehearsal backend always exchanges through torch")
+    ap.add_argument("--exchange", choices=("rccl", "gather", "torch"), default="gather",
+                    help="sharded steps (N > 1, or --sharded): 'gather' (default) = only rank 0 (the display) "
+                         "receives the slices, ncclSend / ncclRecv on the library's own RCCL communicator "
+                         "(och_comm_*, its id broadcast by torch.distributed), the window issued by one "
+                         "och_gpu_render_sharded_steps_dev call per rank; 'rccl' = the same with ncclAllGather; "
+                         "'torch' = dist.all_gather_into_tensor per step from Python.  The gloo rehearsal "
+                         "backend always exchanges through torch"),
     ap.add_argument("--hw-queues", type=int, default=None,
                     help="GPU_MAX_HW_QUEUES for this process (set before HIP starts); default the "
                          "environment's (4 on the box), 8 at N >= 8")
@@ -558,7 +559,7 @@ def main():
     # share at --display-weight); every rank gets the same table.
     deal = None
     if a.display_weight is None:
-        a.display_weight = max(0.5, 1.0 - 0.05 * world)
+        a.display_weight = ort.display_weight(world, exch_mode)
     if world > 1 and a.deal != "rr":
         n_chunks = -(-H // a.row_chunk)
         table = torch.zeros(n_chunks, dtype=torch.int32, device=dev)

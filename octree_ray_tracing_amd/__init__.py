@@ -10,10 +10,10 @@ from ._lib import OchError, library_path, load
 from .builder import NodePool, build_terrain, occupied_box, pack_pool, slot_boxes
 from .editor import Editor
 from .frame import FrameGroup, RcclComm, ShardedFrame, ShardedSteps
-from .tracer import (Direction, GpuPool, HOctree, Octree, camera, deal_chunks, device_count, device_list, host_rcp_lut,
+from .tracer import (Direction, GpuPool, HOctree, Octree, camera, deal_chunks, display_weight, device_count, device_list, host_rcp_lut,
                      rcp_from_lut, rcp_lut_error, shard_rows)
 from .voxels import VoxelData, VoxelDataError
 
 __all__ = ["OchError", "library_path", "load", "NodePool", "build_terrain", "occupied_box", "pack_pool", "slot_boxes", "Editor", "FrameGroup", "RcclComm", "ShardedFrame", "ShardedSteps", "Direction", "GpuPool",
-           "HOctree", "Octree", "camera", "deal_chunks", "device_count", "device_list", "host_rcp_lut", "rcp_from_lut", "rcp_lut_error", "shard_rows",
+           "HOctree", "Octree", "camera", "deal_chunks", "display_weight", "device_count", "device_list", "host_rcp_lut", "rcp_from_lut", "rcp_lut_error", "shard_rows",
            "VoxelData", "VoxelDataError"]

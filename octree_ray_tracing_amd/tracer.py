@@ -387,6 +387,21 @@ def deal_chunks(costs, n_shards: int, weights=None) -> np.ndarray:
     return out
 
 
+# The display rank's share of the row chunks (it also shades the whole frame),
+# per world size and exchange, from tools/proxy_rank.py sweeps of every shard
+# (profiles/r04/r04e/, r04f/): with the gather to rank 0 the
+# other ranks receive nothing, so the display rank takes a smaller share.
+DISPLAY_WEIGHTS = {"gather": {2: 0.9, 4: 0.7, 8: 0.5}, "all_gather": {2: 0.9, 4: 0.8, 8: 0.6}}
+
+
+def display_weight(world: int, exchange: str = "gather") -> float:
+    """Default deal weight of rank 0 (the display rank) at this world size."""
+    table = DISPLAY_WEIGHTS.get(exchange, DISPLAY_WEIGHTS["all_gather"])
+    if world in table:
+        return table[world]
+    return max(0.5, 1.0 - (0.0625 if exchange == "gather" else 0.05) * world)
+
+
 class HOctree(GpuPool):
     """och::h_octree's table on the GPU: 1-based, miss t = +INF (ORT/och_h_octree.h:429)."""
 
