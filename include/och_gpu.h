@@ -416,7 +416,9 @@ OCH_API int och_comm_destroy(och_comm *comm);
 OCH_API int och_comm_info(const och_comm *comm, int *n_ranks, int *rank, int *device);
 /* recv = [n_ranks][bytes]: every rank's `bytes` (ncclAllGather), enqueued on stream. */
 OCH_API int och_comm_all_gather(och_comm *comm, const void *send, void *recv, size_t bytes, void *stream);
-/* Only rank `root` receives recv = [n_ranks][bytes]; the others send (recv may be NULL there). */
+/* Only rank `root` receives recv = [n_ranks][bytes]; the others send (recv may be NULL there).
+ * One ncclSend / ncclRecv group per call: the root receives from every rank, its own slice
+ * included (a send to itself, skipped when send already sits at recv + root * bytes). */
 OCH_API int och_comm_gather(och_comm *comm, const void *send, void *recv, size_t bytes, int root, void *stream);
 
 /* Exchange of a sharded frame (och_gpu_render_sharded_steps_dev). */

@@ -128,17 +128,18 @@ int comm_gather(och_comm *c, const void *send, void *recv, size_t bytes, int roo
     if (c->rank == root) {
         if (recv == nullptr) return comm_fail(OCH_E_INVALID, "the gather root needs a receive buffer");
         char *dst = static_cast<char *>(recv);
-        if (send != dst + (size_t)root * bytes) {
-            const hipError_t e = hipMemcpyAsync(dst + (size_t)root * bytes, send, bytes, hipMemcpyDeviceToDevice, stream);
-            if (e != hipSuccess) return comm_fail(OCH_E_HIP, std::string("gather self copy: ") + hipGetErrorString(e));
-        }
-        if (c->n_ranks == 1) return OCH_OK;
+        // One group: a receive from every rank, the root's own slice included
+        // (a send to itself), so the same RCCL calls run at every world size --
+        // world size 1, the one a one-GPU box can run, exercises them too.
         ncclResult_t r = R.group_start();
+        if (r == ncclSuccess && send != dst + (size_t)root * bytes)
+            r = R.send(send, bytes, ncclUint8, root, c->comm, stream);
         for (int p = 0; p < c->n_ranks && r == ncclSuccess; ++p)
-            if (p != root) r = R.recv(dst + (size_t)p * bytes, bytes, ncclUint8, p, c->comm, stream);
+            if (p != root || send != dst + (size_t)root * bytes)
+                r = R.recv(dst + (size_t)p * bytes, bytes, ncclUint8, p, c->comm, stream);
         const ncclResult_t e = R.group_end();
         if (r == ncclSuccess) r = e;
-        return r == ncclSuccess ? OCH_OK : rccl_fail("ncclRecv group", r);
+        return r == ncclSuccess ? OCH_OK : rccl_fail("ncclSend / ncclRecv group", r);
     }
     const ncclResult_t r = R.send(send, bytes, ncclUint8, root, c->comm, stream);
     return r == ncclSuccess ? OCH_OK : rccl_fail("ncclSend", r);
