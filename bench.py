@@ -677,6 +677,23 @@ def main():
                          "per wave; per_view = one launch per view, two_views = both views' rays in one launch "
                          "(W x 2H, planned with och_gpu_plan_batch_tiled)")
         trace_only["tiled"] = tiled
+        # the arbitrary-order call with both views' rays in one launch: the same
+        # launch size as the render's, so the per-ray comparison with it is not
+        # set by one launch's latency floor (a lone launch ends on its grazing tiles)
+        tms = []
+        for _ in range(5):
+            pool.trace_batch_dev(o_t, both, bd, bv, bt)
+        for _ in range(10):
+            s0, s1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s0.record(stream)
+            pool.trace_batch_dev(o_t, both, bd, bv, bt)
+            s1.record(stream)
+            tms.append((s0, s1))
+        torch.cuda.synchronize()
+        ms = np.array([x.elapsed_time(y) for x, y in tms])
+        trace_only["two_views"] = {"mrays_s": 2 * n_px * len(tms) / ms.sum() / 1e3, "ms_per_launch": float(ms.mean()),
+                                   "rays_per_launch": 2 * n_px,
+                                   "path": "och_gpu_trace_batch_dev over both views' rays (row-major) in one launch"}
         del both, bd, bv, bt
     del hd, hv, ht, hp, dirs
 
@@ -916,6 +933,7 @@ def main():
         lone = latency_ms / (W * H * len(cams))
         trace_only["vs_lone_render_per_ray"] = {
             "untiled_per_view": round(trace_only["ms_per_frame"] / n_px / lone, 3),
+            "untiled_two_views": round(trace_only["two_views"]["ms_per_launch"] / (2 * n_px) / lone, 3),
             "tiled_two_views": round(trace_only["tiled"]["two_views"]["ms_per_launch"] / (2 * n_px) / lone, 3)}
     # warmup, then the timed steps
     for k in range(a.warmup):
