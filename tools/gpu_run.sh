@@ -16,6 +16,7 @@
 #   profile                 tools/profile.sh TAG (PMC passes + window trace)
 #   py[:LABEL]=ARGS         python -u tools/ARGS                -> py_LABEL.log
 #   rehearse_n2             tools/rehearse_n2.sh (2 gloo ranks on one GPU)
+#   rehearse_n8[=ARGS]      tools/rehearse_n8.sh ARGS (8 gloo ranks on one GPU; ARGS go to bench.py)
 #   env=NAME=VALUE          export NAME=VALUE for later steps
 #   lib=NAME                later steps load build_variants/liboch_gpu_NAME.so (tools/build_variants.sh);
 #                           lib=default goes back to the in-tree library
@@ -94,6 +95,9 @@ for step in "$@"; do
     rehearse_n2)
       bash tools/rehearse_n2.sh > "$O/rehearse_n2.txt" 2>&1 || { tail -20 "$O/rehearse_n2.txt"; exit $i; }
       cp gpurun_out/rehearse_n2.json "$O/" 2>/dev/null ;;
+    rehearse_n8)
+      bash tools/rehearse_n8.sh $args > "$O/rehearse_n8.txt" 2>&1 || { tail -20 "$O/rehearse_n8.txt"; exit $i; }
+      cp gpurun_out/rehearse_n8/bench.json "$O/rehearse_n8.json" 2>/dev/null; tail -c 600 "$O/rehearse_n8.txt" ;;
     *)
       echo "unknown step $step" >&2; exit 100 ;;
   esac
