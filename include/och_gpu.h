@@ -188,8 +188,8 @@ typedef enum och_option {
                                   when the option is first set, 2 B per slot) it provably never enters steps
                                   out of it at once, as the cull ends a ray missing every voxel's box; exact
                                   (DESIGN.md §4c), for launches that do not count PUSHes; 2 = counting
-                                  launches too (diagnostic); 0 (default) = off: on the bench's terrain the
-                                  skip walks 25-40 % fewer PUSHes yet runs 17 % slower */
+                                  launches too (diagnostic); 0 (default) = off: the skip walks 25-40 % fewer
+                                  PUSHes yet runs 13-19 % slower on every scene measured */
 } och_option;
 OCH_API int och_gpu_set_option(och_gpu_pool *pool, int option, int value);
 OCH_API int och_gpu_get_option(const och_gpu_pool *pool, int option, int *value);
