@@ -117,9 +117,9 @@ int comm_all_gather(och_comm *c, const void *send, void *recv, size_t bytes, hip
     return r == ncclSuccess ? OCH_OK : rccl_fail("ncclAllGather", r);
 }
 
-// Rank `root` receives every rank's `bytes` into recv[r * bytes] (its own
-// slice copied on the device); the other ranks only send.  One RCCL group of
-// point-to-point calls: no rank but the root spends HBM or CUs on receiving.
+// Rank `root` receives every rank's `bytes` into recv[r * bytes]; the other
+// ranks only send.  One RCCL group of point-to-point calls on the root: no rank
+// but the root spends HBM or CUs on receiving.
 int comm_gather(och_comm *c, const void *send, void *recv, size_t bytes, int root, hipStream_t stream)
 {
     if (!c || !c->comm) return comm_fail(OCH_E_INVALID, "communicator is NULL or destroyed");
