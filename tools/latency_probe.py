@@ -30,7 +30,6 @@ def main():
 
     import torch
     import octree_ray_tracing_amd as ort
-    from oracle import oracle as O
 
     torch.cuda.set_device(0)
     dev = torch.device("cuda", 0)
@@ -70,8 +69,10 @@ def main():
             res[f"render2_layout{layout}_block{block}_us"] = round(timed(lambda: pool.render_views_dev(cams2, both)) * 1e3, 1)
     print(json.dumps({k: v for k, v in res.items()}), flush=True)
     for pitch, pix in WORST.items():
-        rays = O.raygen(0.3, pitch, 1.25, 1920, 1080)
         cam = ort.camera((1.5, 1.5, 1.5), 0.3, pitch, 1.25, 1920, 1080)
+        rays_dev = torch.empty(1920 * 1080 * 3, dtype=torch.float32, device=dev)
+        pool.raygen_dev(cam, rays_dev)           # the reference's raygen, bit-exact (och_gpu_raygen_dev)
+        rays = rays_dev.cpu().numpy().reshape(-1, 3)
         frame = torch.empty(1920 * 1080, dtype=torch.int32, device=dev)
         for layout in (0, 1):
             pool.set_option("layout", layout)
