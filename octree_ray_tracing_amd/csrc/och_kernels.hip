@@ -1328,10 +1328,19 @@ __device__ __forceinline__ uint32_t xcd_block(uint32_t b, uint32_t nb, uint32_t 
 // most expensive workgroups of the planning frame first, so the frame does not
 // end on a few late grazing tiles); cost: optional per-block duration in
 // shader clocks (the planning launch).  Placement only: results are the same.
+// OCH_GRID_VGPR: occupancy experiments -- the grid kernel claims VGPRs up to
+// this register (a clobber of it), so its allocation caps the waves per SIMD
+// (8 up to v63, 7 to v71, 6 to v79, 5 to v95, 4 to v127) and fewer waves
+// share a CU's L1.
+#define OCH_STR2(x) #x
+#define OCH_STR(x) OCH_STR2(x)
 template <class Src, class Sink, int kPacked, bool kCount>
 __global__ void k_trace_grid(DevPool P, Src S, Sink K, uint32_t xcd_group, const uint32_t *__restrict__ order,
                              uint32_t *__restrict__ cost, uint64_t *stamps, uint32_t stamp_cap)
 {
+#ifdef OCH_GRID_VGPR
+    asm volatile("; occupancy cap" ::: "v" OCH_STR(OCH_GRID_VGPR));
+#endif
     extern __shared__ uint32_t lds_stack[];
     const uint64_t t0 = stamps ? realtime() : 0;
     const uint64_t c0 = cost ? __builtin_amdgcn_s_memtime() : 0;
