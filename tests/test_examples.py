@@ -1,7 +1,9 @@
 """The C++ boundary, exercised: examples/render_frame (och::gpu::tree --
 the reference's tree.sse_trace(o, d, dir&, voxel&, t&) call shape and the
-update_image frame) and examples/multi_gpu_frame (och::gpu::frame_group, one
-process over every GPU, RCCL all-gather) are built by __graft_entry__.build()
+update_image frame), examples/multi_gpu_frame (och::gpu::frame_group, one
+process over every GPU, RCCL all-gather) and examples/sharded_frame (one
+process per GPU: the RCCL id handed over through a file, the gather to the
+display rank, och_gpu_render_sharded_steps_dev) are built by __graft_entry__.build()
 against include/och_gpu.hpp, run as programs, and their PPM frames and pick
 ray are compared with the oracle."""
 import re
@@ -17,7 +19,7 @@ ORIGIN = np.array([1.5, 1.5, 1.5], np.float32)
 
 
 def _ensure_examples():
-    if not (EX / "render_frame").exists() or not (EX / "multi_gpu_frame").exists():
+    if not all((EX / x).exists() for x in ("render_frame", "multi_gpu_frame", "sharded_frame")):
         subprocess.run(["make", "-s", "-C", str(EX)], check=True)
 
 
@@ -77,6 +79,26 @@ def test_multi_gpu_frame_example(ort, O, gpu_device, tmp_path):
         assert r.returncode == 0, r.stderr
         tree = ort.build_terrain(depth)
         pool = O.OraclePool(tree.nodes, tree.root, depth, 1)
+        ref = O.trace_batch(pool, O.Rcp(None), ORIGIN, O.raygen(0.3, pitch, 1.25, W, H), nthreads=16)
+        want = rgb_of(O.shade_fast(ref["dir"], ref["voxel"], ort.VoxelData().get_colours())).reshape(H, W, 3)
+        assert np.array_equal(read_ppm(out), want), view
+
+
+@pytest.mark.gpu
+def test_sharded_frame_example(ort, O, gpu_device, tmp_path):
+    """One rank (a one-GPU box): the RCCL id through the file, the gather's
+    ncclSend / ncclRecv group, the display rank's shade -- the frames of
+    och_gpu_render_sharded_steps_dev against the oracle's."""
+    _ensure_examples()
+    depth, W, H = 10, 800, 450
+    tree = ort.build_terrain(depth)
+    pool = O.OraclePool(tree.nodes, tree.root, depth, 1)
+    for view, pitch in ((0, 0.0), (1, -0.6)):
+        out = tmp_path / f"sh{view}.ppm"
+        r = subprocess.run([str(EX / "sharded_frame"), str(depth), str(W), str(H), str(out), "0", "1",
+                            str(tmp_path / f"id{view}"), "4", str(view)], capture_output=True, text=True, timeout=110)
+        assert r.returncode == 0, r.stderr
+        assert "rank 0 of 1" in r.stdout
         ref = O.trace_batch(pool, O.Rcp(None), ORIGIN, O.raygen(0.3, pitch, 1.25, W, H), nthreads=16)
         want = rgb_of(O.shade_fast(ref["dir"], ref["voxel"], ort.VoxelData().get_colours())).reshape(H, W, 3)
         assert np.array_equal(read_ppm(out), want), view
