@@ -183,13 +183,21 @@ typedef enum och_option {
     OCH_OPT_PLAN = 11,         /* shape of och_gpu_plan_views' launch order (set before planning): 0 =
                                   costliest first; P in 1..99 = the costliest P % first, the rest in natural
                                   order (default 10); 100 = costliest and cheapest alternating */
-    OCH_OPT_SKIP = 12          /* 1 = per-node voxel-box skip: a walk that descends into a node whose
+    OCH_OPT_SKIP = 12,         /* 1 = per-node voxel-box skip: a walk that descends into a node whose
                                   voxels' bounding box (precomputed per child slot of the packed layout, built
                                   when the option is first set, 2 B per slot) it provably never enters steps
                                   out of it at once, as the cull ends a ray missing every voxel's box; exact
                                   (DESIGN.md §4c), for launches that do not count PUSHes; 2 = counting
                                   launches too (diagnostic); 0 (default) = off: the skip walks 25-40 % fewer
                                   PUSHes yet runs 13-19 % slower on every scene measured */
+    OCH_OPT_COLUMNS = 13       /* column cull, a refinement of OCH_OPT_CULL (render / trace grid launches;
+                                  counting launches at OCH_OPT_CULL = 2 only): L (1..7) = levels of a
+                                  quadtree over the world's x-y columns holding each block's voxel z range
+                                  (built when set); a wave whose every ray provably enters no block that
+                                  holds a voxel ends those rays as the MISS without walking (exact,
+                                  DESIGN.md §4d); 0 (default) = off: the wave's walk of the quadtree costs
+                                  more than the walks it saves on the bench's views (24.7 G against 32.4 G
+                                  rays/s at L = 6) */
 } och_option;
 OCH_API int och_gpu_set_option(och_gpu_pool *pool, int option, int value);
 OCH_API int och_gpu_get_option(const och_gpu_pool *pool, int option, int *value);
@@ -494,6 +502,15 @@ OCH_API int och_pool_pack(const uint32_t *nodes, uint32_t n_nodes, uint32_t root
  * n_nodes * 8 entries.  OCH_E_INVALID above depth 20. */
 OCH_API int och_pool_slot_boxes(const uint32_t *packed, uint32_t n_nodes, uint32_t packed_root, int depth,
                                 uint16_t *out);
+/* The column cull's quadtree (OCH_OPT_COLUMNS) of a packed pool: levels
+ * 1..levels, level l holding 2^l x 2^l blocks of the world's x-y columns in
+ * Morton order (x in the even bits) from word (4^l - 4) / 3; each word the z
+ * range of the voxels in that block column, zlo | zmax << 16 in voxel units
+ * (inclusive), or 0xFFFF when it holds none.  out holds (4^(levels+1) - 4) / 3
+ * words.  OCH_E_INVALID for levels outside 1..min(7, depth - 1) or depth above
+ * 16. */
+OCH_API int och_pool_columns(const uint32_t *packed, uint32_t n_nodes, uint32_t packed_root, int depth, int levels,
+                             uint32_t *out);
 /* Bounding box of every non-empty leaf voxel reachable from root, in voxel
  * units: voxel (x, y, z) lies in it iff lo <= (x, y, z) < hi per axis.
  * Returns OCH_OK with lo = hi = {0, 0, 0} for a pool without voxels. */

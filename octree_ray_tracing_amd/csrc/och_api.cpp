@@ -147,6 +147,8 @@ struct och_gpu_pool {
     // packed layout (see och_internal.h DevPool)
     uint32_t *d_packed = nullptr;
     uint16_t *d_boxes = nullptr;    // per packed slot: the child's voxel box (och::pool_slot_boxes), or none
+    uint32_t *d_columns = nullptr;  // the column quadtree (och::pool_columns), or none
+    int col_levels = 0;             // its levels
     uint32_t packed_root = 0;
     uint32_t packed_nodes = 0;
     uint32_t packed_top_ids[5] = {1, 1, 1, 1, 1};   // first id past levels 1..T
@@ -162,6 +164,7 @@ struct och_gpu_pool {
     int opt_timing = 1;                        // OCH_OPT_TIMING
     int opt_plan = 10;                         // OCH_OPT_PLAN (shape of och_gpu_plan_views' order)
     int opt_skip = 0;                          // OCH_OPT_SKIP (per-node voxel-box skip; boxes built on first use)
+    int opt_columns = 0;                       // OCH_OPT_COLUMNS (column cull: quadtree levels, 0 = off)
     hipEvent_t next_ev_start = nullptr;        // och_gpu_set_launch_events: the next launch's events
     hipEvent_t next_ev_stop = nullptr;
     // bounding box of the pool's voxels (voxel units, [lo, hi)), for the cull
@@ -245,6 +248,11 @@ struct och_gpu_pool {
         // aim it at the node array, which spans more than 16 B per node, and
         // skip = 0 keeps every ray's skipmask 0
         p.box_base = p.boxes ? p.boxes : reinterpret_cast<const uint16_t *>(p.nodes);
+        // the column quadtree describes the voxels of the pool it was built
+        // from (upload_packed); an editor's writes since make it stale
+        const bool cols = p.cull && d_columns && d_packed && !packed_by_slot && !torn;
+        p.columns = cols ? d_columns : nullptr;
+        p.col_levels = cols ? col_levels : 0;
         for (int a = 0; a < 3; ++a) {
             p.cull_lo[a] = 1.0F + std::ldexp((float)box_lo[a], -depth);
             p.cull_hi[a] = 1.0F + std::ldexp((float)box_hi[a], -depth);
@@ -454,16 +462,13 @@ bool pack_pool(const uint32_t *nodes, uint32_t n_nodes, uint32_t root, int depth
 
 }  // namespace
 
-// Per-slot voxel boxes of a packed pool (the per-node skip, och_internal.h
-// DevPool::boxes): for every interior slot holding child C, the bounding box
-// of the voxels under C in C's own cell, world orientation, quantised
-// outwards to quarters on x and y and sixteenths on z.
-bool och::pool_slot_boxes(const uint32_t *packed, uint32_t n_nodes, uint32_t packed_root, int depth,
-                          std::vector<uint16_t> &out)
+bool och::pool_node_boxes(const uint32_t *packed, uint32_t n_nodes, uint32_t packed_root, int depth,
+                          std::vector<uint8_t> &level, std::vector<int32_t> &box)
 {
-    if (depth < 2 || depth > kSkipMaxDepth || n_nodes < 2) return false;
+    if (depth < 2 || depth > 24 || n_nodes < 2) return false;
     const uint32_t root = packed_root & kIdLimitMask;
-    std::vector<uint8_t> level(n_nodes, 0);
+    if (root == 0 || root >= n_nodes) return false;
+    level.assign(n_nodes, 0);
     level[root] = 1;
     // breadth-first ids: a parent's id is below its children's
     for (uint32_t v = 1; v < n_nodes; ++v) {
@@ -477,7 +482,7 @@ bool och::pool_slot_boxes(const uint32_t *packed, uint32_t n_nodes, uint32_t pac
         }
     }
     // voxel units relative to the node's corner: [lo, hi) per axis
-    std::vector<int32_t> box((size_t)n_nodes * 6, 0);
+    box.assign((size_t)n_nodes * 6, 0);
     for (uint32_t v = n_nodes - 1; v >= 1; --v) {
         if (!level[v]) continue;
         int32_t *b = &box[(size_t)v * 6];
@@ -496,6 +501,20 @@ bool och::pool_slot_boxes(const uint32_t *packed, uint32_t n_nodes, uint32_t pac
             }
         }
     }
+    return true;
+}
+
+// Per-slot voxel boxes of a packed pool (the per-node skip, och_internal.h
+// DevPool::boxes): for every interior slot holding child C, the bounding box
+// of the voxels under C in C's own cell, world orientation, quantised
+// outwards to quarters on x and y and sixteenths on z.
+bool och::pool_slot_boxes(const uint32_t *packed, uint32_t n_nodes, uint32_t packed_root, int depth,
+                          std::vector<uint16_t> &out)
+{
+    if (depth > kSkipMaxDepth) return false;
+    std::vector<uint8_t> level;
+    std::vector<int32_t> box;
+    if (!pool_node_boxes(packed, n_nodes, packed_root, depth, level, box)) return false;
     out.assign((size_t)n_nodes * 8, 0);
     for (uint32_t v = 1; v < n_nodes; ++v) {
         if (!level[v] || level[v] >= depth) continue;
@@ -521,6 +540,67 @@ bool och::pool_slot_boxes(const uint32_t *packed, uint32_t n_nodes, uint32_t pac
     return true;
 }
 
+// The column quadtree (DevPool::columns): for every block of 2^(depth - levels)
+// x 2^(depth - levels) voxel columns, the z range of its voxels, from the
+// exact node boxes of the tree's nodes at level levels + 1 (their cells are
+// the block's cubes), then each coarser level as the union of its 4 blocks.
+bool och::pool_columns(const uint32_t *packed, uint32_t n_nodes, uint32_t packed_root, int depth, int levels,
+                       std::vector<uint32_t> &out)
+{
+    if (levels < 1 || levels > kColumnMaxLevels || levels > depth - 1 || depth > kColumnMaxDepth) return false;
+    std::vector<uint8_t> level;
+    std::vector<int32_t> box;
+    if (!pool_node_boxes(packed, n_nodes, packed_root, depth, level, box)) return false;
+    const uint32_t G = 1u << levels;
+    std::vector<int32_t> lo(G * G, INT32_MAX), hi(G * G, INT32_MIN);     // [lo, hi) per block column
+    const int32_t cube = 1 << (depth - levels);                           // a level-(levels + 1) node's cell
+    struct Item {
+        uint32_t v;
+        int L;
+        uint32_t x, y, z;
+    };
+    std::vector<Item> todo{{packed_root & kIdLimitMask, 1, 0, 0, 0}};
+    while (!todo.empty()) {
+        const Item it = todo.back();
+        todo.pop_back();
+        const int32_t *b = &box[(size_t)it.v * 6];
+        if (b[2] > b[5]) continue;                                        // no voxel under this node
+        if (it.L == levels + 1) {
+            const uint32_t c = it.y * G + it.x;
+            lo[c] = std::min(lo[c], (int32_t)it.z * cube + b[2]);
+            hi[c] = std::max(hi[c], (int32_t)it.z * cube + b[5]);
+            continue;
+        }
+        for (int k = 0; k < 8; ++k) {
+            const uint32_t w = packed[(size_t)it.v * 8 + k];
+            if (w) todo.push_back({w & kIdLimitMask, it.L + 1, 2 * it.x + (k & 1), 2 * it.y + ((k >> 1) & 1),
+                                   2 * it.z + ((k >> 2) & 1)});
+        }
+    }
+    auto morton = [](uint32_t x, uint32_t y) {
+        uint32_t m = 0;
+        for (int i = 0; i < kColumnMaxLevels; ++i) m |= ((x >> i) & 1u) << (2 * i) | ((y >> i) & 1u) << (2 * i + 1);
+        return m;
+    };
+    auto word = [](int32_t l, int32_t h) { return l < h ? (uint32_t)l | (uint32_t)(h - 1) << 16 : 0xFFFFu; };
+    auto off = [](int l) { return ((size_t(1) << (2 * l)) - 4) / 3; };
+    out.assign(off(levels + 1), 0xFFFFu);
+    for (uint32_t y = 0; y < G; ++y)
+        for (uint32_t x = 0; x < G; ++x) out[off(levels) + morton(x, y)] = word(lo[y * G + x], hi[y * G + x]);
+    for (int l = levels - 1; l >= 1; --l)
+        for (size_t m = 0; m < (size_t(1) << (2 * l)); ++m) {
+            int32_t zl = INT32_MAX, zh = INT32_MIN;
+            for (int k = 0; k < 4; ++k) {
+                const uint32_t w = out[off(l + 1) + 4 * m + k];
+                if ((w & 0xFFFFu) > (w >> 16)) continue;                  // empty
+                zl = std::min(zl, (int32_t)(w & 0xFFFFu));
+                zh = std::max(zh, (int32_t)(w >> 16) + 1);
+            }
+            out[off(l) + m] = word(zl, zh);
+        }
+    return true;
+}
+
 namespace {
 
 // The per-node skip's boxes (OCH_OPT_SKIP) of the packed pool, built when the
@@ -543,14 +623,41 @@ int ensure_boxes(och_gpu_pool *p)
     return upload_boxes(p, packed);
 }
 
+// The column quadtree (OCH_OPT_COLUMNS levels) of the packed pool.
+int upload_columns(och_gpu_pool *p, const std::vector<uint32_t> &packed)
+{
+    if (p->d_columns) OCH_HIP(hipFree(p->d_columns));
+    p->d_columns = nullptr;
+    p->col_levels = 0;
+    const int levels = std::min(p->opt_columns, p->depth - 1);
+    std::vector<uint32_t> cols;
+    if (levels < 1 || !och::pool_columns(packed.data(), p->packed_nodes, p->packed_root, p->depth, levels, cols))
+        return OCH_OK;
+    OCH_HIP(hipMalloc(&p->d_columns, cols.size() * 4));
+    OCH_HIP(hipMemcpy(p->d_columns, cols.data(), cols.size() * 4, hipMemcpyHostToDevice));
+    p->col_levels = levels;
+    return OCH_OK;
+}
+
+int ensure_columns(och_gpu_pool *p)
+{
+    if (!p->d_packed || p->packed_by_slot) return OCH_OK;
+    std::vector<uint32_t> packed((size_t)p->packed_nodes * 8);
+    OCH_HIP(hipMemcpy(packed.data(), p->d_packed, packed.size() * 4, hipMemcpyDeviceToHost));
+    return upload_columns(p, packed);
+}
+
 int upload_packed(och_gpu_pool *p, const uint32_t *nodes, uint32_t n_nodes)
 {
     std::vector<uint32_t> packed;
     uint32_t proot = 0;
     if (p->d_packed) OCH_HIP(hipFree(p->d_packed));
     if (p->d_boxes) OCH_HIP(hipFree(p->d_boxes));
+    if (p->d_columns) OCH_HIP(hipFree(p->d_columns));
     p->d_packed = nullptr;
     p->d_boxes = nullptr;
+    p->d_columns = nullptr;
+    p->col_levels = 0;
     p->packed_nodes = 0;
     p->packed_by_slot = false;
     if (!pack_pool(nodes, n_nodes, p->root, p->depth, p->index_base, packed, proot, p->packed_top_ids))
@@ -559,6 +666,8 @@ int upload_packed(och_gpu_pool *p, const uint32_t *nodes, uint32_t n_nodes)
     OCH_HIP(hipMemcpy(p->d_packed, packed.data(), packed.size() * 4, hipMemcpyHostToDevice));
     p->packed_root = proot;
     p->packed_nodes = (uint32_t)(packed.size() / 8);
+    if (p->opt_columns)
+        if (int st = upload_columns(p, packed)) return st;
     return p->opt_skip ? upload_boxes(p, packed) : OCH_OK;
 }
 
@@ -714,6 +823,7 @@ OCH_API int och_gpu_pool_destroy(och_gpu_pool *p)
     if (p->d_nodes) (void)hipFree(p->d_nodes);
     if (p->d_packed) (void)hipFree(p->d_packed);
     if (p->d_boxes) (void)hipFree(p->d_boxes);
+    if (p->d_columns) (void)hipFree(p->d_columns);
     if (p->d_lut) (void)hipFree(p->d_lut);
     if (p->d_palette) (void)hipFree(p->d_palette);
     if (p->d_code_table) (void)hipFree(p->d_code_table);
@@ -1020,6 +1130,15 @@ OCH_API int och_gpu_set_option(och_gpu_pool *p, int option, int value)
         if (value < 0 || value > 100) return fail(OCH_E_INVALID, "plan shape must be 0..100");
         p->opt_plan = value;
         return OCH_OK;
+    case OCH_OPT_COLUMNS:
+        if (value < 0 || value > och::kColumnMaxLevels)
+            return fail(OCH_E_INVALID, "columns must be 0..%d quadtree levels", och::kColumnMaxLevels);
+        if (value != p->opt_columns) {
+            DeviceGuard g(p->device);
+            p->opt_columns = value;
+            return ensure_columns(p);
+        }
+        return OCH_OK;
     case OCH_OPT_SKIP:
         if (value < 0 || value > 2) return fail(OCH_E_INVALID, "skip must be 0, 1 or 2");
         p->opt_skip = value;
@@ -1050,6 +1169,7 @@ OCH_API int och_gpu_get_option(const och_gpu_pool *p, int option, int *value)
     case OCH_OPT_TIMING: *value = p->opt_timing; return OCH_OK;
     case OCH_OPT_PLAN: *value = p->opt_plan; return OCH_OK;
     case OCH_OPT_SKIP: *value = p->opt_skip; return OCH_OK;
+    case OCH_OPT_COLUMNS: *value = p->opt_columns; return OCH_OK;
     default: return fail(OCH_E_INVALID, "unknown option %d", option);
     }
 }
@@ -1898,6 +2018,17 @@ OCH_API int och_pool_slot_boxes(const uint32_t *packed, uint32_t n_nodes, uint32
         return fail(OCH_E_INVALID, "no slot boxes for this pool (depth %d above %d, or not a breadth-first packed pool)",
                     depth, och::kSkipMaxDepth);
     std::memcpy(out, boxes.data(), boxes.size() * 2);
+    return OCH_OK;
+}
+
+OCH_API int och_pool_columns(const uint32_t *packed, uint32_t n_nodes, uint32_t packed_root, int depth, int levels,
+                             uint32_t *out)
+{
+    if (!packed || !out || n_nodes < 2) return fail(OCH_E_INVALID, "bad column arguments");
+    std::vector<uint32_t> cols;
+    if (!och::pool_columns(packed, n_nodes, packed_root, depth, levels, cols))
+        return fail(OCH_E_INVALID, "no column quadtree of %d levels for this pool (depth %d)", levels, depth);
+    std::memcpy(out, cols.data(), cols.size() * 4);
     return OCH_OK;
 }
 

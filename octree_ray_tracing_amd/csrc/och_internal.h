@@ -46,6 +46,13 @@ struct DevPool {
     const uint16_t *boxes;
     int32_t skip;
     const uint16_t *box_base;   // boxes, or the node array when there are none (the load's address)
+    // Column cull (OCH_OPT_COLUMNS; och_kernels.hip column_cull_wave): a
+    // quadtree over the world's x-y columns, levels 1..col_levels (2^l x 2^l
+    // blocks at level l, Morton order, level l at (4^l - 1) / 3 - 1 words from
+    // the start), each word the z range of the voxels in that block column,
+    // zlo | zmax << 16 in voxel units (zlo > zmax: none); null when off.
+    const uint32_t *columns;
+    int32_t col_levels;
 };
 
 // Per-slot voxel boxes (DevPool::boxes): x and y in quarters of the child's
@@ -57,6 +64,20 @@ constexpr int kSkipMaxDepth = 20;
 constexpr uint16_t kSkipEmptyBox = 0xFFFF;
 bool pool_slot_boxes(const uint32_t *packed, uint32_t n_nodes, uint32_t packed_root, int depth,
                      std::vector<uint16_t> &out);
+
+// Exact voxel boxes of every node of a packed pool (the bottom-up pass both
+// the skip's slot boxes and the column quadtree start from): level[v] (1 =
+// root, 0 = unreachable) and box[6 v ..] = lo x, y, z, hi x, y, z in voxel
+// units relative to the node's corner, [lo, hi) (lo > hi: no voxel).
+bool pool_node_boxes(const uint32_t *packed, uint32_t n_nodes, uint32_t packed_root, int depth,
+                     std::vector<uint8_t> &level, std::vector<int32_t> &box);
+
+// The column quadtree (DevPool::columns) of a packed pool, levels 1..levels
+// (levels <= depth - 1, depth <= kColumnMaxDepth); false when it has none.
+constexpr int kColumnMaxDepth = 16;
+constexpr int kColumnMaxLevels = 7;
+bool pool_columns(const uint32_t *packed, uint32_t n_nodes, uint32_t packed_root, int depth, int levels,
+                  std::vector<uint32_t> &out);
 
 // Largest RCPPS-table relative error for which camera_proven_miss is sound
 // (och_kernels.hip has the budget: per-axis factors within 2^-9 of 1 against

@@ -215,6 +215,92 @@ __device__ __forceinline__ bool ray_cull(const Ray &r, const DevPool &P, const f
     return ok && (enter > leave || leave < 0.0F);
 }
 
+// Column cull (OCH_OPT_COLUMNS; DESIGN.md §4d has the proof): the cull's
+// test for a box B applies to any box that holds the voxels a ray could hit,
+// so a ray that fails it for every block of a partition of the voxels into
+// boxes enters no voxel cell and ends in the MISS the walk would reach.  The
+// blocks are the columns of a quadtree over the world's x-y extent
+// (DevPool::columns: a block's box is its x-y square times the z range of the
+// voxels above it).  The wave walks the quadtree once, uniformly: a block no
+// lane can enter is pruned with everything below it; a leaf block some lane
+// can enter ends the test, and the whole wave walks as before.  Otherwise
+// every lane failed every block on each path to every leaf holding voxels,
+// and the whole wave's rays are proven misses.  Children are visited nearest
+// the camera first (the first lane's direction signs), so a wave that will
+// walk finds its entered leaf early.
+__device__ __forceinline__ bool column_box_entered(const Ray &r, const float lo[3], const float hi[3])
+{
+    float enter = -INFINITY, leave = INFINITY;
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        const float k = (r.inv >> a) & 1u ? 3.0F : 0.0F;        // the reflected frame, as ray_cull
+        const float t1 = __builtin_fmaf(fabsf(__fsub_rn(k, lo[a])), r.c[a], r.b[a]);
+        const float t2 = __builtin_fmaf(fabsf(__fsub_rn(k, hi[a])), r.c[a], r.b[a]);
+        enter = fmaxf(enter, fminf(t1, t2));
+        leave = fminf(leave, fmaxf(t1, t2));
+    }
+    return !(enter > leave || leave < 0.0F);
+}
+
+// OCH_COL_DZ (experiment, measured: no gain): only waves whose
+// first ray dips less than this (d_z > -OCH_COL_DZ) try the column cull.
+__device__ __forceinline__ bool col_try(const float *d)
+{
+#ifdef OCH_COL_DZ
+    return __builtin_amdgcn_readfirstlane(d[2] > -(float)OCH_COL_DZ ? 1u : 0u) != 0u;
+#else
+    (void)d;
+    return true;
+#endif
+}
+
+__device__ __forceinline__ bool column_cull_wave(const Ray &r, const DevPool &P, const float *o)
+{
+    bool ok = true;                                              // ray_cull's preconditions
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        ok &= ((fbits(r.c[a]) >> 23) & 0xFFu) - 1u < 251u;
+        ok &= o[a] > 1.0F && o[a] < 2.0F;
+    }
+    if (__ballot(!ok)) return false;
+    const uint32_t levels = (uint32_t)P.col_levels;
+    const uint32_t flip = __builtin_amdgcn_readfirstlane(~r.inv & 3u);   // x bit 0, y bit 1: near half first
+    const float vox = ffrom((uint32_t)(127 - P.depth) << 23);             // 2^-depth
+    uint32_t l = 1, m = 0;                                      // level and visit index, wave-uniform
+    while (l != 0) {
+        const uint32_t code = m ^ (flip * (((1u << (2 * l)) - 1u) / 3u));  // the flip in every digit
+        // a uniform word: a scalar load (the compiler's own would be a vector
+        // load, as the kernel writes other memory), read-only
+        uint32_t w;
+        asm volatile("s_load_dword %0, %1, %2\n\ts_waitcnt lgkmcnt(0)"
+                     : "=s"(w)
+                     : "s"(P.columns), "s"((((1u << (2 * l)) - 4u) / 3u + code) * 4u)
+                     : "memory");
+        if ((w & 0xFFFFu) <= (w >> 16)) {                       // the block holds voxels
+            uint32_t bx = 0, by = 0;
+            for (uint32_t i = 0; i < l; ++i) {
+                bx |= ((code >> (2 * i)) & 1u) << i;
+                by |= ((code >> (2 * i + 1)) & 1u) << i;
+            }
+            const float size = ffrom((127u - l) << 23);          // 2^-l: every corner below is exact
+            const float lo[3] = {1.0F + (float)bx * size, 1.0F + (float)by * size, 1.0F + (float)(w & 0xFFFFu) * vox};
+            const float hi[3] = {lo[0] + size, lo[1] + size, 1.0F + (float)((w >> 16) + 1u) * vox};
+            if (__ballot(column_box_entered(r, lo, hi))) {
+                if (l == levels) return false;                  // a lane may enter a leaf block: walk
+                ++l;
+                m <<= 2;
+                continue;
+            }
+        }
+        ++m;                                                    // next sibling, up when the four are done
+        while (l != 0 && (m & 3u) == 0) {
+            --l;
+            m >>= 2;
+        }
+    }
+    return true;
+}
+
 // Setup, ORT/och_h_octree.h:294-338, then the first PUSH at the root.
 // stack: this lane's LDS column, depth + 1 slots `stride` words apart.
 // kCull: a ray that ray_cull proves a miss ends here (ray_active false,
@@ -222,15 +308,18 @@ __device__ __forceinline__ bool ray_cull(const Ray &r, const DevPool &P, const f
 // before iterating.  Launches that count PUSHes cull only at OCH_OPT_CULL = 2
 // (a diagnostic: how many PUSHes the culled launch walks), so their counts
 // stay the reference's.
-template <bool kCount, bool kCull>
+template <bool kCount, bool kCull, bool kColumns = false>
 __device__ __forceinline__ bool ray_setup(Ray &r, const DevPool &P, const float *o, const float *d, uint32_t *stack,
                                           uint32_t stride);
 
-template <int kPacked, bool kCount, bool kCull = false, bool kAsm = false>
+// kColumns: the column cull after the occupied-box cull (primary-ray grid
+// launches; column_cull_wave), under the cull's option: launches that count
+// PUSHes only at OCH_OPT_CULL = 2, the diagnostic.
+template <int kPacked, bool kCount, bool kCull = false, bool kAsm = false, bool kColumns = false>
 __device__ __forceinline__ void ray_init(Ray &r, const DevPool &P, const float *o, const float *d, uint32_t *stack,
                                          uint32_t stride)
 {
-    if (!ray_setup<kCount, kCull>(r, P, o, d, stack, stride)) return;
+    if (!ray_setup<kCount, kCull, kColumns>(r, P, o, d, stack, stride)) return;
     if (kPacked && OCH_MERGED_DESCEND)
         ray_push_descend<kCount, kAsm, kPacked == kPackedSkip>(r, P, stride);
     else
@@ -239,7 +328,7 @@ __device__ __forceinline__ void ray_init(Ray &r, const DevPool &P, const float *
 
 // ray_init's setup (:294-338) up to, not including, the root PUSH.  false:
 // the ray is culled (recorded as the MISS, 0 PUSHes, ray_active false).
-template <bool kCount, bool kCull>
+template <bool kCount, bool kCull, bool kColumns>
 __device__ __forceinline__ bool ray_setup(Ray &r, const DevPool &P, const float *o, const float *d, uint32_t *stack,
                                           uint32_t stride)
 {
@@ -289,7 +378,8 @@ __device__ __forceinline__ bool ray_setup(Ray &r, const DevPool &P, const float 
         exact &= o[a] > 1.0F && o[a] < 2.0F;
     }
     r.skipmask = exact && P.boxes && skip_on(P, kCount) ? 0xFFFFu : 0u;
-    if (kCull && (kCount ? P.cull == 2 : P.cull != 0) && ray_cull(r, P, o)) {
+    if (kCull && (kCount ? P.cull == 2 : P.cull != 0) &&
+        (ray_cull(r, P, o) || (kColumns && P.columns && col_try(d) && column_cull_wave(r, P, o)))) {
         r.dim = 1u << 23;                                                   // finished: the MISS
         set_mode(r, kStepping);
         if (!OCH_DIM_LEVEL) r.level = 0;
@@ -1391,7 +1481,7 @@ __global__ void k_trace_grid(DevPool P, Src S, Sink K, uint32_t xcd_group, const
             K.put(out, Hit{OCH_EXIT, 0u, P.miss_bits, 0u});
         } else {
             Ray r;
-            ray_init<kPacked, kCount, true, kAsmLoad>(r, P, o, d, lds_stack + threadIdx.x, blockDim.x);
+            ray_init<kPacked, kCount, true, kAsmLoad, true>(r, P, o, d, lds_stack + threadIdx.x, blockDim.x);
             ray_run<kPacked, kCount, kAsmLoad>(r, P, blockDim.x, top);
             K.put(out, ray_result<kPacked, kAsmLoad>(r, P));
         }

@@ -169,7 +169,7 @@ class GpuPool:
 
     OPTIONS = {"schedule": 0, "block": 1, "waves_per_cu": 2, "refill": 3, "layout": 4, "tile_order": 5,
                "bounce_compact": 6, "chunk_tiles": 7, "cull": 8, "merge": 9, "timing": 10, "plan": 11,
-               "skip": 12}
+               "skip": 12, "columns": 13}
 
     def set_option(self, name: str, value: int):
         """Launch options (och_gpu_set_option): schedule (0 grid / 1 persistent / 2 grid with lane
