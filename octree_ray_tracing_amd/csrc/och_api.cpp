@@ -642,6 +642,8 @@ int upload_columns(och_gpu_pool *p, const std::vector<uint32_t> &packed)
 int ensure_columns(och_gpu_pool *p)
 {
     if (!p->d_packed || p->packed_by_slot) return OCH_OK;
+    // launches in flight on any stream may still read the quadtree being replaced
+    if (p->d_columns) OCH_HIP(hipDeviceSynchronize());
     std::vector<uint32_t> packed((size_t)p->packed_nodes * 8);
     OCH_HIP(hipMemcpy(packed.data(), p->d_packed, packed.size() * 4, hipMemcpyDeviceToHost));
     return upload_columns(p, packed);
