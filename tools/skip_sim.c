@@ -12,7 +12,9 @@
  * the same t), so records are unchanged.  This walks the bench's camera
  * frames over the packed depth-12 DAG twice -- the reference walk and the
  * walk with the skip -- checks every record is identical, and reports the
- * PUSHes (and the costliest 8x8 tiles, which set a frame's latency).
+ * PUSHes (and the costliest 8x8 tiles, which set a frame's latency), and the
+ * descents (PUSHes that find their child: one dependent load each) with each
+ * tile's lockstep maximum -- what a wave costs.
  *
  * Input: packed nodes (och_pool_pack, n x 8 u32, row 0 padding), node levels
  * (u8 per row) and per-node boxes (6 x u8 per row: lo x,y,z then hi x,y,z in
@@ -36,7 +38,7 @@ static const uint8_t *LV, *BX;
 static int DEPTH, Q, MINLV;
 static uint32_t ROOT;
 
-typedef struct { int dir; uint32_t voxel; uint32_t t; int push; } Rec;
+typedef struct { int dir; uint32_t voxel; uint32_t t; int push; int desc; int skips; } Rec;
 
 /* ORT/och_h_octree.h:292-447 over the packed pool (child id in the low 24 bits),
  * host RCPPS; skip = 1: a present child whose voxel box the ray provably
@@ -62,7 +64,7 @@ static Rec trace(const float *o, const float *d, int skip)
     uint32_t dim = 1u << 22, stack[32], node = ROOT;
     int sp = 0, level = 1, axis = 8;
     float tmin = 0.0F;
-    Rec r = {0, 0, 0, 0};
+    Rec r = {0, 0, 0, 0, 0, 0};
     enum { PUSH, STEP, POP } st = PUSH;
     for (;;) {
         if (st == PUSH) {
@@ -82,9 +84,10 @@ static Rec trace(const float *o, const float *d, int skip)
                     enter = fmaxf(enter, thi);
                     leave = fminf(leave, tlo);
                 }
-                if (enter > leave || leave < tmin) child = 0;
+                if (enter > leave || leave < tmin) { child = 0; ++r.skips; }
             }
             if (!child) { st = STEP; continue; }
+            ++r.desc;                      /* a descent or the HIT: one dependent load */
             if (level++ == DEPTH) {
                 r.voxel = child;
                 r.dir = (axis >> 1) + 3 * ((inv & axis) == 0);
@@ -141,6 +144,7 @@ static void camera(float yaw, float pitch, int W, int H, int col, int row, float
 static float PITCH;
 enum { W = 1920, H = 1080, TX = W / 8, TY = H / 8, NT = 16 };
 static long tile_push[2][TX * TY];
+static long tile_desc_max[3][TX * TY], tile_push_max[2][TX * TY], desc_sum[3][NT];
 static long mism[NT], hits[NT];
 
 static uint64_t lcg(uint64_t *s) { *s = *s * 6364136223846793005ull + 1442695040888963407ull; return *s >> 33; }
@@ -164,6 +168,17 @@ static void *worker(void *arg)
             const Rec a = trace(o, d, 0), b = trace(o, d, 1);
             tile_push[0][t] += a.push;
             tile_push[1][t] += b.push;
+            /* the lockstep cost of the tile's wave: its longest lane */
+            if (a.desc > tile_desc_max[0][t]) tile_desc_max[0][t] = a.desc;
+            if (b.desc > tile_desc_max[1][t]) tile_desc_max[1][t] = b.desc;
+            if (a.push > tile_push_max[0][t]) tile_push_max[0][t] = a.push;
+            if (b.push > tile_push_max[1][t]) tile_push_max[1][t] = b.push;
+            desc_sum[0][id] += a.desc;
+            desc_sum[1][id] += b.desc;
+            /* the GPU's skip tests a child's box after descending into it: each
+               skipped child still costs its descent */
+            if (b.desc + b.skips > tile_desc_max[2][t]) tile_desc_max[2][t] = b.desc + b.skips;
+            desc_sum[2][id] += b.desc + b.skips;
             mism[id] += a.dir != b.dir || a.voxel != b.voxel || a.t != b.t;
             hits[id] += a.dir < 6;
         }
@@ -208,6 +223,17 @@ int main(int argc, char **argv)
     long tot[2] = {0, 0}, mm = 0, hh = 0;
     for (int t = 0; t < TX * TY; ++t) { tot[0] += tile_push[0][t]; tot[1] += tile_push[1][t]; }
     for (int i = 0; i < NT; ++i) { mm += mism[i]; hh += hits[i]; }
+    long dm[3] = {0, 0, 0}, pm[2] = {0, 0}, ds[3] = {0, 0, 0};
+    for (int t = 0; t < TX * TY; ++t) {
+        for (int k = 0; k < 3; ++k) dm[k] += tile_desc_max[k][t];
+        for (int k = 0; k < 2; ++k) pm[k] += tile_push_max[k][t];
+    }
+    for (int i = 0; i < NT; ++i)
+        for (int k = 0; k < 3; ++k) ds[k] += desc_sum[k][i];
+    printf("{\"pitch\": %.2f, \"descents_per_ray\": [%.3f, %.3f, %.3f], \"sum_tile_max_descents\": [%ld, %ld, %ld], "
+           "\"sum_tile_max_push\": [%ld, %ld]}   (reference, skip tested before the descent, skip after it)\n",
+           PITCH, ds[0] / (double)(W * H), ds[1] / (double)(W * H), ds[2] / (double)(W * H), dm[0], dm[1], dm[2],
+           pm[0], pm[1]);
     qsort(tile_push[0], TX * TY, sizeof(long), cmp_desc);
     qsort(tile_push[1], TX * TY, sizeof(long), cmp_desc);
     printf("{\"pitch\": %.2f, \"Q\": %d, \"min_level\": %d, \"rays\": %d, \"hits\": %ld, \"mismatches\": %ld, "
