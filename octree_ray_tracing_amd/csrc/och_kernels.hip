@@ -130,6 +130,25 @@ __host__ __device__ __forceinline__ bool skip_on(const DevPool &P, bool count)
 constexpr int kPackedSkip = 2;
 
 constexpr uint32_t kIdMask = 0x00FFFFFFu;
+#ifndef OCH_POP_SELECT
+#define OCH_POP_SELECT 1
+#endif
+#ifndef OCH_MAD24
+#define OCH_MAD24 1
+#endif
+// Byte offset of child slot c24 - 24 of the node whose slot word is w, from
+// the node pool's base plus 96: (id * 8 + c24) * 4, id = w's low 24 bits.  One
+// v_mad_u32_u24 and a shift (the compiler turns the mul24 by 8 into a shift
+// and a mask, one VALU more per descent).
+__device__ __forceinline__ uint32_t slot_offset(uint32_t w, uint32_t c24)
+{
+    if (OCH_MAD24) {
+        uint32_t t;
+        asm("v_mad_u32_u24 %0, %1, 8, %2" : "=v"(t) : "v"(w), "v"(c24));
+        return t << 2;
+    }
+    return ((w & kIdMask) << 5) + (c24 << 2);
+}
 
 // The PUSH test and slot fetch (ORT/och_h_octree.h:342-344): the packed
 // layout tests presence with the child mask held in the node's slot word and
@@ -464,9 +483,21 @@ __device__ __forceinline__ void ray_phase_step(Ray &r, uint32_t stride)
             const uint32_t pa = sx ? r.p[0] : (sy ? r.p[1] : r.p[2]);
             // bit 23 stands for "past the root": the MISS, also when p_a has no
             // bit at 23 (an origin outside the root reflects to p = 0 or below 1)
+#if OCH_POP_SELECT
+            // branch-free: a single POP is the chain from pa = d2 (d2 & -d2 = d2)
+            const uint32_t d2 = r.dim << 1;
+            const uint32_t up = ((chain ? pa : d2) & (0u - d2)) | (1u << 23);
+#else
             const uint32_t up = chain ? ((pa & (0u - (r.dim << 1))) | (1u << 23)) : (r.dim << 1);
+#endif
+#if OCH_POP_SELECT
+            uint32_t k = __builtin_ctz(up);                                 // the new level's bit
+            asm volatile("" : "+v"(k));        // 1 << k, not re-folded into up & -up (one VALU more)
+            const uint32_t nd = 1u << k;                                    // new child-size bit
+#else
             const uint32_t nd = up & (0u - up);                             // new child-size bit
             const uint32_t k = __builtin_ctz(nd);
+#endif
             // one 24-bit multiply-add: k < 32, stride <= 1024 words
             r.sp = reinterpret_cast<uint32_t *>(reinterpret_cast<char *>(r.sp23) - __mul24((int)k, 4 * (int)stride));
             r.cur = *r.sp;                                                  // :434 (slot 0 after the MISS)
@@ -570,7 +601,7 @@ template <bool kCount>
 __device__ __forceinline__ void ray_descend(Ray &r, const DevPool &P, uint32_t stride)
 {
     const uint32_t c24 = r.idx ^ r.inv;
-    const uint32_t off = ((r.cur & kIdMask) << 5) + (c24 << 2);
+    const uint32_t off = slot_offset(r.cur, c24);
     const uint32_t *src = reinterpret_cast<const uint32_t *>(reinterpret_cast<const char *>(P.nodes) - 96 + off);
     *r.sp = r.cur;
     r.sp += stride;
@@ -707,7 +738,7 @@ __device__ __forceinline__ void ray_push_descend(Ray &r, const DevPool &P, uint3
     asm volatile("" : "+v"(r.mode));
     if (!present) return;
     // 32-bit byte offset from the uniform base: one scaled add, SGPR base address
-    const uint32_t off = ((r.cur & kIdMask) << 5) + (c24 << 2);
+    const uint32_t off = slot_offset(r.cur, c24);
     const uint32_t *src = reinterpret_cast<const uint32_t *>(
         reinterpret_cast<const char *>(OCH_LDS_TOP && top && (r.cur & kIdMask) < P.top_ids[OCH_LDS_TOP] ? top : P.nodes) -
         96 + off);
