@@ -735,8 +735,9 @@ __device__ __forceinline__ void ray_push_descend(Ray &r, const DevPool &P, uint3
     const uint32_t present = __builtin_amdgcn_ubfe(r.cur, c24, 1u);
     // kStepping (0) or, with the word loaded into cur, any nonzero "PUSH due"
     set_mode(r, OCH_LOAD_INTO_CUR ? present : present * kPending);
+    const bool go = present != 0;           // compared before the barrier: present's register becomes mode's
     asm volatile("" : "+v"(r.mode));
-    if (!present) return;
+    if (!go) return;
     // 32-bit byte offset from the uniform base: one scaled add, SGPR base address
     const uint32_t off = slot_offset(r.cur, c24);
     const uint32_t *src = reinterpret_cast<const uint32_t *>(
@@ -853,9 +854,11 @@ __device__ __forceinline__ void ray_iterate(Ray &r, const DevPool &P, uint32_t s
     if (kPacked && OCH_MERGED_DESCEND) {
         if (due_to_step(r)) ray_phase_step<kPacked>(r, stride);
         // no activity test: a miss leaves the lane kStepping, a HIT ends in this phase
-        uint32_t m = r.mode;                  // tested through an opaque copy, so the skipping
-        asm volatile("" : "+v"(m));           // lanes' r.mode is not re-materialised as kStepping
-        if (m != kStepping) ray_push_descend<kCount, kAsm, kPacked == kPackedSkip>(r, P, stride, top);
+        // tested before an opaque barrier on mode, so the skipping lanes' mode
+        // is not re-materialised as kStepping after the test (nor copied)
+        const bool push = r.mode != kStepping;
+        asm volatile("" : "+v"(r.mode));
+        if (push) ray_push_descend<kCount, kAsm, kPacked == kPackedSkip>(r, P, stride, top);
         return;
     }
     if (!kPacked && in_mode(r, kPending)) ray_phase_descend<kPacked>(r, P, stride);
