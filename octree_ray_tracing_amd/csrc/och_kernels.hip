@@ -133,6 +133,9 @@ constexpr uint32_t kIdMask = 0x00FFFFFFu;
 #ifndef OCH_POP_SELECT
 #define OCH_POP_SELECT 1
 #endif
+#ifndef OCH_ADDC_IDX
+#define OCH_ADDC_IDX 1
+#endif
 #ifndef OCH_MAD24
 #define OCH_MAD24 1
 #endif
@@ -778,12 +781,40 @@ __device__ __forceinline__ void ray_push_descend(Ray &r, const DevPool &P, uint3
     r.p[1] = uy ? my : r.p[1];
     r.p[2] = uz ? mz : r.p[2];
 #else
+    if (OCH_ADDC_IDX) {
+        // z, y, x: idx = 2 idx + upper as one v_addc_co_u32 with the compare's
+        // mask as carry-in (the compiler builds 3 v_cndmask + v_or3 instead).
+        // s_nop 1: the two wait states between a VALU write of vcc and its
+        // read as a lane mask, which the compiler inserts for its own code
 #pragma unroll
-    for (int a = 0; a < 3; ++a) {
-        const uint32_t mid = r.p[a] | r.dim;
-        const bool upper = __builtin_fmaf(ffrom(mid), r.c[a], r.b[a]) >= tm;
-        nidx |= (uint32_t)upper << a;
-        r.p[a] = upper ? mid : r.p[a];
+        for (int a = 2; a >= 0; --a) {
+            const uint32_t mid = r.p[a] | r.dim;
+            const float t = __builtin_fmaf(ffrom(mid), r.c[a], r.b[a]);
+            if (a == 2)
+                asm volatile("v_cmp_ge_f32_e32 vcc, %2, %3\n\t"
+                             "s_nop 1\n\t"
+                             "v_cndmask_b32_e32 %0, %0, %4, vcc\n\t"
+                             "v_cndmask_b32_e64 %1, 0, 1, vcc"
+                             : "+v"(r.p[a]), "=v"(nidx)
+                             : "v"(t), "v"(tm), "v"(mid)
+                             : "vcc");
+            else
+                asm volatile("v_cmp_ge_f32_e32 vcc, %2, %3\n\t"
+                             "s_nop 1\n\t"
+                             "v_cndmask_b32_e32 %0, %0, %4, vcc\n\t"
+                             "v_addc_co_u32_e32 %1, vcc, %1, %1, vcc"
+                             : "+v"(r.p[a]), "+v"(nidx)
+                             : "v"(t), "v"(tm), "v"(mid)
+                             : "vcc");
+        }
+    } else {
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+            const uint32_t mid = r.p[a] | r.dim;
+            const bool upper = __builtin_fmaf(ffrom(mid), r.c[a], r.b[a]) >= tm;
+            nidx |= (uint32_t)upper << a;
+            r.p[a] = upper ? mid : r.p[a];
+        }
     }
 #endif
     r.idx = nidx;
