@@ -78,3 +78,30 @@ def test_store_of_cur_in_flight_fails():
 """
     problems, _ = check(body)
     assert problems
+
+
+def mask_check(body: str):
+    return isa_check.check_mask_hazards("kern", isa_check.functions(HEAD + body + TAIL)["_Z4kern"])
+
+
+def test_mask_wait_states():
+    """Check 3: a VALU-written lane mask read as a mask needs 2 wait states
+    (the descent's hand-placed child index, OCH_ADDC_IDX, keeps them)."""
+    good = """\tv_cmp_ge_f32_e32 vcc, v23, v21
+\ts_nop 1
+\tv_cndmask_b32_e32 v13, v13, v22, vcc
+\tv_addc_co_u32_e32 v19, vcc, v19, v19, vcc
+\tv_cmp_eq_u32_e64 s[4:5], v21, v23
+\tv_cmp_ne_u32_e32 vcc, v21, v22
+\ts_mov_b64 s[8:9], 0
+\tv_cndmask_b32_e64 v17, 4, 2, s[4:5]
+"""
+    assert mask_check(good) == []
+    for bad in ("\tv_cmp_ge_f32_e32 vcc, v23, v21\n\tv_cndmask_b32_e32 v13, v13, v22, vcc\n",
+                "\tv_cmp_ge_f32_e32 vcc, v23, v21\n\ts_nop 0\n\tv_addc_co_u32_e32 v19, vcc, v19, v19, vcc\n",
+                "\tv_cmp_eq_u32_e64 s[4:5], v21, v23\n\tv_mov_b32 v1, v2\n\tv_cndmask_b32_e64 v17, 4, 2, s[4:5]\n"):
+        assert len(mask_check(bad)) == 1, bad
+    # a carry chain (carry-out read as the next carry-in) is not this hazard
+    assert mask_check("\tv_add_co_u32_e32 v1, vcc, v2, v3\n\tv_addc_co_u32_e32 v4, vcc, v5, v6, vcc\n") == []
+    # a scalar write of the mask in between replaces the VALU's; a label resets
+    assert mask_check("\tv_cmp_ge_f32_e32 vcc, v23, v21\n\ts_mov_b64 vcc, -1\n\tv_cndmask_b32_e32 v1, v1, v2, vcc\n") == []

@@ -16,6 +16,13 @@ with the product's flags and checks, in every function that issues the load
      (a copy, a spill, a full-wave select).  Writes there are allowed: they are
      the STEP phase's temporaries in lanes that issued no load (exec-masked,
      so the load's return and they never meet, och_kernels.hip OCH_ASM_LOAD).
+  3. in every function, a lane mask (vcc or an SGPR pair) written by a VALU
+     compare is read as a lane mask (v_cndmask, a carry-in) no sooner than 2
+     wait states later (instructions or s_nop states in between, within a basic
+     block; a carry-out read as the next carry-in, the 64-bit add chain, is not
+     this hazard).  The compiler keeps that distance in
+     its own code (its minimum over these kernels is 2); the check holds the
+     hand-placed VALU of the descent's child index (OCH_ADDC_IDX) to it.
 Exit status 0 and a one-line summary when every kernel passes; 1 with the
 offending instruction otherwise.  Run by the csrc Makefile (`make isa-check`),
 __graft_entry__.build() and tests/test_isa_check.py.
@@ -174,6 +181,46 @@ def check_function(name: str, lines: list[str]):
     return problems, len(loads)
 
 
+MASK_READ_E32 = ("v_cndmask_b32_e32", "v_addc_co_u32_e32", "v_subb_co_u32_e32", "v_subbrev_co_u32_e32")
+MASK_READ_E64 = ("v_cndmask_b32_e64", "v_addc_co_u32_e64", "v_subb_co_u32_e64", "v_subbrev_co_u32_e64")
+CARRY_WRITE = re.compile(r"^v_(add|sub|subrev|addc|subb|subbrev)_co_u32_(e32|e64)$")
+MASK_WAIT_STATES = 2
+
+
+def check_mask_hazards(name: str, lines: list[str]) -> list[str]:
+    """Check 3: VALU lane-mask writes and their reads as lane masks."""
+    problems, last, pos = [], {}, 0
+    for line in lines:
+        t = line.split(";")[0].strip()
+        if not t or t.startswith("."):
+            if LABEL_RE.match(t):
+                last = {}
+            continue
+        if LABEL_RE.match(t):
+            last = {}
+            continue
+        mn, ops = split_operands(t)
+        if mn == "s_nop":
+            pos += int(ops[0], 0) + 1
+            continue
+        read = "vcc" if mn in MASK_READ_E32 else (ops[-1] if mn in MASK_READ_E64 and ops else None)
+        if read in last and last[read] is not None and pos - last[read] < MASK_WAIT_STATES:
+            problems.append(f"{name}: {t} reads the lane mask {read} {pos - last[read]} wait state(s) after "
+                            f"a VALU wrote it (needs {MASK_WAIT_STATES})")
+        pos += 1
+        if mn.startswith("v_cmp_"):
+            dst = "vcc" if mn.endswith(("_e32", "_sdwa")) else (ops[0] if ops else None)
+            if dst:
+                last[dst] = pos
+        elif CARRY_WRITE.match(mn):
+            dst = "vcc" if mn.endswith("_e32") else (ops[1] if len(ops) > 1 else None)
+            if dst:
+                last[dst] = None               # a carry-out: not a compare's mask
+        elif mn.startswith("s_") and ops and ops[0] in last:
+            del last[ops[0]]                   # a scalar write replaces the VALU's
+    return problems
+
+
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--source", default=str(CSRC / "och_kernels.hip"))
@@ -189,6 +236,7 @@ def main(argv=None) -> int:
             checked.append(name)
             loads += n
         problems += p
+        problems += check_mask_hazards(name, lines)
     want = ("k_trace_grid", "k_trace_bounce")
     missing = [w for w in want if not any(w in c for c in checked)]
     asm_on = "och_cur_load" in asm
