@@ -221,6 +221,30 @@ def check_mask_hazards(name: str, lines: list[str]) -> list[str]:
     return problems
 
 
+RENDER_KERNEL = "k_trace_gridINS0_12CameraSourceENS0_9FrameSinkELi1ELb0"   # the bench's render launch
+
+
+def walk_loop_counts(lines: list[str]):
+    """Static VALU / SALU of the walk loop (the loop holding the descent's
+    asm load) of one function: from its header to the descent's branch back
+    to the latch, plus the latch.  None when the layout is not recognised."""
+    ins = [l.split(";")[0].rstrip() if not l.lstrip().startswith(".LBB") else l for l in lines]
+    pos = {m.group(1): i for i, l in enumerate(ins) if (m := re.match(r"^(\.LBB\d+_\d+):", l.strip()))}
+    for i, l in enumerate(lines):
+        if "Inner Loop Header: Depth=1" not in l:
+            continue
+        for k in range(i + 1, len(lines)):
+            m = re.match(r"\s*s_branch\s+(\.LBB\d+_\d+)", lines[k])
+            if m and pos.get(m.group(1), len(lines)) < i:
+                body = lines[i:k + 1] + lines[pos[m.group(1)]:i]
+                if not any("och_cur_load" in b for b in body):
+                    break
+                valu = sum(1 for b in body if re.match(r"\s*v_", b))
+                salu = sum(1 for b in body if re.match(r"\s*s_", b) and not re.match(r"\s*s_(nop|waitcnt|cbranch|branch)", b))
+                return valu, salu
+    return None
+
+
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--source", default=str(CSRC / "och_kernels.hip"))
@@ -242,6 +266,10 @@ def main(argv=None) -> int:
     asm_on = "och_cur_load" in asm
     summary = {"functions": len(fns), "checked": len(checked), "asm_loads": loads, "problems": len(problems),
                "asm_load_enabled": asm_on}
+    render = [n for n in fns if RENDER_KERNEL in n]
+    counts = walk_loop_counts(fns[render[0]]) if render else None
+    if counts:
+        summary["render_loop_valu"], summary["render_loop_salu"] = counts
     if asm_on and missing:
         problems.append(f"no asm load found in {missing}")
     if problems:
