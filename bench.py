@@ -365,6 +365,143 @@ def other_configs(a, dev, stream):
     return out
 
 
+def single_gpu_base(a, nodes, root, W, H, cams, streams, dev, frames_ref):
+    """scaling_base (N > 1, rank 0 alone): the same W x H two-view frame on one
+    GPU, rendered the way the N = 1 bench renders configs[2] -- the fused RGBA8
+    launch (raygen + traversal + trace_pixel shading) of both views, three
+    frames in flight, the window issued by one och_gpu_render_steps_dev call,
+    the launch order planned at the library's default -- while the other ranks
+    wait at a barrier.  frames_ref: the sharded run's last RGBA8 frames on rank
+    0, which this run's must equal (same cameras)."""
+    import torch
+    import octree_ray_tracing_amd as ort
+    from octree_ray_tracing_amd._lib import Camera, load as load_lib
+
+    lib = load_lib()
+    B = min(3, len(streams))
+    st = list(streams[:B])
+    pool = ort.HOctree(nodes, root, a.depth, device=dev.index)
+    try:
+        pool.set_palette(ort.VoxelData().get_colours())
+        for kv in a.opt:
+            k, v = kv.split("=")
+            pool.set_option(k, int(v))
+        pool.set_stream(st[0])
+        if not any(kv.startswith("tile_order=") for kv in a.opt):
+            pool.set_option("tile_order", 2)
+        if pool.get_option("tile_order") >= 2:
+            pool.plan_views(cams, a.row_chunk, 0, 1)
+        frames = [torch.empty((len(cams), H, W), dtype=torch.int32, device=dev) for _ in range(B)]
+        arr = (Camera * len(cams))(*cams)
+        sp = (ctypes.c_void_p * B)(*[s_.cuda_stream for s_ in st])
+        fp = (ctypes.c_void_p * B)(*[f.data_ptr() for f in frames])
+
+        def drain():
+            while not all(s_.query() for s_ in st):
+                pass
+            torch.cuda.synchronize()
+
+        def window(n):
+            drain()
+            t0 = time.perf_counter()
+            if lib.och_gpu_render_steps_dev(pool._h, ctypes.cast(arr, ctypes.c_void_p), len(cams), n, sp, fp, B,
+                                            None, None, a.row_chunk, 0):
+                raise RuntimeError(f"scaling_base: {lib.och_last_error().decode()}")
+            drain()
+            return time.perf_counter() - t0
+
+        window(max(a.warmup, 1))
+        el = window(a.steps)
+        last = frames[(a.steps - 1) % B].cpu().numpy()
+        rays = W * H * len(cams)
+        out = {"value": round(rays * a.steps / el / 1e6, 2), "unit": "Mrays/s",
+               "ms_per_step": round(el / a.steps * 1e3, 4), "steps": a.steps, "frames_in_flight": B,
+               "workload": f"the same {W}x{H} two-view frame on one MI355X (rank 0 alone): the N = 1 bench's path "
+                           "(fused RGBA8 launch, och_gpu_render_steps_dev window)",
+               "frames_equal_sharded": None if frames_ref is None else bool(np.array_equal(last, frames_ref))}
+        if a.sustain > 0:
+            n_s = max(a.steps, int(math.ceil(a.sustain / (el / a.steps))))
+            out["sustained"] = round(statistics.median([rays * n_s / window(n_s) / 1e6 for _ in range(3)]), 2)
+        return out
+    finally:
+        torch.cuda.synchronize()
+        pool.close()
+
+
+def group_bench(a):
+    """`bench.py --gpus N --launch group`: one process drives N devices through
+    the library's device group (och_frame_group_*, the form a C++ host of the
+    reference would use): a pool replica per device, rows dealt by one timed
+    render (och_frame_group_plan), per frame every device renders its slice
+    as colour codes, RCCL all-gathers the slices (ncclCommInitAll
+    communicators, one issuing thread per device) and shades the whole frame.
+    A window is one och_frame_group_render_steps call; value = the frames'
+    rays / the wall time between synchronisations of every device.  The
+    last frame of every device is checked against the oracle (rank 0's) and
+    against rank 0's copy."""
+    import torch
+    import octree_ray_tracing_amd as ort
+    from octree_ray_tracing_amd.frame import FrameGroup
+
+    n = a.gpus
+    inflight, _ = pipeline_defaults(n, a.inflight, a.hw_queues)
+    W, H = frame_size(n, a.width, a.height, a.scaling)
+    torch.cuda.set_device(0)
+    tree = ort.build_terrain(a.depth, use_gpu=True)
+    cams = [ort.camera(ORIGIN, YAW, p, FOV, W, H) for p in PITCHES]
+    g = FrameGroup(tree.nodes, tree.root, a.depth, devices=list(range(n)))
+    try:
+        g.set_palette(ort.VoxelData().get_colours())
+        for kv in a.opt:
+            k, v = kv.split("=")
+            g.set_option(k, int(v))
+        g.plan(cams, a.row_chunk)
+
+        def window(steps):
+            g.synchronize()
+            t0 = time.perf_counter()
+            g.render_steps(cams, steps, inflight, a.row_chunk)
+            g.synchronize()
+            return time.perf_counter() - t0
+
+        window(max(a.warmup, 1))
+        el = window(a.steps)
+        frames = [g.download(r) for r in range(n)]
+        rays = W * H * len(cams)
+        sustained = None
+        if a.sustain > 0:
+            n_s = max(a.steps, int(math.ceil(a.sustain / (el / a.steps))))
+            vals = [rays * n_s / window(n_s) / 1e6 for _ in range(3)]
+            sustained = {"value": round(statistics.median(vals), 2), "unit": "Mrays/s", "steps_per_run": n_s,
+                         "values": [round(v, 2) for v in vals]}
+    finally:
+        g.close()
+    parity = None
+    if not a.no_parity:
+        _, parity = cpu_leg(tree.nodes, tree.root, a.depth, W, H, frames[0], None, time_it=False, budget_s=0)
+        parity["devices_equal_rank0"] = all(np.array_equal(f, frames[0]) for f in frames)
+        if not parity["devices_equal_rank0"]:
+            parity["mismatches"] += 1
+    line = {
+        "metric": "Mrays/sec primary traversal (depth-12 SVO-DAG, raygen+trace+shade per frame)",
+        "value": round(rays * a.steps / el / 1e6, 2), "unit": "Mrays/s", "n_gpus": n, "steps": a.steps,
+        "warmup": a.warmup, "ms_per_step": round(el / a.steps * 1e3, 4), "higher_is_better": True,
+        "scaling": "strong", "vs_baseline": None, "dtype": "f32",
+        "data": "synthetic: the reference's terrain fill at depth %d, built on the GPU (och_build_terrain)" % a.depth,
+        "config": {"workload": (f"{W}x{H}, two views per step, depth-{a.depth} DAG over {n} MI355X from one process "
+                                "(och_frame_group_*)"),
+                   "launch": "one process, one issuing thread per device (och_frame_group_render_steps)",
+                   "exchange": "RCCL all-gather (ncclCommInitAll communicators), every device shades the frame",
+                   "row_deal": "och_frame_group_plan: chunks dealt by their cost in one timed render",
+                   "frames_in_flight": inflight, "width": W, "height": H, "depth": a.depth,
+                   "dag_nodes": int(tree.n_nodes), "parallelism": f"rows{n}"},
+        "sustained": sustained, "parity": parity, "roofline": None, "cpu_baseline": None,
+    }
+    print(json.dumps(line), flush=True)
+    if parity is not None and parity["mismatches"]:
+        raise SystemExit("group frames differ from the oracle")
+
+
 def load_pmc(kernel: str, config_key: str):
     """The committed rocprofv3 PMC summary of this configuration, if it was
     taken of the kernel source in this tree (profiles/pmc_summary.json,
@@ -399,9 +536,102 @@ def load_window():
     return {"source": "profiles/window_summary.json", **{k: d.get(k) for k in keep}}
 
 
+def resolve_launch(gpus: int, env, launch: str, n_devices: int) -> str:
+    """How `bench.py --gpus N` runs, decided before HIP starts:
+      "rank"  -- this process is one rank of a launcher's job (WORLD_SIZE set,
+                 e.g. the driver's torch.distributed.run), or N = 1;
+      "procs" -- no launcher and N > 1: start N ranks under
+                 torch.distributed.run as child processes and exit with their
+                 status (never exec: this process has not touched the GPU);
+      "group" -- --launch group: this one process drives N devices through
+                 och_frame_group_* (one issuing thread per device).
+    Exits non-zero, instead of silently measuring fewer GPUs, when fewer than
+    N devices are visible or when WORLD_SIZE disagrees with --gpus.
+    n_devices: torch.cuda.device_count() (does not initialise HIP here)."""
+    if gpus < 1:
+        raise SystemExit("--gpus must be >= 1")
+    world = env.get("WORLD_SIZE")
+    if world is not None:
+        if launch == "group":
+            raise SystemExit("--launch group drives every device from one process; run it without a launcher")
+        if int(world) != gpus:
+            raise SystemExit(f"--gpus {gpus} but WORLD_SIZE {world}: refusing to measure a different GPU count")
+        # the gloo rehearsal runs several ranks per GPU on purpose
+        if env.get("OCH_DIST_BACKEND", "nccl") != "gloo" and n_devices < int(world):
+            raise SystemExit(f"WORLD_SIZE {world} ranks but {n_devices} GPU(s) visible")
+        return "rank"
+    if launch == "group":
+        if n_devices < gpus:
+            raise SystemExit(f"--gpus {gpus} asked, {n_devices} GPU(s) visible")
+        return "group"
+    if gpus == 1:
+        return "rank"
+    if n_devices < gpus:
+        raise SystemExit(f"--gpus {gpus} asked, {n_devices} GPU(s) visible: refusing to run fewer ranks")
+    return "procs"
+
+
+def spawn_ranks(gpus: int, argv) -> int:
+    """`bench.py --gpus N` without a launcher: the same N-rank job the driver
+    starts (torch.distributed.run, one process per GPU, 127.0.0.1), run as a
+    child process; returns its exit status."""
+    import socket
+    import subprocess
+
+    with socket.socket() as s:                 # a free rendezvous port on the loopback
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), str(Path(__file__).resolve()), *argv]
+    log(f"bench: no launcher in the environment; starting {gpus} ranks: {' '.join(cmd)}")
+    return subprocess.run(cmd).returncode
+
+
+def slice_checksum(t):
+    """Order-sensitive checksum of a device tensor's bytes (int64, on its device)."""
+    import torch
+    x = t.reshape(-1).view(torch.uint8).to(torch.int64)
+    w = torch.arange(x.numel(), device=x.device, dtype=torch.int64) % 65521 + 1
+    return (x * w).sum()
+
+
+def check_exchange(frame, world: int, rank: int, receives: bool):
+    """After one exchanged frame in `frame` (a ShardedFrame): every rank's
+    checksum of its own slice goes to every rank over torch.distributed, and
+    every rank that received the slices (all of them after an all-gather,
+    rank 0 after a gather) compares them with its copies in `gathered`.
+    Returns the total count of mismatching slices over all ranks."""
+    import torch
+    import torch.distributed as dist
+
+    own = slice_checksum(frame.slice).reshape(1)
+    every = torch.zeros(world, dtype=torch.int64, device=own.device)
+    if dist.get_backend() == "gloo":
+        outs = [torch.zeros(1, dtype=torch.int64) for _ in range(world)]
+        dist.all_gather(outs, own.cpu())
+        every.copy_(torch.cat(outs))
+    else:
+        dist.all_gather_into_tensor(every, own)
+    bad = torch.zeros(1, dtype=torch.int64, device=own.device)
+    if receives:
+        got = torch.stack([slice_checksum(frame.gathered[r]) for r in range(world)])
+        bad += (got != every).sum()
+    coll(dist.all_reduce, bad)
+    return int(bad.item())
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--launch", choices=("procs", "group"), default="procs",
+                    help="--gpus N > 1 without a launcher (no WORLD_SIZE): 'procs' (default) starts N ranks under "
+                         "torch.distributed.run, one process per GPU, as the driver does; 'group' drives the N "
+                         "devices from this one process through och_frame_group_* (ncclCommInitAll, one issuing "
+                         "thread per device).  --launch group also runs at --gpus 1")
+    ap.add_argument("--no-scaling-base", action="store_true",
+                    help="N > 1: skip scaling_base (rank 0 alone rendering the same frame, as N = 1 would)")
+    ap.add_argument("--no-exchange-check", action="store_true",
+                    help="N > 1: skip the checksum check of one exchanged frame before the timed window")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--depth", type=int, default=12)
@@ -481,17 +711,28 @@ def main():
     ap.add_argument("--sharded", action="store_true",
                     help="N = 1: the N > 1 step at world size 1 -- render colour codes, exchange them over RCCL "
                          "(--exchange) and shade -- instead of the fused launch writing RGBA8 frames")
-    ap.add_argument("--exchange", choices=("rccl", "gather", "torch"), default="gather",
-                    help="sharded steps (N > 1, or --sharded): 'gather' (default) = only rank 0 (the display) "
-                         "receives the slices, ncclSend / ncclRecv on the library's own RCCL communicator "
+    ap.add_argument("--exchange", choices=("rccl", "gather", "torch"), default="rccl",
+                    help="sharded steps (N > 1, or --sharded): 'rccl' (default; configs[3]'s 'RCCL framebuffer "
+                         "all-gather') = ncclAllGather of the slices on the library's own RCCL communicator "
                          "(och_comm_*, its id broadcast by torch.distributed), the window issued by one "
-                         "och_gpu_render_sharded_steps_dev call per rank; 'rccl' = the same with ncclAllGather; "
-                         "'torch' = dist.all_gather_into_tensor per step from Python.  The gloo rehearsal "
-                         "backend always exchanges through torch"),
+                         "och_gpu_render_sharded_steps_dev call per rank; 'gather' = only rank 0 (the display) "
+                         "receives them (ncclSend / ncclRecv; also timed beside the all-gather as "
+                         "exchange_gather); 'torch' = dist.all_gather_into_tensor per step from Python.  The gloo "
+                         "rehearsal backend always exchanges through torch"),
     ap.add_argument("--hw-queues", type=int, default=None,
                     help="GPU_MAX_HW_QUEUES for this process (set before HIP starts); default the "
                          "environment's (4 on the box), 8 at N >= 8")
     a = ap.parse_args()
+
+    # A plain `bench.py --gpus N` (no launcher) must measure N GPUs or fail:
+    # torch.cuda.device_count() does not initialise HIP on this image, so the
+    # child ranks can still be started from here.
+    import torch
+    launch = resolve_launch(a.gpus, os.environ, a.launch, torch.cuda.device_count())
+    if launch == "procs":
+        sys.exit(spawn_ranks(a.gpus, sys.argv[1:]))
+    if launch == "group":
+        return group_bench(a)
 
     # Frames in flight and hardware queues by world size (tools/proxy_rank.py,
     # every shard, profiles/r03/proxy/r03z*): at N = 8 a rank's launches are half
@@ -514,8 +755,6 @@ def main():
         # Rehearsal of the N > 1 path on a box with fewer GPUs than ranks:
         # ranks share devices round-robin and collectives go through the host.
         local %= max(1, torch.cuda.device_count())
-    if world != a.gpus:
-        log(f"warning: --gpus {a.gpus} but WORLD_SIZE {world}; using WORLD_SIZE")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     sharded = world > 1 or a.sharded
@@ -552,6 +791,16 @@ def main():
     exch_mode = "gather" if (comm is not None and a.exchange == "gather") else "all_gather"
     if exch_mode == "gather" and a.shade != "display":
         raise SystemExit("--exchange gather needs --shade display")
+
+    def exchange_label():
+        """What the sharded step's exchange is, as it runs now (config.exchange)."""
+        if not sharded:
+            return None
+        if comm is not None:
+            return ("RCCL " + ("gather to rank 0 (ncclSend / ncclRecv)" if exch_mode == "gather" else
+                               "all-gather (ncclAllGather)") + " on the library's communicator (och_comm_*)")
+        return ("torch.distributed all_gather_into_tensor" if backend == "nccl" else
+                "torch.distributed gloo all_gather through the host (rehearsal)")
     cams = [ort.camera(ORIGIN, YAW, p, FOV, W, H) for p in PITCHES]
     # N > 1: which rank renders which row chunks.  Rank 0 times one render of
     # the whole frame per chunk and deals the chunks longest first onto the
@@ -576,12 +825,17 @@ def main():
         prio = [int(x) for x in a.stream_priority.split(",") if x.strip()]
         streams = [stream] + [torch.cuda.Stream(device=dev, priority=prio[i] if i < len(prio) else 0)
                               for i in range(max(1, a.inflight) - 1)]
-    sfs = []
-    for s_ in streams:
-        with torch.cuda.stream(s_):
-            sfs.append(ShardedFrame(pool, W, H, a.row_chunk, n_views=len(PITCHES), indexed=indexed, shade=a.shade,
-                                    direct=direct, deal=deal, comm=comm, sharded=sharded, exchange=exch_mode))
-    pool.set_stream(stream)
+
+    def make_frames():
+        out = []
+        for s_ in streams:
+            with torch.cuda.stream(s_):
+                out.append(ShardedFrame(pool, W, H, a.row_chunk, n_views=len(PITCHES), indexed=indexed,
+                                        shade=a.shade, direct=direct, deal=deal, comm=comm, sharded=sharded,
+                                        exchange=exch_mode))
+        pool.set_stream(stream)
+        return out
+    sfs = make_frames()
     # Launch order: one planning render of these views times every tile, and
     # the costliest tiles go first (och_gpu_plan_views; dispatch order only,
     # frames identical), so no frame ends on a few late grazing tiles.
@@ -707,8 +961,9 @@ def main():
     # waited (rocprofv3 --hip-trace, profiles/r03/window/).
     # N > 1 (colour codes): the render is issued the same way; the all-gather and
     # the display rank's shade stay in ShardedFrame.exchange, on the frame's stream.
-    fast = None
-    if (direct or (indexed and sharded)) and not a.no_fast_issue:
+    def make_fast():
+        if not ((direct or (indexed and sharded)) and not a.no_fast_issue):
+            return None
         from octree_ray_tracing_amd._lib import Camera, load as load_lib
         lib = load_lib()
         cam_arr = (Camera * len(cams))(*cams)
@@ -718,8 +973,9 @@ def main():
             args = [(h, cp, len(cams), ctypes.c_void_p(f_.frames.data_ptr()), a.row_chunk, 0, 1) for f_ in sfs]
         else:
             args = [(h, cp, len(cams), ctypes.c_void_p(f_.slice.data_ptr()), a.row_chunk, rank, world) for f_ in sfs]
-        fast = {"lib": lib, "cams": cam_arr, "h": h, "direct": direct,
+        return {"lib": lib, "cams": cam_arr, "h": h, "direct": direct,
                 "args": [[(h, ctypes.c_void_p(s_.cuda_stream)), ra] for s_, ra in zip(streams, args)]}
+    fast = make_fast()
 
     def prepare_native(n, bounce, ev):
         """N = 1, direct frames: the window's n frames as ONE library call
@@ -756,10 +1012,11 @@ def main():
     if comm is not None and a.issue == "native" and a.step_events == "dispatch" and not a.no_fast_issue:
         sharded_steps = {b: ShardedSteps(sfs, streams, comm, cams, bounce=b) for b in (False, True)}
         native_issue = True
+    arm_steps = None           # a timed arm with another exchange (exchange_gather): its ShardedSteps
 
     def prepare_sharded(n, bounce, ev):
         pairs = [ev_pool[(len(ev) + k) % len(ev_pool)] for k in range(n)] if ev is not None else []
-        issue_ = sharded_steps[bool(bounce)].prepare(
+        issue_ = (arm_steps or sharded_steps)[bool(bounce)].prepare(
             n, [x.h.value for x, _ in pairs] if ev is not None else None,
             [y.h.value for _, y in pairs] if ev is not None else None)
 
@@ -922,6 +1179,40 @@ def main():
         rank_s.append([float(el.item())])
         return float(el.item())
 
+    # N > 1: one frame through the exchange the window will time, checked before
+    # anything is timed -- every rank's checksum of its own slice against the
+    # receiving ranks' copies.  A library-communicator exchange that delivers
+    # wrong bytes falls back to torch.distributed's all-gather (checked again);
+    # a second mismatch ends the run with a non-zero status.
+    exchange_check = None
+    if world > 1 and not a.no_exchange_check:
+        def one_frame():
+            if sharded_steps is not None:
+                prepare_sharded(1, False, None)()
+            else:
+                step(0)
+            drain()
+
+        def checked(label):
+            one_frame()
+            bad = check_exchange(sfs[0], world, rank, exch_mode != "gather" or rank == 0)
+            return {"exchange": label, "frames": 1, "slices": world, "mismatches": bad}
+        exchange_check = checked(exchange_label())
+        if exchange_check["mismatches"] and comm is not None:
+            log(f"exchange check: {exchange_check['mismatches']} slice(s) differ after {exchange_label()}; "
+                "falling back to torch.distributed all_gather_into_tensor")
+            torch.cuda.synchronize()
+            comm.close()
+            comm, exch_mode, a.exchange = None, "all_gather", "torch"
+            sfs = make_frames()
+            fast = make_fast()
+            sharded_steps, native_issue = None, False
+            exchange_check["fallback"] = checked(exchange_label())
+            if exchange_check["fallback"]["mismatches"]:
+                raise SystemExit(f"exchange check failed twice: {exchange_check}")
+        elif exchange_check["mismatches"]:
+            raise SystemExit(f"exchange check failed: {exchange_check}")
+
     # Frame latency: the render launch alone on an otherwise idle GPU.
     lat = []
     for k in range(max(a.warmup, 1) + 5):
@@ -968,6 +1259,31 @@ def main():
         vals = [W * H * len(cams) * n_s / r / 1e6 for r in runs]
         sustained = {"value": round(statistics.median(vals), 2), "unit": "Mrays/s", "steps_per_run": n_s,
                      "runs_s": [round(r, 4) for r in runs], "values": [round(v, 2) for v in vals]}
+
+    # N > 1 with the all-gather: the same window with the other exchange the
+    # library offers -- only the display rank receives the slices (ncclSend /
+    # ncclRecv) -- beside it, on the same frames, deal and streams, after its
+    # own one-frame check.  Not the line's value: configs[3] names the all-gather.
+    exchange_gather = None
+    if world > 1 and sharded_steps is not None and exch_mode == "all_gather" and a.shade == "display":
+        arm_steps = {False: ShardedSteps(sfs, streams, comm, cams, exchange="gather")}
+        prepare_sharded(1, False, None)()
+        drain()
+        bad = check_exchange(sfs[0], world, rank, rank == 0)
+        exchange_gather = {"exchange": "RCCL gather to rank 0 (ncclSend / ncclRecv) on the library's communicator",
+                           "check_mismatches": bad}
+        if not bad:
+            prepare_sharded(a.warmup, False, None)()
+            el_g = timed(a.steps)
+            exchange_gather.update({"value": round(total_rays / el_g / 1e6, 2),
+                                    "ms_per_step": round(el_g / a.steps * 1e3, 4),
+                                    "per_rank_ms_per_step": [round(t / a.steps * 1e3, 4) for t in rank_s[-1]]})
+            if sustained is not None:
+                el_gs = timed(sustained["steps_per_run"])
+                exchange_gather["sustained"] = round(W * H * len(cams) * sustained["steps_per_run"] / el_gs / 1e6, 2)
+        exchange_gather["note"] = ("same frames, streams and row deal as the headline (rank 0 at the all-gather's "
+                                   f"weight {a.display_weight}); only rank 0 receives and shades")
+        arm_steps = None
 
     # The same window with the occupied-box cull off (every ray walks): the
     # traversal speed like-for-like with round 1 and with the CPU baseline.
@@ -1173,6 +1489,17 @@ def main():
     else:
         roof.update({k: hbm[k] for k in ("bound", "achieved", "peak", "unit", "frac")})
 
+    # N > 1: the like-for-like one-GPU rate of this same frame (rank 0 alone,
+    # the other ranks idle at a barrier), so a scaling curve compares frames
+    # of one size: the driver's N = 1 line is configs[2]'s 1920x1080 frame.
+    scaling_base = None
+    if world > 1 and not a.no_scaling_base:
+        drain()
+        dist.barrier()
+        if rank == 0:
+            scaling_base = single_gpu_base(a, nodes, root, W, H, cams, streams, dev, frames_host)
+        dist.barrier()
+
     # The other BASELINE configs on this GPU, N = 1 only (each a separate,
     # smaller workload; not the headline): configs[1] = depth-10 DAG at
     # 1920x1080 through the same pipelined two-view step; configs[0] = the
@@ -1192,11 +1519,14 @@ def main():
         if world == 1:
             workload = "configs[2]: 4096^3 depth-12 och_h_octree DAG, 1920x1080 primary rays, 1 MI355X" + (
                 " (the sharded N > 1 step at world size 1: codes, RCCL exchange, shade)" if sharded else "")
-        elif a.scaling == "strong" and (W, H) == (3840, 2160):
-            workload = (f"configs[3]: 4096^3 depth-12, 3840x2160 primary rays tiled across {world} MI355X "
-                        "with RCCL framebuffer all-gather")
         else:
-            workload = f"depth-12 DAG, {W}x{H} frame row-sharded over {world} MI355X + RCCL all-gather"
+            how = ("RCCL framebuffer all-gather" if exch_mode == "all_gather" and backend == "nccl" else
+                   "RCCL gather of the framebuffer to the display rank" if exch_mode == "gather" else
+                   "a gloo all-gather through the host (rehearsal, not RCCL)")
+            if a.scaling == "strong" and (W, H) == (3840, 2160) and a.depth == 12:
+                workload = f"configs[3]: 4096^3 depth-12, 3840x2160 primary rays tiled across {world} MI355X with {how}"
+            else:
+                workload = f"depth-{a.depth} DAG, {W}x{H} frame row-sharded over {world} MI355X with {how}"
         line = {
             "metric": "Mrays/sec primary traversal (depth-12 SVO-DAG, raygen+trace+shade per frame)",
             "value": round(value, 2),
@@ -1225,18 +1555,16 @@ def main():
                                  else "one och_gpu_render_steps_dev call per timed window (the library issues each "
                                  "step's launch)" if native_issue else "one C-ABI render call per step"
                                  if fast is not None else "Python wrappers per step"),
-                       "exchange": (None if not sharded else
-                                    f"RCCL {'gather to rank 0 (ncclSend/ncclRecv)' if exch_mode == 'gather' else 'all-gather'} "
-                                    "on the library's communicator (och_comm_*)" if comm is not None else
-                                    "torch.distributed all_gather_into_tensor" if backend == "nccl" else
-                                    "torch.distributed gloo all_gather through the host (rehearsal)"),
+                       "exchange": exchange_label(),
+                       "launch": ("one process per GPU (torch.distributed.run)" if world > 1 else "one process"),
                        "row_deal": (None if world == 1 else
                                     "round-robin 8-row chunks" if deal is None else
                                     f"row chunks dealt by {a.deal} (och_deal_chunks), rank 0 weight "
                                     f"{a.display_weight if a.shade == 'display' else 1.0}; chunks per rank "
                                     f"{np.bincount(deal, minlength=world).tolist()}"),
                        "shade": ("the render launch shades each pixel (trace_pixel) into the RGBA8 frames" if direct
-                                 else "every rank all-gathers the frame's codes; " +
+                                 else ("rank 0 gathers" if exch_mode == "gather" else "every rank all-gathers")
+                                 + " the frame's codes; " +
                                  ("rank 0 (the display) shades them to RGBA8" if a.shade == "display" and world > 1
                                   else "every rank shades them to RGBA8")),
                        "frames": ("rgba8 frames written by the fused launch (no exchange at N = 1)" if direct else
@@ -1253,6 +1581,9 @@ def main():
             "walked_rays_note": "Mrays/s of the rays that walk the DAG (value x (1 - culled_frac)); the "
                                 "occupied-box cull ends the rest as proven misses",
             "per_rank_ms_per_step": per_rank_ms,
+            **({"exchange_check": exchange_check} if exchange_check else {}),
+            **({"exchange_gather": exchange_gather} if exchange_gather else {}),
+            **({"scaling_base": scaling_base} if scaling_base else {}),
             **({"extra_windows": extra, "extra_windows_no_events": extra_noev} if extra else {}),
             **({"host_stamps_ns": stamps} if stamps else {}),
             "trace_batch": trace_only,

@@ -390,9 +390,11 @@ class ShardedSteps:
     on streams[k % B] into frames[k % B]'s buffers -- the work of
     ShardedFrame.render on that stream, with no interpreter between a frame's
     launches.  frames: one ShardedFrame per stream, indexed, sharing one pool
-    and made with this comm."""
+    and made with this comm.  exchange: override the frames' own exchange mode
+    ("all_gather" or "gather"; both need every rank's gathered buffer only
+    where it receives)."""
 
-    def __init__(self, frames, streams, comm: RcclComm, cams, bounce: bool = False):
+    def __init__(self, frames, streams, comm: RcclComm, cams, bounce: bool = False, exchange: str | None = None):
         f0 = frames[0]
         if len(frames) != len(streams) or not all(f.comm is comm and f.indexed and not f.direct for f in frames):
             raise ValueError("one indexed, sharded ShardedFrame per stream, all on this comm")
@@ -403,9 +405,14 @@ class ShardedSteps:
         self.cams = (Camera * len(cams))(*cams)
         self.n_views = len(cams)
         B = len(frames)
-        mode = f0.exchange_mode
+        mode = f0.exchange_mode if exchange is None else exchange
+        if mode not in ("all_gather", "gather"):
+            raise ValueError("exchange must be 'all_gather' or 'gather'")
+        if mode == "gather" and f0.shade != "display":
+            raise ValueError("exchange='gather' needs shade='display'")
         if mode == "all_gather" and f0.shade == "display":
             mode = "display"
+        self.mode = mode
         self.exchange = EXCHANGE[mode]
         receives = mode != "gather" or f0.rank == 0
         shades = mode == "all_gather" or f0.rank == 0

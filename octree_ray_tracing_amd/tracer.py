@@ -394,8 +394,9 @@ def deal_chunks(costs, n_shards: int, weights=None) -> np.ndarray:
 DISPLAY_WEIGHTS = {"gather": {2: 0.9, 4: 0.7, 8: 0.5}, "all_gather": {2: 0.9, 4: 0.8, 8: 0.6}}
 
 
-def display_weight(world: int, exchange: str = "gather") -> float:
-    """Default deal weight of rank 0 (the display rank) at this world size."""
+def display_weight(world: int, exchange: str = "all_gather") -> float:
+    """Default deal weight of rank 0 (the display rank) at this world size,
+    for the exchange configs[3] names (the all-gather) unless told otherwise."""
     table = DISPLAY_WEIGHTS.get(exchange, DISPLAY_WEIGHTS["all_gather"])
     if world in table:
         return table[world]

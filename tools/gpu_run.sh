@@ -23,6 +23,7 @@
 #   pmc:LABEL=COUNTERS      one rocprofv3 --pmc pass (quote the counter list) over the bench's 20-step
 #                           window (BENCH_PMC_ARGS adds bench args) -> pmc_LABEL/, summarised into
 #                           pmc_LABEL.json (tools/pmc_summary.py --window); passes of one LABEL accumulate
+#   rocpy:LABEL=SCRIPT ARGS rocprofv3 --kernel-trace --stats of python -u tools/SCRIPT ARGS -> roc_LABEL/
 #   pmcpy:LABEL=COUNTERS@SCRIPT ARGS   the same pass over python -u tools/SCRIPT ARGS, every dispatch
 #                           summarised (no window) -> pmc_LABEL.json
 # Example:
@@ -86,6 +87,12 @@ for step in "$@"; do
         --no-cull-off --moving-steps 0 $BENCH_PMC_ARGS > "$O/pmc_${label}_$i.json" 2> "$O/pmc_${label}_$i.err" \
         || { tail -20 "$O/pmc_${label}_$i.err"; exit $i; }
       python tools/pmc_summary.py "$O/pmc_$label" --window > "$O/pmc_$label.json" || exit $i ;;
+    rocpy)
+      # rocprofv3 kernel trace (timestamps + per-kernel stats, no counters) of python -u tools/ARGS
+      export TMPDIR=/tmp
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/roc_$label" -o run -- \
+        python -u tools/$args > "$O/roc_$label.log" 2>&1 || { tail -20 "$O/roc_$label.log"; exit $i; }
+      tail -3 "$O/roc_$label.log" ;;
     pmcpy)
       export TMPDIR=/tmp
       counters=${args%%@*}; script=${args#*@}
