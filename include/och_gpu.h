@@ -145,59 +145,38 @@ OCH_API int och_gpu_set_palette(och_gpu_pool *pool, const uint32_t *rgba, uint32
  * non-blocking stream of its own. */
 OCH_API int och_gpu_set_stream(och_gpu_pool *pool, void *hip_stream);
 OCH_API int och_gpu_synchronize(och_gpu_pool *pool);
-/* Launch schedule of trace/render kernels. */
+/* Launch options of trace/render kernels.  Every launch is a grid of one ray
+ * per thread.  Ids 0, 2, 3, 7, 9, 12 and 13 belonged to arms measured slower
+ * on every scene and retired in round 5 (persistent and refill schedules,
+ * in-block wave merging, the per-node voxel-box skip, the column cull;
+ * DESIGN.md section 8): setting or reading them fails with OCH_E_INVALID. */
 typedef enum och_option {
-    OCH_OPT_SCHEDULE = 0,      /* 0 = grid (one ray per thread), 1 = persistent waves with lane refill,
-                                  2 = grid with lane refill: each wave walks a chunk of OCH_OPT_CHUNK_TILES
-                                  64-ray tiles and refills its idle lanes (ballot + popcount) whenever at
-                                  least OCH_OPT_REFILL of them have finished */
-    OCH_OPT_BLOCK = 1,         /* threads per workgroup: 64..1024, multiple of 64 (default 256) */
-    OCH_OPT_WAVES_PER_CU = 2,  /* persistent: resident waves per compute unit (default 32) */
-    OCH_OPT_REFILL = 3,        /* schedules 1, 2: refill a wave once this many of its lanes are idle (1..64) */
+    OCH_OPT_BLOCK = 1,         /* threads per workgroup: 64..1024, multiple of 64 (default 64) */
     OCH_OPT_LAYOUT = 4,        /* 0 = the caller's node layout; 1 = packed (default when the DAG has < 2^24
                                   (node, level) pairs): per-level breadth-first ids, interior slots carry the
                                   child's occupancy mask so only descents and hits touch memory */
     OCH_OPT_TILE_ORDER = 5,    /* camera rays (render): 0 = 8x8-pixel tiles row-major; 1 = 64x64-pixel supertiles,
                                   each handed to one XCD so neighbouring rays share that XCD's L2; 2 = the launch
                                   order planned by och_gpu_plan_views (costliest tiles first) for frames of the
-                                  planned geometry, else 0.  Dispatch order only: frames are identical */
-    OCH_OPT_BOUNCE_COMPACT = 6,/* config 5: 1 = compact each block's secondary rays into its first lanes (wave
-                                  ballot/popcount + LDS queue) before tracing them; 0 = trace each in place, the
-                                  walk started on its primary's LDS stack; 2 = per block, compact when that packs
-                                  the block's secondary rays into fewer waves than hold them, else in place */
-    OCH_OPT_CHUNK_TILES = 7,   /* schedule 2: 64-ray tiles per wave, a power of two in 1..64 (default 4) */
+                                  planned geometry, else 0; 3 = that plan grouped per XCD.  Dispatch order only:
+                                  frames are identical */
+    OCH_OPT_BOUNCE_COMPACT = 6,/* config 5: 1 (default) = compact each block's secondary rays into its first lanes
+                                  (wave ballot/popcount + LDS queue) before tracing them; 0 = trace each in place;
+                                  2 = per block, compact when that packs the block's secondary rays into fewer
+                                  waves than hold them, else in place */
     OCH_OPT_CULL = 8,          /* 1 (default) = a ray whose walk provably never enters the bounding box of the
                                   pool's voxels (och_pool_occupied_box) is recorded as the miss it would end in,
                                   without walking (camera rays: a cheaper conservative test first, before the
                                   ray's setup); exact, for launches that do not count
                                   PUSHes.  0 = every ray walks.  2 = diagnostic: launches that count PUSHes
                                   cull too, a culled ray counting 0 (the PUSHes the culled launch walks) */
-    OCH_OPT_MERGE = 9,         /* K > 0: grid launches without PUSH counts on the packed layout, with a block of
-                                  128..1024 threads, merge the block's waves every K iterations: the rays left
-                                  move into the free lanes of the fewest waves, the emptied waves exit (records
-                                  unchanged).  0 (default) = off */
     OCH_OPT_TIMING = 10,       /* per-launch timing of trace/render kernels (och_gpu_last_kernel_ms):
                                   1 (default) = recorded by the kernel's own dispatch (hipExtLaunchKernel: no
                                   packets between two launches of a stream); 2 = hipEventRecord before and
                                   after the launch; 0 = not timed */
-    OCH_OPT_PLAN = 11,         /* shape of och_gpu_plan_views' launch order (set before planning): 0 =
+    OCH_OPT_PLAN = 11          /* shape of och_gpu_plan_views' launch order (set before planning): 0 =
                                   costliest first; P in 1..99 = the costliest P % first, the rest in natural
                                   order (default 10); 100 = costliest and cheapest alternating */
-    OCH_OPT_SKIP = 12,         /* 1 = per-node voxel-box skip: a walk that descends into a node whose
-                                  voxels' bounding box (precomputed per child slot of the packed layout, built
-                                  when the option is first set, 2 B per slot) it provably never enters steps
-                                  out of it at once, as the cull ends a ray missing every voxel's box; exact
-                                  (DESIGN.md §4c), for launches that do not count PUSHes; 2 = counting
-                                  launches too (diagnostic); 0 (default) = off: the skip walks 25-40 % fewer
-                                  PUSHes yet runs 13-19 % slower on every scene measured */
-    OCH_OPT_COLUMNS = 13       /* column cull, a refinement of OCH_OPT_CULL (render / trace grid launches;
-                                  counting launches at OCH_OPT_CULL = 2 only): L (1..7) = levels of a
-                                  quadtree over the world's x-y columns holding each block's voxel z range
-                                  (built when set); a wave whose every ray provably enters no block that
-                                  holds a voxel ends those rays as the MISS without walking (exact,
-                                  DESIGN.md §4d); 0 (default) = off: the wave's walk of the quadtree costs
-                                  more than the walks it saves on the bench's views (24.7 G against 32.4 G
-                                  rays/s at L = 6) */
 } och_option;
 OCH_API int och_gpu_set_option(och_gpu_pool *pool, int option, int value);
 OCH_API int och_gpu_get_option(const och_gpu_pool *pool, int option, int *value);
@@ -206,8 +185,8 @@ OCH_API int och_gpu_get_option(const och_gpu_pool *pool, int option, int *value)
  * 100 MHz), HW_ID | XCC_ID << 32, rays finished.  NULL turns it off. */
 OCH_API int och_gpu_set_stamp_buffer(och_gpu_pool *pool, uint64_t *stamps, uint32_t capacity_waves);
 /* Diagnostics: HIP's occupancy answer (workgroups per CU) for kind 0 = render
- * grid kernel, 1 = render persistent kernel, 2 = trace grid kernel, at the
- * pool's block size and stack depth. */
+ * grid kernel or 2 = trace grid kernel, at the pool's block size and stack
+ * depth (kind 1, the retired persistent kernel, fails). */
 OCH_API int och_gpu_occupancy(const och_gpu_pool *pool, int kind, int *blocks_per_cu);
 /* Duration of the most recent trace/render kernel launched on the pool,
  * measured with HIP events on the stream it ran on (blocks until it ends).
@@ -254,7 +233,7 @@ OCH_API int och_gpu_trace_batch_tiled_dev(och_gpu_pool *pool, const float *origi
                                           int32_t *hit_direction, uint32_t *hit_voxel, float *hit_time,
                                           uint32_t *push_count);
 /* Plan the launch order of tiled batches of n rays `width` wide (block size
- * and schedule included in the key): one timed trace of these rays, then
+ * included in the key): one timed trace of these rays, then
  * costliest tiles first.  Synchronous; a plan stays valid while the rays
  * change (it orders dispatch only). */
 OCH_API int och_gpu_plan_batch_tiled(och_gpu_pool *pool, const float *origin, int origin_stride,
@@ -493,24 +472,6 @@ OCH_API void och_host_pool_free(och_host_pool *pool);
  * root_id | root_mask << 24.  out = NULL only reports *out_nodes. */
 OCH_API int och_pool_pack(const uint32_t *nodes, uint32_t n_nodes, uint32_t root, int depth, int index_base,
                           uint32_t *out, uint32_t out_capacity, uint32_t *out_nodes, uint32_t *out_root);
-/* The per-node skip's boxes (OCH_OPT_SKIP) of a packed pool (och_pool_pack's
- * output): out[8 * id + k] describes the child in slot k of node id -- the
- * bounding box of the voxels under it in its own cell, world orientation,
- * quantised outwards: bits 0-1 x lo and 2-3 (4 - x hi) in quarters, 4-7 the
- * same for y, 8-11 z lo and 12-15 (16 - z hi) in sixteenths; 0 = the whole
- * cell, 0xFFFF = no voxel.  Leaf-level and empty slots hold 0.  out holds
- * n_nodes * 8 entries.  OCH_E_INVALID above depth 20. */
-OCH_API int och_pool_slot_boxes(const uint32_t *packed, uint32_t n_nodes, uint32_t packed_root, int depth,
-                                uint16_t *out);
-/* The column cull's quadtree (OCH_OPT_COLUMNS) of a packed pool: levels
- * 1..levels, level l holding 2^l x 2^l blocks of the world's x-y columns in
- * Morton order (x in the even bits) from word (4^l - 4) / 3; each word the z
- * range of the voxels in that block column, zlo | zmax << 16 in voxel units
- * (inclusive), or 0xFFFF when it holds none.  out holds (4^(levels+1) - 4) / 3
- * words.  OCH_E_INVALID for levels outside 1..min(7, depth - 1) or depth above
- * 16. */
-OCH_API int och_pool_columns(const uint32_t *packed, uint32_t n_nodes, uint32_t packed_root, int depth, int levels,
-                             uint32_t *out);
 /* Bounding box of every non-empty leaf voxel reachable from root, in voxel
  * units: voxel (x, y, z) lies in it iff lo <= (x, y, z) < hi per axis.
  * Returns OCH_OK with lo = hi = {0, 0, 0} for a pool without voxels. */

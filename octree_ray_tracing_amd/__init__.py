@@ -7,13 +7,13 @@ liboch_gpu.so behind the C ABI of include/och_gpu.h.  This package is the
 host-side mirror of the reference interface over that ABI.
 """
 from ._lib import OchError, library_path, load
-from .builder import NodePool, build_terrain, columns, occupied_box, pack_pool, slot_boxes
+from .builder import NodePool, build_terrain, occupied_box, pack_pool
 from .editor import Editor
 from .frame import FrameGroup, RcclComm, ShardedFrame, ShardedSteps
 from .tracer import (Direction, GpuPool, HOctree, Octree, camera, deal_chunks, display_weight, device_count, device_list, host_rcp_lut,
                      rcp_from_lut, rcp_lut_error, shard_rows)
 from .voxels import VoxelData, VoxelDataError
 
-__all__ = ["OchError", "library_path", "load", "NodePool", "build_terrain", "columns", "occupied_box", "pack_pool", "slot_boxes", "Editor", "FrameGroup", "RcclComm", "ShardedFrame", "ShardedSteps", "Direction", "GpuPool",
+__all__ = ["OchError", "library_path", "load", "NodePool", "build_terrain", "occupied_box", "pack_pool", "Editor", "FrameGroup", "RcclComm", "ShardedFrame", "ShardedSteps", "Direction", "GpuPool",
            "HOctree", "Octree", "camera", "deal_chunks", "display_weight", "device_count", "device_list", "host_rcp_lut", "rcp_from_lut", "rcp_lut_error", "shard_rows",
            "VoxelData", "VoxelDataError"]

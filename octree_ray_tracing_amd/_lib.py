@@ -108,8 +108,6 @@ PROTOTYPES = {
     "och_pool_pack": (C.c_int, [_P, _u32, _u32, C.c_int, C.c_int, _P, _u32, C.POINTER(_u32), C.POINTER(_u32)]),
     "och_pool_at": (_u32, [_P, _u32, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int]),
     "och_pool_occupied_box": (C.c_int, [_P, _u32, _u32, C.c_int, C.c_int, _P, _P]),
-    "och_pool_slot_boxes": (C.c_int, [_P, _u32, _u32, C.c_int, _P]),
-    "och_pool_columns": (C.c_int, [_P, _u32, _u32, C.c_int, C.c_int, _P]),
     "och_editor_create": (C.c_int, [_P, _u32, _u32, C.c_int, _u32, C.POINTER(_P)]),
     "och_editor_destroy": (C.c_int, [_P]),
     "och_editor_set": (C.c_int, [_P, C.c_int, C.c_int, C.c_int, _u32]),

@@ -122,24 +122,6 @@ def occupied_box(nodes: np.ndarray, root: int, depth: int, index_base: int = 1):
     return tuple(lo), tuple(hi)
 
 
-def slot_boxes(packed: np.ndarray, packed_root: int, depth: int) -> np.ndarray:
-    """The per-node skip's boxes of a packed pool (och_pool_slot_boxes): uint16 (n, 8)."""
-    packed = np.ascontiguousarray(packed, np.uint32).reshape(-1, 8)
-    out = np.zeros(packed.shape, np.uint16)
-    call("och_pool_slot_boxes", packed.ctypes.data, packed.shape[0], int(packed_root), int(depth), out.ctypes.data)
-    return out
-
-
-def columns(packed: np.ndarray, packed_root: int, depth: int, levels: int) -> list:
-    """The column cull's quadtree of a packed pool (och_pool_columns): one uint32
-    array per level 1..levels, 4^l words in Morton order (zlo | zmax << 16, or 0xFFFF)."""
-    packed = np.ascontiguousarray(packed, np.uint32).reshape(-1, 8)
-    out = np.zeros(((1 << (2 * levels + 2)) - 4) // 3, np.uint32)
-    call("och_pool_columns", packed.ctypes.data, packed.shape[0], int(packed_root), int(depth), int(levels),
-         out.ctypes.data)
-    return [out[((1 << (2 * l)) - 4) // 3:((1 << (2 * l + 2)) - 4) // 3] for l in range(1, levels + 1)]
-
-
 def pack_pool(nodes: np.ndarray, root: int, depth: int, index_base: int = 1):
     """The packed device layout of a pool (och_pool_pack): (packed nodes, packed root)."""
     nodes = np.ascontiguousarray(nodes, np.uint32).reshape(-1, 8)

@@ -19,7 +19,6 @@
 namespace {
 
 constexpr uint32_t kIdLimit = 1u << 24;   // packed ids are 24 bits
-constexpr uint32_t kIdLimitMask = kIdLimit - 1;
 
 thread_local std::string g_error;
 
@@ -137,21 +136,15 @@ struct och_gpu_pool {
     hipEvent_t ev_start = nullptr, ev_stop = nullptr;
     bool timed = false;
     // schedule (och_gpu_set_option)
-    int opt_schedule = 0, opt_block = 64, opt_waves_per_cu = 32, opt_refill = 16, opt_chunk_tiles = 4;
-    int cus = 256;
-    uint32_t *d_counter = nullptr;
+    int opt_block = 64;
     uint64_t *stamps = nullptr;
     uint32_t stamp_cap = 0;
     // host mirror of the uploaded nodes (user numbering), for validating edits
     std::vector<uint32_t> mirror;
     // packed layout (see och_internal.h DevPool)
     uint32_t *d_packed = nullptr;
-    uint16_t *d_boxes = nullptr;    // per packed slot: the child's voxel box (och::pool_slot_boxes), or none
-    uint32_t *d_columns = nullptr;  // the column quadtree (och::pool_columns), or none
-    int col_levels = 0;             // its levels
     uint32_t packed_root = 0;
     uint32_t packed_nodes = 0;
-    uint32_t packed_top_ids[5] = {1, 1, 1, 1, 1};   // first id past levels 1..T
     bool packed_by_slot = false;    // d_packed numbered like d_nodes (editor flushes)
     uint64_t serial = 0;            // process-unique, never reused (och::pool_serial)
     uint64_t last_writer = 0;       // editor id of the last och::pool_commit, 0 otherwise
@@ -160,11 +153,8 @@ struct och_gpu_pool {
     int opt_tile_order = 0;
     int opt_bounce_compact = 1;
     int opt_cull = 1;
-    int opt_merge = 0;
     int opt_timing = 1;                        // OCH_OPT_TIMING
     int opt_plan = 10;                         // OCH_OPT_PLAN (shape of och_gpu_plan_views' order)
-    int opt_skip = 0;                          // OCH_OPT_SKIP (per-node voxel-box skip; boxes built on first use)
-    int opt_columns = 0;                       // OCH_OPT_COLUMNS (column cull: quadtree levels, 0 = off)
     hipEvent_t next_ev_start = nullptr;        // och_gpu_set_launch_events: the next launch's events
     hipEvent_t next_ev_stop = nullptr;
     // bounding box of the pool's voxels (voxel units, [lo, hi)), for the cull
@@ -200,21 +190,14 @@ struct och_gpu_pool {
     och::Schedule schedule() const
     {
         och::Schedule sc;
-        sc.kind = opt_schedule;
-        sc.chunk_tiles = opt_chunk_tiles;
         sc.block = opt_block;
-        sc.waves_per_cu = opt_waves_per_cu;
-        sc.refill_min = opt_refill;
         sc.tile_order = opt_tile_order;
         sc.bounce_compact = opt_bounce_compact;
-        sc.cus = cus;
-        sc.counter = d_counter;
         sc.stamps = stamps;
         sc.stamp_cap = stamp_cap;
         sc.order = nullptr;
         sc.order_n = 0;
         sc.cost = nullptr;
-        sc.merge_k = opt_merge;
         sc.ev_start = nullptr;
         sc.ev_stop = nullptr;
         return sc;
@@ -234,25 +217,11 @@ struct och_gpu_pool {
         std::memcpy(&mb, &miss_t, 4);
         p.miss_bits = mb;
         p.half_voxel = std::ldexp(1.0F, -(depth + 1));
-        for (int t = 0; t < 5; ++t) p.top_ids[t] = pk && !packed_by_slot ? packed_top_ids[t] : 1u;
         p.dim_lo = 1u << (23 - depth);
         p.dim_span = (1u << 22) - p.dim_lo;
         // 1 + k / 2^depth is an exact float for depth <= 22
         p.cull = box_any ? opt_cull : 0;
         p.cam_cull = lut_error <= och::kCameraCullRcpError ? 1 : 0;
-        // the boxes describe the breadth-first packed layout only (an editor's
-        // slot-numbered layout has none)
-        p.boxes = pk && !packed_by_slot ? d_boxes : nullptr;
-        p.skip = p.boxes ? opt_skip : 0;
-        // without boxes the kernel still issues its box load (branch-free):
-        // aim it at the node array, which spans more than 16 B per node, and
-        // skip = 0 keeps every ray's skipmask 0
-        p.box_base = p.boxes ? p.boxes : reinterpret_cast<const uint16_t *>(p.nodes);
-        // the column quadtree describes the voxels of the pool it was built
-        // from (upload_packed); an editor's writes since make it stale
-        const bool cols = p.cull && d_columns && d_packed && !packed_by_slot && !torn;
-        p.columns = cols ? d_columns : nullptr;
-        p.col_levels = cols ? col_levels : 0;
         for (int a = 0; a < 3; ++a) {
             p.cull_lo[a] = 1.0F + std::ldexp((float)box_lo[a], -depth);
             p.cull_hi[a] = 1.0F + std::ldexp((float)box_hi[a], -depth);
@@ -389,7 +358,7 @@ void set_box(och_gpu_pool *p, const uint32_t *nodes, uint32_t n_nodes)
 // alone) is simply emitted once per level.  Returns false when more than
 // 2^24 - 1 ids would be needed.
 bool pack_pool(const uint32_t *nodes, uint32_t n_nodes, uint32_t root, int depth, int base,
-               std::vector<uint32_t> &out, uint32_t &packed_root, uint32_t *top_ids = nullptr)
+               std::vector<uint32_t> &out, uint32_t &packed_root)
 {
     auto mask_of = [&](uint32_t v) {
         const uint32_t *c = nodes + (size_t)(v - base) * 8;
@@ -439,12 +408,6 @@ bool pack_pool(const uint32_t *nodes, uint32_t n_nodes, uint32_t root, int depth
             if (c[k]) id_of(c[k], level + 1, true);
         if (next > kIdLimit) return false;
     }
-    if (top_ids)
-        for (int t = 0; t < 5; ++t) {
-            uint32_t n_top = 0;
-            while (n_top < order_l.size() && order_l[n_top] <= t) ++n_top;
-            top_ids[t] = 1 + n_top;                       // ids are breadth-first, 1-based
-        }
     out.resize((size_t)next * 8, 0u);
     for (size_t q = 0; q < order_v.size(); ++q) {
         const uint32_t v = order_v[q];
@@ -460,217 +423,21 @@ bool pack_pool(const uint32_t *nodes, uint32_t n_nodes, uint32_t root, int depth
     return true;
 }
 
-}  // namespace
-
-bool och::pool_node_boxes(const uint32_t *packed, uint32_t n_nodes, uint32_t packed_root, int depth,
-                          std::vector<uint8_t> &level, std::vector<int32_t> &box)
-{
-    if (depth < 2 || depth > 24 || n_nodes < 2) return false;
-    const uint32_t root = packed_root & kIdLimitMask;
-    if (root == 0 || root >= n_nodes) return false;
-    level.assign(n_nodes, 0);
-    level[root] = 1;
-    // breadth-first ids: a parent's id is below its children's
-    for (uint32_t v = 1; v < n_nodes; ++v) {
-        if (!level[v] || level[v] >= depth) continue;
-        for (int k = 0; k < 8; ++k) {
-            const uint32_t w = packed[(size_t)v * 8 + k];
-            if (!w) continue;
-            const uint32_t c = w & kIdLimitMask;
-            if (c <= v || c >= n_nodes) return false;
-            level[c] = (uint8_t)(level[v] + 1);
-        }
-    }
-    // voxel units relative to the node's corner: [lo, hi) per axis
-    box.assign((size_t)n_nodes * 6, 0);
-    for (uint32_t v = n_nodes - 1; v >= 1; --v) {
-        if (!level[v]) continue;
-        int32_t *b = &box[(size_t)v * 6];
-        b[0] = b[1] = b[2] = INT32_MAX;
-        b[3] = b[4] = b[5] = INT32_MIN;
-        const int32_t half = 1 << (depth - level[v]);           // child size in voxels
-        for (int k = 0; k < 8; ++k) {
-            const uint32_t w = packed[(size_t)v * 8 + k];
-            if (!w) continue;
-            const int32_t *cb = level[v] == depth ? nullptr : &box[(size_t)(w & kIdLimitMask) * 6];
-            if (cb && cb[0] > cb[3]) continue;                   // an empty node holds no voxel
-            for (int a = 0; a < 3; ++a) {
-                const int32_t off = ((k >> a) & 1) * half;
-                b[a] = std::min(b[a], cb ? off + cb[a] : off);
-                b[3 + a] = std::max(b[3 + a], cb ? off + cb[3 + a] : off + 1);
-            }
-        }
-    }
-    return true;
-}
-
-// Per-slot voxel boxes of a packed pool (the per-node skip, och_internal.h
-// DevPool::boxes): for every interior slot holding child C, the bounding box
-// of the voxels under C in C's own cell, world orientation, quantised
-// outwards to quarters on x and y and sixteenths on z.
-bool och::pool_slot_boxes(const uint32_t *packed, uint32_t n_nodes, uint32_t packed_root, int depth,
-                          std::vector<uint16_t> &out)
-{
-    if (depth > kSkipMaxDepth) return false;
-    std::vector<uint8_t> level;
-    std::vector<int32_t> box;
-    if (!pool_node_boxes(packed, n_nodes, packed_root, depth, level, box)) return false;
-    out.assign((size_t)n_nodes * 8, 0);
-    for (uint32_t v = 1; v < n_nodes; ++v) {
-        if (!level[v] || level[v] >= depth) continue;
-        const int64_t size = int64_t(1) << (depth - level[v]);   // the child's cell, voxels
-        for (int k = 0; k < 8; ++k) {
-            const uint32_t w = packed[(size_t)v * 8 + k];
-            if (!w) continue;
-            const int32_t *b = &box[(size_t)(w & kIdLimitMask) * 6];
-            if (b[0] > b[3]) {                  // no voxel under the child: an empty box, the walk skips it
-                out[(size_t)v * 8 + k] = kSkipEmptyBox;
-                continue;
-            }
-            uint32_t code = 0;
-            for (int a = 0; a < 3; ++a) {
-                const int64_t q = a < 2 ? 4 : 16, bits = a < 2 ? 2 : 4;
-                const int64_t lo = (int64_t)b[a] * q / size;                  // floor (b >= 0)
-                const int64_t hi = ((int64_t)b[3 + a] * q + size - 1) / size; // ceil
-                code |= (uint32_t)lo << (4 * a) | (uint32_t)(q - hi) << (4 * a + bits);
-            }
-            out[(size_t)v * 8 + k] = (uint16_t)code;
-        }
-    }
-    return true;
-}
-
-// The column quadtree (DevPool::columns): for every block of 2^(depth - levels)
-// x 2^(depth - levels) voxel columns, the z range of its voxels, from the
-// exact node boxes of the tree's nodes at level levels + 1 (their cells are
-// the block's cubes), then each coarser level as the union of its 4 blocks.
-bool och::pool_columns(const uint32_t *packed, uint32_t n_nodes, uint32_t packed_root, int depth, int levels,
-                       std::vector<uint32_t> &out)
-{
-    if (levels < 1 || levels > kColumnMaxLevels || levels > depth - 1 || depth > kColumnMaxDepth) return false;
-    std::vector<uint8_t> level;
-    std::vector<int32_t> box;
-    if (!pool_node_boxes(packed, n_nodes, packed_root, depth, level, box)) return false;
-    const uint32_t G = 1u << levels;
-    std::vector<int32_t> lo(G * G, INT32_MAX), hi(G * G, INT32_MIN);     // [lo, hi) per block column
-    const int32_t cube = 1 << (depth - levels);                           // a level-(levels + 1) node's cell
-    struct Item {
-        uint32_t v;
-        int L;
-        uint32_t x, y, z;
-    };
-    std::vector<Item> todo{{packed_root & kIdLimitMask, 1, 0, 0, 0}};
-    while (!todo.empty()) {
-        const Item it = todo.back();
-        todo.pop_back();
-        const int32_t *b = &box[(size_t)it.v * 6];
-        if (b[2] > b[5]) continue;                                        // no voxel under this node
-        if (it.L == levels + 1) {
-            const uint32_t c = it.y * G + it.x;
-            lo[c] = std::min(lo[c], (int32_t)it.z * cube + b[2]);
-            hi[c] = std::max(hi[c], (int32_t)it.z * cube + b[5]);
-            continue;
-        }
-        for (int k = 0; k < 8; ++k) {
-            const uint32_t w = packed[(size_t)it.v * 8 + k];
-            if (w) todo.push_back({w & kIdLimitMask, it.L + 1, 2 * it.x + (k & 1), 2 * it.y + ((k >> 1) & 1),
-                                   2 * it.z + ((k >> 2) & 1)});
-        }
-    }
-    auto morton = [](uint32_t x, uint32_t y) {
-        uint32_t m = 0;
-        for (int i = 0; i < kColumnMaxLevels; ++i) m |= ((x >> i) & 1u) << (2 * i) | ((y >> i) & 1u) << (2 * i + 1);
-        return m;
-    };
-    auto word = [](int32_t l, int32_t h) { return l < h ? (uint32_t)l | (uint32_t)(h - 1) << 16 : 0xFFFFu; };
-    auto off = [](int l) { return ((size_t(1) << (2 * l)) - 4) / 3; };
-    out.assign(off(levels + 1), 0xFFFFu);
-    for (uint32_t y = 0; y < G; ++y)
-        for (uint32_t x = 0; x < G; ++x) out[off(levels) + morton(x, y)] = word(lo[y * G + x], hi[y * G + x]);
-    for (int l = levels - 1; l >= 1; --l)
-        for (size_t m = 0; m < (size_t(1) << (2 * l)); ++m) {
-            int32_t zl = INT32_MAX, zh = INT32_MIN;
-            for (int k = 0; k < 4; ++k) {
-                const uint32_t w = out[off(l + 1) + 4 * m + k];
-                if ((w & 0xFFFFu) > (w >> 16)) continue;                  // empty
-                zl = std::min(zl, (int32_t)(w & 0xFFFFu));
-                zh = std::max(zh, (int32_t)(w >> 16) + 1);
-            }
-            out[off(l) + m] = word(zl, zh);
-        }
-    return true;
-}
-
-namespace {
-
-// The per-node skip's boxes (OCH_OPT_SKIP) of the packed pool, built when the
-// skip is first switched on: 2 B per slot, 80 MB at depth 12, that a pool
-// which never skips does not carry.
-int upload_boxes(och_gpu_pool *p, const std::vector<uint32_t> &packed)
-{
-    std::vector<uint16_t> boxes;
-    if (!och::pool_slot_boxes(packed.data(), p->packed_nodes, p->packed_root, p->depth, boxes)) return OCH_OK;
-    OCH_HIP(hipMalloc(&p->d_boxes, boxes.size() * 2));
-    OCH_HIP(hipMemcpy(p->d_boxes, boxes.data(), boxes.size() * 2, hipMemcpyHostToDevice));
-    return OCH_OK;
-}
-
-int ensure_boxes(och_gpu_pool *p)
-{
-    if (p->d_boxes || !p->d_packed || p->packed_by_slot) return OCH_OK;
-    std::vector<uint32_t> packed((size_t)p->packed_nodes * 8);
-    OCH_HIP(hipMemcpy(packed.data(), p->d_packed, packed.size() * 4, hipMemcpyDeviceToHost));
-    return upload_boxes(p, packed);
-}
-
-// The column quadtree (OCH_OPT_COLUMNS levels) of the packed pool.
-int upload_columns(och_gpu_pool *p, const std::vector<uint32_t> &packed)
-{
-    if (p->d_columns) OCH_HIP(hipFree(p->d_columns));
-    p->d_columns = nullptr;
-    p->col_levels = 0;
-    const int levels = std::min(p->opt_columns, p->depth - 1);
-    std::vector<uint32_t> cols;
-    if (levels < 1 || !och::pool_columns(packed.data(), p->packed_nodes, p->packed_root, p->depth, levels, cols))
-        return OCH_OK;
-    OCH_HIP(hipMalloc(&p->d_columns, cols.size() * 4));
-    OCH_HIP(hipMemcpy(p->d_columns, cols.data(), cols.size() * 4, hipMemcpyHostToDevice));
-    p->col_levels = levels;
-    return OCH_OK;
-}
-
-int ensure_columns(och_gpu_pool *p)
-{
-    if (!p->d_packed || p->packed_by_slot) return OCH_OK;
-    // launches in flight on any stream may still read the quadtree being replaced
-    if (p->d_columns) OCH_HIP(hipDeviceSynchronize());
-    std::vector<uint32_t> packed((size_t)p->packed_nodes * 8);
-    OCH_HIP(hipMemcpy(packed.data(), p->d_packed, packed.size() * 4, hipMemcpyDeviceToHost));
-    return upload_columns(p, packed);
-}
-
 int upload_packed(och_gpu_pool *p, const uint32_t *nodes, uint32_t n_nodes)
 {
     std::vector<uint32_t> packed;
     uint32_t proot = 0;
     if (p->d_packed) OCH_HIP(hipFree(p->d_packed));
-    if (p->d_boxes) OCH_HIP(hipFree(p->d_boxes));
-    if (p->d_columns) OCH_HIP(hipFree(p->d_columns));
     p->d_packed = nullptr;
-    p->d_boxes = nullptr;
-    p->d_columns = nullptr;
-    p->col_levels = 0;
     p->packed_nodes = 0;
     p->packed_by_slot = false;
-    if (!pack_pool(nodes, n_nodes, p->root, p->depth, p->index_base, packed, proot, p->packed_top_ids))
+    if (!pack_pool(nodes, n_nodes, p->root, p->depth, p->index_base, packed, proot))
         return OCH_OK;   // raw only
     OCH_HIP(hipMalloc(&p->d_packed, packed.size() * 4));
     OCH_HIP(hipMemcpy(p->d_packed, packed.data(), packed.size() * 4, hipMemcpyHostToDevice));
     p->packed_root = proot;
     p->packed_nodes = (uint32_t)(packed.size() / 8);
-    if (p->opt_columns)
-        if (int st = upload_columns(p, packed)) return st;
-    return p->opt_skip ? upload_boxes(p, packed) : OCH_OK;
+    return OCH_OK;
 }
 
 // Largest relative error |r * x - 1| of the table model over x in [-2, -1):
@@ -796,10 +563,6 @@ OCH_API int och_gpu_pool_create(const uint32_t *nodes, uint32_t n_nodes, uint32_
     set_box(p, nodes, n_nodes);
     st = upload_packed(p, nodes, n_nodes);
     if (st != OCH_OK) return bail(st);
-    hipDeviceProp_t prop;
-    if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
-        p->cus = prop.multiProcessorCount;
-    if (hipMalloc(&p->d_counter, 256) != hipSuccess) return bail(fail(OCH_E_NOMEM, "counter allocation failed"));
     if (hipStreamCreateWithFlags(&p->own_stream, hipStreamNonBlocking) != hipSuccess ||
         // timing only: no system-scope release at the timed kernel's end
         hipEventCreateWithFlags(&p->ev_start, hipEventDisableSystemFence) != hipSuccess ||
@@ -824,8 +587,6 @@ OCH_API int och_gpu_pool_destroy(och_gpu_pool *p)
     if (p->use_ext) (void)hipStreamSynchronize(p->ext_stream);
     if (p->d_nodes) (void)hipFree(p->d_nodes);
     if (p->d_packed) (void)hipFree(p->d_packed);
-    if (p->d_boxes) (void)hipFree(p->d_boxes);
-    if (p->d_columns) (void)hipFree(p->d_columns);
     if (p->d_lut) (void)hipFree(p->d_lut);
     if (p->d_palette) (void)hipFree(p->d_palette);
     if (p->d_code_table) (void)hipFree(p->d_code_table);
@@ -836,7 +597,6 @@ OCH_API int och_gpu_pool_destroy(och_gpu_pool *p)
         if (o) (void)hipFree(o);
     for (uint32_t *o : p->d_order_xcd)
         if (o) (void)hipFree(o);
-    if (p->d_counter) (void)hipFree(p->d_counter);
     if (p->d_chunk_map) (void)hipFree(p->d_chunk_map);
     if (p->d_owner) (void)hipFree(p->d_owner);
     if (p->ev_start) (void)hipEventDestroy(p->ev_start);
@@ -1078,25 +838,21 @@ OCH_API int och_gpu_set_stream(och_gpu_pool *p, void *stream)
     return OCH_OK;
 }
 
+// Option ids retired in round 5 (measured slower on every scene, DESIGN.md
+// §8): 0 schedule (persistent / refill), 2 waves per CU, 3 refill, 7 chunk
+// tiles, 9 merge, 12 per-node skip, 13 column cull.  Their ids stay unused.
+static int retired_option(int option)
+{
+    return fail(OCH_E_INVALID, "option %d was retired (the grid schedule alone remains; DESIGN.md section 8)", option);
+}
+
 OCH_API int och_gpu_set_option(och_gpu_pool *p, int option, int value)
 {
     if (!p) return fail(OCH_E_INVALID, "pool is NULL");
     switch (option) {
-    case OCH_OPT_SCHEDULE:
-        if (value < 0 || value > 2) return fail(OCH_E_INVALID, "schedule must be 0, 1 or 2");
-        p->opt_schedule = value;
-        return OCH_OK;
     case OCH_OPT_BLOCK:
         if (value < 64 || value > 1024 || value % 64) return fail(OCH_E_INVALID, "block %d", value);
         p->opt_block = value;
-        return OCH_OK;
-    case OCH_OPT_WAVES_PER_CU:
-        if (value < 1 || value > 32) return fail(OCH_E_INVALID, "waves per CU %d outside 1..32", value);
-        p->opt_waves_per_cu = value;
-        return OCH_OK;
-    case OCH_OPT_REFILL:
-        if (value < 1 || value > 64) return fail(OCH_E_INVALID, "refill %d outside 1..64", value);
-        p->opt_refill = value;
         return OCH_OK;
     case OCH_OPT_LAYOUT:
         if (value != 0 && value != 1) return fail(OCH_E_INVALID, "layout must be 0 or 1");
@@ -1111,18 +867,9 @@ OCH_API int och_gpu_set_option(och_gpu_pool *p, int option, int value)
         if (value < 0 || value > 2) return fail(OCH_E_INVALID, "bounce compaction must be 0, 1 or 2");
         p->opt_bounce_compact = value;
         return OCH_OK;
-    case OCH_OPT_CHUNK_TILES:
-        if (value < 1 || value > 64 || (value & (value - 1)))
-            return fail(OCH_E_INVALID, "chunk tiles %d: a power of two in 1..64", value);
-        p->opt_chunk_tiles = value;
-        return OCH_OK;
     case OCH_OPT_CULL:
         if (value < 0 || value > 2) return fail(OCH_E_INVALID, "cull must be 0, 1 or 2");
         p->opt_cull = value;
-        return OCH_OK;
-    case OCH_OPT_MERGE:
-        if (value < 0 || value > 4096) return fail(OCH_E_INVALID, "merge rounds %d outside 0..4096", value);
-        p->opt_merge = value;
         return OCH_OK;
     case OCH_OPT_TIMING:
         if (value < 0 || value > 2) return fail(OCH_E_INVALID, "timing must be 0, 1 or 2");
@@ -1132,23 +879,8 @@ OCH_API int och_gpu_set_option(och_gpu_pool *p, int option, int value)
         if (value < 0 || value > 100) return fail(OCH_E_INVALID, "plan shape must be 0..100");
         p->opt_plan = value;
         return OCH_OK;
-    case OCH_OPT_COLUMNS:
-        if (value < 0 || value > och::kColumnMaxLevels)
-            return fail(OCH_E_INVALID, "columns must be 0..%d quadtree levels", och::kColumnMaxLevels);
-        if (value != p->opt_columns) {
-            DeviceGuard g(p->device);
-            p->opt_columns = value;
-            return ensure_columns(p);
-        }
-        return OCH_OK;
-    case OCH_OPT_SKIP:
-        if (value < 0 || value > 2) return fail(OCH_E_INVALID, "skip must be 0, 1 or 2");
-        p->opt_skip = value;
-        if (value) {
-            DeviceGuard g(p->device);
-            return ensure_boxes(p);
-        }
-        return OCH_OK;
+    case 0: case 2: case 3: case 7: case 9: case 12: case 13:
+        return retired_option(option);
     default:
         return fail(OCH_E_INVALID, "unknown option %d", option);
     }
@@ -1158,20 +890,15 @@ OCH_API int och_gpu_get_option(const och_gpu_pool *p, int option, int *value)
 {
     if (!p || !value) return fail(OCH_E_INVALID, "NULL argument");
     switch (option) {
-    case OCH_OPT_SCHEDULE: *value = p->opt_schedule; return OCH_OK;
     case OCH_OPT_BLOCK: *value = p->opt_block; return OCH_OK;
-    case OCH_OPT_WAVES_PER_CU: *value = p->opt_waves_per_cu; return OCH_OK;
-    case OCH_OPT_REFILL: *value = p->opt_refill; return OCH_OK;
     case OCH_OPT_LAYOUT: *value = (p->opt_layout == 1 && p->d_packed) ? 1 : 0; return OCH_OK;
     case OCH_OPT_TILE_ORDER: *value = p->opt_tile_order; return OCH_OK;
     case OCH_OPT_BOUNCE_COMPACT: *value = p->opt_bounce_compact; return OCH_OK;
-    case OCH_OPT_CHUNK_TILES: *value = p->opt_chunk_tiles; return OCH_OK;
     case OCH_OPT_CULL: *value = p->opt_cull; return OCH_OK;
-    case OCH_OPT_MERGE: *value = p->opt_merge; return OCH_OK;
     case OCH_OPT_TIMING: *value = p->opt_timing; return OCH_OK;
     case OCH_OPT_PLAN: *value = p->opt_plan; return OCH_OK;
-    case OCH_OPT_SKIP: *value = p->opt_skip; return OCH_OK;
-    case OCH_OPT_COLUMNS: *value = p->opt_columns; return OCH_OK;
+    case 0: case 2: case 3: case 7: case 9: case 12: case 13:
+        return retired_option(option);
     default: return fail(OCH_E_INVALID, "unknown option %d", option);
     }
 }
@@ -1316,7 +1043,7 @@ int tiled_args(const och_gpu_pool *p, const float *origin, int origin_stride, co
 // The key of a tiled batch's launch plan: the geometry and the block size.
 void batch_key(const och_gpu_pool *p, uint32_t n, uint32_t width, int64_t key[9])
 {
-    const int64_t k[9] = {n, width, p->opt_block, p->opt_schedule, 0, 0, 0, 0, 0};
+    const int64_t k[9] = {n, width, p->opt_block, 0, 0, 0, 0, 0, 0};
     std::memcpy(key, k, sizeof k);
 }
 
@@ -1332,7 +1059,7 @@ OCH_API int och_gpu_trace_batch_tiled_dev(och_gpu_pool *p, const float *origin, 
     int ts;
     och::Schedule sc = timed_schedule(p, ts);
     if (ts) return ts;
-    if (p->opt_tile_order >= 2 && p->opt_schedule == 0 && p->d_order[2]) {
+    if (p->opt_tile_order >= 2 && p->d_order[2]) {
         int64_t key[9];
         batch_key(p, n, width, key);
         if (std::memcmp(key, p->plan_key[2], sizeof key) == 0) {
@@ -1360,10 +1087,8 @@ OCH_API int och_gpu_plan_batch_tiled(och_gpu_pool *p, const float *origin, int o
     uint32_t *cost = reinterpret_cast<uint32_t *>(base + 3 * out_bytes);
     OCH_HIP(hipMemsetAsync(cost, 0xFF, (size_t)max_blocks * 4, p->stream()));
     och::Schedule sc = p->schedule();
-    sc.kind = 0;
     sc.tile_order = 0;
     sc.cost = cost;
-    sc.merge_k = 0;
     OCH_HIP(och::launch_trace_batch_tiled(p->dev(), origin, origin_stride, dirs, n, width,
                                           reinterpret_cast<int32_t *>(base), reinterpret_cast<uint32_t *>(base + out_bytes),
                                           reinterpret_cast<uint32_t *>(base + 2 * out_bytes), nullptr, sc, p->stream()));
@@ -1510,7 +1235,7 @@ int render_views(och_gpu_pool *p, const och_camera *cams, int n_views, uint32_t 
     och::Schedule sc = timed_schedule(p, ts);
     if (ts) return ts;
     const int which = bounce ? 1 : 0;
-    if (p->opt_tile_order >= 2 && (bounce || p->opt_schedule == 0) && p->d_order[which]) {
+    if (p->opt_tile_order >= 2 && p->d_order[which]) {
         const int64_t key[9] = {cams[0].width, cams[0].height, n_views, row_chunk, shard, n_shards, p->opt_block,
                                 bounce ? p->opt_bounce_compact : 0, dealt ? (int64_t)p->deal_serial : 0};
         if (std::memcmp(key, p->plan_key[which], sizeof key) == 0) {
@@ -1598,10 +1323,8 @@ OCH_API int och_gpu_plan_views(och_gpu_pool *p, const och_camera *cams, int n_vi
     for (int which = 0; which < 2; ++which) {
         OCH_HIP(hipMemsetAsync(cost, 0xFF, (size_t)max_blocks * 4, p->stream()));
         och::Schedule sc = p->schedule();
-        sc.kind = 0;
         sc.tile_order = 0;
         sc.cost = cost;
-        sc.merge_k = 0;                       // costs come from the plain grid kernel (same grid)
         if (which == 0)
             OCH_HIP(och::launch_render(p->dev(), f, sc, p->stream()));
         else
@@ -1749,7 +1472,7 @@ OCH_API int och_gpu_chunk_costs(och_gpu_pool *p, const och_camera *cams, int n_v
     const uint32_t tiles_x = (uint32_t)(W + 7) / 8, tiles_y = (uint32_t)(H + 7) / 8;
     // tiles per workgroup exactly as launch_as sizes the grid kernel's grid
     const uint32_t tiles = (uint32_t)n_views * tiles_x * tiles_y,
-                   per_block = (uint32_t)p->opt_block / 64 * (och::kDualRays ? 2u : 1u);
+                   per_block = (uint32_t)p->opt_block / 64;
     const uint32_t n_blocks = (tiles + per_block - 1) / per_block;
     const size_t frame_bytes = ((size_t)n_views * H * W * 4 + 255) & ~(size_t)255;
     int st = ensure_scratch(p, frame_bytes + (size_t)n_blocks * 4);
@@ -1767,15 +1490,12 @@ OCH_API int och_gpu_chunk_costs(och_gpu_pool *p, const och_camera *cams, int n_v
     f.n_shards = 1;
     f.slice_rows = H;
     f.chunk_map = nullptr;
-    // The plain grid kernel writes the costs (the merging kernel writes none,
-    // ADVICE r3): every launched workgroup overwrites its 0xFFFFFFFF, so a
+    // The grid kernel writes the costs: every launched workgroup overwrites its 0xFFFFFFFF, so a
     // block the launch did not cover is caught below instead of being read as
     // uninitialised scratch.
     och::Schedule sc = p->schedule();
-    sc.kind = 0;
     sc.tile_order = 0;
     sc.cost = cost;
-    sc.merge_k = 0;
     OCH_HIP(hipMemsetAsync(cost, 0xFF, (size_t)n_blocks * 4, p->stream()));
     OCH_HIP(och::launch_render(p->dev(), f, sc, p->stream()));
     std::vector<uint32_t> c(n_blocks);
@@ -2008,29 +1728,6 @@ OCH_API int och_pool_pack(const uint32_t *nodes, uint32_t n_nodes, uint32_t root
         if (out_capacity < *out_nodes) return fail(OCH_E_CAPACITY, "output holds %u nodes, %u needed", out_capacity, *out_nodes);
         std::memcpy(out, packed.data(), packed.size() * 4);
     }
-    return OCH_OK;
-}
-
-OCH_API int och_pool_slot_boxes(const uint32_t *packed, uint32_t n_nodes, uint32_t packed_root, int depth,
-                                uint16_t *out)
-{
-    if (!packed || !out || n_nodes < 2) return fail(OCH_E_INVALID, "bad slot-box arguments");
-    std::vector<uint16_t> boxes;
-    if (!och::pool_slot_boxes(packed, n_nodes, packed_root, depth, boxes))
-        return fail(OCH_E_INVALID, "no slot boxes for this pool (depth %d above %d, or not a breadth-first packed pool)",
-                    depth, och::kSkipMaxDepth);
-    std::memcpy(out, boxes.data(), boxes.size() * 2);
-    return OCH_OK;
-}
-
-OCH_API int och_pool_columns(const uint32_t *packed, uint32_t n_nodes, uint32_t packed_root, int depth, int levels,
-                             uint32_t *out)
-{
-    if (!packed || !out || n_nodes < 2) return fail(OCH_E_INVALID, "bad column arguments");
-    std::vector<uint32_t> cols;
-    if (!och::pool_columns(packed, n_nodes, packed_root, depth, levels, cols))
-        return fail(OCH_E_INVALID, "no column quadtree of %d levels for this pool (depth %d)", levels, depth);
-    std::memcpy(out, cols.data(), cols.size() * 4);
     return OCH_OK;
 }
 

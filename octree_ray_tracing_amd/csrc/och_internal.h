@@ -29,7 +29,6 @@ struct DevPool {
     int32_t lut_shift;
     uint32_t miss_bits;     // hit_time bits of a miss (+INF or +0.0)
     float half_voxel;       // voxel_dim / 2 = 2^-(depth+1) (ORT/och_h_octree.h:28), bounce origins
-    uint32_t top_ids[5];    // packed layout: ids below top_ids[T] belong to levels 1..T (OCH_LDS_TOP)
     uint32_t dim_lo;        // child-size bit at the leaf level, 1 << (23 - depth)
     uint32_t dim_span;      // (1 << 22) - dim_lo: a walk is active while dim - dim_lo <= dim_span
     // Occupied-box cull (OCH_OPT_CULL, och_kernels.hip ray_cull): the bounding
@@ -40,44 +39,7 @@ struct DevPool {
     // budgets the RCPPS table's relative error: 1 only when the uploaded
     // table's maximum error is within kCameraCullRcpError (och_api.cpp).
     int32_t cam_cull;
-    // Per-node voxel-box skip (OCH_OPT_SKIP; och_kernels.hip ray_skip_node):
-    // per packed slot, the voxel box of its child (och::pool_slot_boxes), or
-    // null; skip as OCH_OPT_SKIP (0 when boxes is null).
-    const uint16_t *boxes;
-    int32_t skip;
-    const uint16_t *box_base;   // boxes, or the node array when there are none (the load's address)
-    // Column cull (OCH_OPT_COLUMNS; och_kernels.hip column_cull_wave): a
-    // quadtree over the world's x-y columns, levels 1..col_levels (2^l x 2^l
-    // blocks at level l, Morton order, level l at (4^l - 1) / 3 - 1 words from
-    // the start), each word the z range of the voxels in that block column,
-    // zlo | zmax << 16 in voxel units (zlo > zmax: none); null when off.
-    const uint32_t *columns;
-    int32_t col_levels;
 };
-
-// Per-slot voxel boxes (DevPool::boxes): x and y in quarters of the child's
-// cell, z in sixteenths, each as lo and (Q - hi): bits 0-1 x lo, 2-3 x, 4-5 y
-// lo, 6-7 y, 8-11 z lo, 12-15 z.  0 = the whole cell; kSkipEmptyBox = no voxel.
-// Depths above kSkipMaxDepth carry none (a sixteenth of the leaf-parent cell
-// must be whole mantissa bits).
-constexpr int kSkipMaxDepth = 20;
-constexpr uint16_t kSkipEmptyBox = 0xFFFF;
-bool pool_slot_boxes(const uint32_t *packed, uint32_t n_nodes, uint32_t packed_root, int depth,
-                     std::vector<uint16_t> &out);
-
-// Exact voxel boxes of every node of a packed pool (the bottom-up pass both
-// the skip's slot boxes and the column quadtree start from): level[v] (1 =
-// root, 0 = unreachable) and box[6 v ..] = lo x, y, z, hi x, y, z in voxel
-// units relative to the node's corner, [lo, hi) (lo > hi: no voxel).
-bool pool_node_boxes(const uint32_t *packed, uint32_t n_nodes, uint32_t packed_root, int depth,
-                     std::vector<uint8_t> &level, std::vector<int32_t> &box);
-
-// The column quadtree (DevPool::columns) of a packed pool, levels 1..levels
-// (levels <= depth - 1, depth <= kColumnMaxDepth); false when it has none.
-constexpr int kColumnMaxDepth = 16;
-constexpr int kColumnMaxLevels = 7;
-bool pool_columns(const uint32_t *packed, uint32_t n_nodes, uint32_t packed_root, int depth, int levels,
-                  std::vector<uint32_t> &out);
 
 // Largest RCPPS-table relative error for which camera_proven_miss is sound
 // (och_kernels.hip has the budget: per-axis factors within 2^-9 of 1 against
@@ -158,35 +120,20 @@ struct DevFrame {
     const int32_t *chunk_map; // row deal: this shard's global chunk per local chunk (-1 = padding), or null
 };
 
-// OCH_DUAL builds: the grid kernel walks two rays per lane (two 8x8 tiles per
-// wave), so a workgroup covers twice the tiles (och_gpu_chunk_costs).
-#ifndef OCH_DUAL
-#define OCH_DUAL 0
-#endif
-constexpr bool kDualRays = OCH_DUAL != 0;
-
 // Threads per workgroup of the config-5 (bounce) kernels: compaction spans
 // the block's 4 waves.
 constexpr int kBounceBlock = 256;
 
 // How trace/render launches are scheduled (och_gpu_set_option).
 struct Schedule {
-    int kind;               // 0 grid, 1 persistent (resident waves pulling rays from *counter),
-                            // 2 grid with lane refill (each wave walks a chunk of chunk_tiles tiles)
-    int chunk_tiles;        // refill: 8x8 tiles (64 rays each) per wave
     int block;              // threads per workgroup (multiple of 64)
-    int waves_per_cu;       // persistent grid size per CU
-    int refill_min;         // persistent / refill: refill once this many lanes of a wave are idle
-    int tile_order;         // camera rays: 0 row-major 8x8 tiles, 1 supertiles grouped per XCD
+    int tile_order;         // camera rays: 0 row-major 8x8 tiles, 1 supertiles grouped per XCD, 2 planned order
     int bounce_compact;     // config 5: compact the block's secondary rays into its first lanes
-    int cus;                // compute units of the device
-    uint32_t *counter;      // device ray counter (persistent)
     uint64_t *stamps;       // optional per-wave residency records
     uint32_t stamp_cap;
-    const uint32_t *order;  // grid: optional workgroup permutation (och_gpu_plan_views)
+    const uint32_t *order;  // optional workgroup permutation (och_gpu_plan_views)
     uint32_t order_n;       // entries in *order: a launch whose grid differs runs in natural order
-    uint32_t *cost;         // grid: optional per-workgroup duration output (the planning launch)
-    int merge_k;            // grid, packed, no PUSH counts: in-block wave merging every merge_k iterations (0 off)
+    uint32_t *cost;         // optional per-workgroup duration output (the planning launch)
     hipEvent_t ev_start;    // optional: recorded by the traversal kernel's own dispatch (hipExtLaunchKernel)
     hipEvent_t ev_stop;
 };
@@ -199,8 +146,8 @@ hipError_t launch_trace_batch(const DevPool &p, const float *origin, int origin_
 hipError_t launch_trace_batch_tiled(const DevPool &p, const float *origin, int origin_stride, const float *dirs,
                                     uint32_t n, uint32_t width, int32_t *hit_dir, uint32_t *hit_voxel,
                                     uint32_t *hit_time, uint32_t *push_count, const Schedule &sc, hipStream_t stream);
-// hipOccupancyMaxActiveBlocksPerMultiprocessor of kind 0 render-grid,
-// 1 render-persistent, 2 trace-grid, at this block size and stack depth.
+// hipOccupancyMaxActiveBlocksPerMultiprocessor of kind 0 render grid or
+// 2 trace grid, at this block size and stack depth.
 hipError_t occupancy_blocks_per_cu(int kind, int block, int depth, int *blocks);
 // Config 5: primary ray, then one mirrored secondary ray per hit (see
 // bounce_ray in och_kernels.hip); secondary records get direction -1 when the

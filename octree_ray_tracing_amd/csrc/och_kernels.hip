@@ -1,25 +1,28 @@
 // och_kernels.hip -- gfx950 (CDNA4) kernels of the SVO-DAG ray caster.
 //
 // One ray per lane of a 64-wide wavefront.  Per-ray state (reflected-frame
-// position bits, ray coefficients, child index, level) lives in VGPRs; the
-// parent stack lives in LDS, lane-strided so a wave's 64 pushes hit 64
+// position bits, ray coefficients, child index, child size) lives in VGPRs;
+// the parent stack lives in LDS, lane-strided so a wave's 64 pushes hit 64
 // distinct banks.  Every floating-point step reproduces the reference's SSE
 // sequence bit for bit: fused only where the reference calls _mm_fmadd_ps,
 // RCPPS emulated from a host-captured table, x86's default NaN restored
 // before the unsigned t compare, denormal masks compared as integers.
 // Build with -ffp-contract=off and without denormal flushing.
 //
-// Three schedules share the traversal:
-//   grid       -- one ray per thread, the hardware dispatcher balances waves;
-//   refill     -- one wave per chunk of a few tiles; finished lanes take the
-//                 chunk's next rays whenever enough of them are idle;
-//   persistent -- a resident grid of waves pulls rays from a device counter;
-//                 when enough lanes of a wave have finished (ballot +
-//                 popcount), one atomic refills them, so no lane idles while
-//                 its wave's slowest ray is still walking the DAG.
-// Two ray sources (a ray array, or the camera of tree_camera::update_position
-// mapped 8x8-pixel tile per wave) and two sinks (hit records, or the shaded
-// RGBA8 framebuffer of update_image) make up trace_batch and render.
+// One schedule: a grid of one ray per thread, the hardware dispatcher
+// balancing waves, in an optional cost-planned workgroup order.  Three ray
+// sources (a ray array, the same rays as an image walked 8x8 tile per wave,
+// or the camera of tree_camera::update_position mapped 8x8-pixel tile per
+// wave) and the sinks (hit records, the shaded RGBA8 framebuffer of
+// update_image, or 1-byte colour codes for the multi-GPU exchange) make up
+// trace_batch and render.  Config 5 (secondary rays) compacts each block's
+// bounced rays through an LDS queue (ballot + popcount).
+//
+// Arms measured and retired (persistent and refill schedules, in-block wave
+// merging, the per-node voxel-box skip, the column cull, LDS-resident top
+// levels, two rays per lane, the step-run walk, the secondary walk restarted
+// on the primary's stack, packed FMAs, non-temporal frame stores) are kept as
+// a diff under profiles/r05/retired/ (DESIGN.md §8).
 #include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -43,11 +46,6 @@ namespace och {
 namespace {
 
 constexpr uint32_t kX86DefaultNaN = 0xFFC00000u;
-
-typedef float float2v __attribute__((ext_vector_type(2)));
-#ifndef OCH_PK_FMA
-#define OCH_PK_FMA 0
-#endif
 
 constexpr int kMaxViews = OCH_MAX_VIEWS;
 
@@ -82,29 +80,24 @@ struct Ray {
     uint32_t inv;         // direction-sign mask (1 = positive) | 24: idx ^ inv = 24 + child index,
                           // the bit of that child in a packed slot word
     uint32_t idx;         // child index bits at the current level
-    uint32_t dim;         // mantissa bit of the current child size
+    uint32_t dim;         // mantissa bit of the current child size: level L <-> 1 << (23 - L)
     uint32_t cur;         // the current node: packed slot word (id | child mask << 24), or raw index
     uint32_t *sp;         // this lane's LDS stack slot for the current level (parents below it)
-    uint32_t *sp23;       // sp at dim = 1 (slot 23): sp = sp23 - ctz(dim) * stride (OCH_POP_CHAIN)
+    uint32_t *sp23;       // sp at dim = 1 (slot 23): sp = sp23 - ctz(dim) * stride (the POP chain)
     uint32_t t_min;       // bits of the entry t of the current cell
     uint32_t min_axis;    // 1, 2, 4 (last STEP axis) or 8 (none yet)
-    uint32_t child;       // slot word loaded by the last PUSH (pending); the voxel id after a hit
-    int level;            // 1..depth while walking; 0 after a miss, depth + 1 after a hit
-    uint32_t mode;        // kAtPush (or finished), kStepping, kPending
+    uint32_t child;       // raw layout: slot word loaded by the last PUSH (pending); the voxel id after a hit
+    uint32_t mode;        // see below
     uint32_t push;
-    uint32_t box;         // the voxel box of the node the last descent entered (OCH_NODE_SKIP), else 0
-    uint32_t skipmask;    // 0xFFFF when the per-node skip is exact for this ray, else 0
 };
 
-// Ray phase: due to PUSH (or finished), due to STEP (after a failed PUSH or a
-// POP), or a PUSH found its child and the slot word is in flight.  In the
-// merged loop "due to PUSH" is any of 1, 2, 4 (the advanced axis, see
-// ray_phase_step), so kStepping is 0 and kPending lies outside the axis bits;
-// the encoding saves the phase copies at the loop's joins (2 VALU per
-// iteration, +0.6 % pipelined, profiles/r02/ab/ab_mode.txt).
+// Ray phase.  Packed layout (one merged PUSH + descend phase): kStepping (0)
+// when due to STEP, any nonzero value when due to PUSH -- the advanced axis
+// (1, 2, 4) or the present bit, so no phase copies are made at the loop's
+// joins (2 VALU per iteration, +0.6 % pipelined, profiles/r02/ab/ab_mode.txt).
+// Raw layout (three phases): kAtPush, kStepping, or kPending (a PUSH's slot
+// load is in flight).
 constexpr uint32_t kAtPush = 1, kStepping = 0, kPending = 8;
-
-__device__ __forceinline__ void set_mode(Ray &r, uint32_t m) { r.mode = m; }
 
 // The phase is one VGPR value, opaque to the compiler at each test, so a
 // phase test is one compare; as two bools the compiler carried lane masks
@@ -115,97 +108,30 @@ __device__ __forceinline__ bool in_mode(Ray &r, uint32_t m)
     return r.mode == m;
 }
 
-#ifndef OCH_NODE_SKIP
-#define OCH_NODE_SKIP 1
-#endif
-__host__ __device__ __forceinline__ bool skip_on(const DevPool &P, bool count)
-{
-    return OCH_NODE_SKIP && P.boxes && (count ? P.skip == 2 : P.skip != 0);
-}
-// The walk's layout template argument (kPacked): 0 the pointer pool, 1 the
-// packed pool, kPackedSkip the packed pool with the per-node skip.  The skip
-// is its own instantiation: its box load, test and back-out cost about 11 %
-// of the packed walk's rate when merely present (measured), so
-// the launch that does not skip runs code without them.
-constexpr int kPackedSkip = 2;
-
-constexpr uint32_t kIdMask = 0x00FFFFFFu;
-#ifndef OCH_POP_SELECT
-#define OCH_POP_SELECT 1
-#endif
-#ifndef OCH_ADDC_IDX
-#define OCH_ADDC_IDX 1
-#endif
-#ifndef OCH_MAD24
-#define OCH_MAD24 1
-#endif
 // Byte offset of child slot c24 - 24 of the node whose slot word is w, from
 // the node pool's base plus 96: (id * 8 + c24) * 4, id = w's low 24 bits.  One
 // v_mad_u32_u24 and a shift (the compiler turns the mul24 by 8 into a shift
 // and a mask, one VALU more per descent).
 __device__ __forceinline__ uint32_t slot_offset(uint32_t w, uint32_t c24)
 {
-    if (OCH_MAD24) {
-        uint32_t t;
-        asm("v_mad_u32_u24 %0, %1, 8, %2" : "=v"(t) : "v"(w), "v"(c24));
-        return t << 2;
-    }
-    return ((w & kIdMask) << 5) + (c24 << 2);
+    uint32_t t;
+    asm("v_mad_u32_u24 %0, %1, 8, %2" : "=v"(t) : "v"(w), "v"(c24));
+    return t << 2;
 }
 
-// The PUSH test and slot fetch (ORT/och_h_octree.h:342-344): the packed
-// layout tests presence with the child mask held in the node's slot word and
-// loads only present children; the raw layout loads every slot and tests it
-// when the load has landed (ray_phase_descend).
-template <int kPacked, bool kCount>
-__device__ __forceinline__ void ray_push(Ray &r, const DevPool &P)
+// The raw layout's PUSH (ORT/och_h_octree.h:342-344): the slot must be loaded
+// to be tested, which happens when the load has landed (ray_phase_descend).
+template <bool kCount>
+__device__ __forceinline__ void ray_push_raw(Ray &r, const DevPool &P)
 {
     if (kCount) ++r.push;
     const uint32_t c24 = r.idx ^ r.inv;                                     // 24 + child index
-    const uint32_t present = kPacked ? __builtin_amdgcn_ubfe(r.cur, c24, 1u) : 1u;
-    set_mode(r, present * kPending);                                        // kStepping or kPending
-    asm volatile("" : "+v"(r.mode));                                        // one shift, not a move per branch
-#if OCH_PUSH_UNCOND
-    // The slot exists whether or not the child does (cur names a pool node),
-    // so every PUSH may load it; the word is used only when present.
-    if (kPacked || present) r.child = (P.nodes - 24)[8u * (kPacked ? (r.cur & kIdMask) : r.cur) + c24];
-#else
-    if (present) r.child = (P.nodes - 24)[8u * (kPacked ? (r.cur & kIdMask) : r.cur) + c24];
-#endif
+    r.mode = kPending;
+    r.child = (P.nodes - 24)[8u * r.cur + c24];
 }
 
-#ifndef OCH_MERGED_DESCEND
-#define OCH_MERGED_DESCEND 1
-#endif
-// OCH_DIM_LEVEL: no level counter; the level is implied by the child-size bit
-// (level L <-> dim = 1 << (23 - L)): a MISS shifts dim past 1 << 22, a HIT
-// below 1 << (23 - depth), so the walk is active while dim stays in range.
-#ifndef OCH_DIM_LEVEL
-#define OCH_DIM_LEVEL 1
-#endif
-// OCH_LDS_TOP = T: the grid kernel keeps the packed nodes of levels 1..T in
-// LDS and reads near-root PUSHes from there (experiment, SURVEY §7 kernel notes).
-#ifndef OCH_LDS_TOP
-#define OCH_LDS_TOP 0
-#endif
-// OCH_LOAD_INTO_CUR: the merged loop loads a present child's slot word
-// straight into the ray's current-node register (after the parent went to
-// the stack), so the next PUSH needs no "pending" select.
-#ifndef OCH_LOAD_INTO_CUR
-#define OCH_LOAD_INTO_CUR 1
-#endif
-// OCH_POP_CHAIN: a POP and the POPs and the advance that follow it in one step
-// (merged loop; ray_phase_step has the proof).
-#ifndef OCH_POP_CHAIN
-#define OCH_POP_CHAIN 1
-#endif
-// OCH_DUAL: the grid kernel walks two rays per lane (two tiles per wave).
-#ifndef OCH_DUAL
-#define OCH_DUAL 0
-#endif
-template <bool kCount, bool kAsm, bool kBox>
-__device__ __forceinline__ void ray_push_descend(Ray &r, const DevPool &P, uint32_t stride,
-                                                 const uint32_t *top = nullptr);
+template <bool kCount, bool kAsm>
+__device__ __forceinline__ void ray_push_descend(Ray &r, const DevPool &P, uint32_t stride);
 
 // Occupied-box cull (OCH_OPT_CULL; DESIGN.md §4b has the proof).  With
 // t_a(q) = fma(q, c_a, b_a), the walk's t of plane q on axis a in the
@@ -237,120 +163,13 @@ __device__ __forceinline__ bool ray_cull(const Ray &r, const DevPool &P, const f
     return ok && (enter > leave || leave < 0.0F);
 }
 
-// Column cull (OCH_OPT_COLUMNS; DESIGN.md §4d has the proof): the cull's
-// test for a box B applies to any box that holds the voxels a ray could hit,
-// so a ray that fails it for every block of a partition of the voxels into
-// boxes enters no voxel cell and ends in the MISS the walk would reach.  The
-// blocks are the columns of a quadtree over the world's x-y extent
-// (DevPool::columns: a block's box is its x-y square times the z range of the
-// voxels above it).  The wave walks the quadtree once, uniformly: a block no
-// lane can enter is pruned with everything below it; a leaf block some lane
-// can enter ends the test, and the whole wave walks as before.  Otherwise
-// every lane failed every block on each path to every leaf holding voxels,
-// and the whole wave's rays are proven misses.  Children are visited nearest
-// the camera first (the first lane's direction signs), so a wave that will
-// walk finds its entered leaf early.
-__device__ __forceinline__ bool column_box_entered(const Ray &r, const float lo[3], const float hi[3])
-{
-    float enter = -INFINITY, leave = INFINITY;
-#pragma unroll
-    for (int a = 0; a < 3; ++a) {
-        const float k = (r.inv >> a) & 1u ? 3.0F : 0.0F;        // the reflected frame, as ray_cull
-        const float t1 = __builtin_fmaf(fabsf(__fsub_rn(k, lo[a])), r.c[a], r.b[a]);
-        const float t2 = __builtin_fmaf(fabsf(__fsub_rn(k, hi[a])), r.c[a], r.b[a]);
-        enter = fmaxf(enter, fminf(t1, t2));
-        leave = fminf(leave, fmaxf(t1, t2));
-    }
-    return !(enter > leave || leave < 0.0F);
-}
-
-// OCH_COL_DZ (experiment, measured: no gain): only waves whose
-// first ray dips less than this (d_z > -OCH_COL_DZ) try the column cull.
-__device__ __forceinline__ bool col_try(const float *d)
-{
-#ifdef OCH_COL_DZ
-    return __builtin_amdgcn_readfirstlane(d[2] > -(float)OCH_COL_DZ ? 1u : 0u) != 0u;
-#else
-    (void)d;
-    return true;
-#endif
-}
-
-__device__ __forceinline__ bool column_cull_wave(const Ray &r, const DevPool &P, const float *o)
-{
-    bool ok = true;                                              // ray_cull's preconditions
-#pragma unroll
-    for (int a = 0; a < 3; ++a) {
-        ok &= ((fbits(r.c[a]) >> 23) & 0xFFu) - 1u < 251u;
-        ok &= o[a] > 1.0F && o[a] < 2.0F;
-    }
-    if (__ballot(!ok)) return false;
-    const uint32_t levels = (uint32_t)P.col_levels;
-    const uint32_t flip = __builtin_amdgcn_readfirstlane(~r.inv & 3u);   // x bit 0, y bit 1: near half first
-    const float vox = ffrom((uint32_t)(127 - P.depth) << 23);             // 2^-depth
-    uint32_t l = 1, m = 0;                                      // level and visit index, wave-uniform
-    while (l != 0) {
-        const uint32_t code = m ^ (flip * (((1u << (2 * l)) - 1u) / 3u));  // the flip in every digit
-        // a uniform word: a scalar load (the compiler's own would be a vector
-        // load, as the kernel writes other memory), read-only
-        uint32_t w;
-        asm volatile("s_load_dword %0, %1, %2\n\ts_waitcnt lgkmcnt(0)"
-                     : "=s"(w)
-                     : "s"(P.columns), "s"((((1u << (2 * l)) - 4u) / 3u + code) * 4u)
-                     : "memory");
-        if ((w & 0xFFFFu) <= (w >> 16)) {                       // the block holds voxels
-            uint32_t bx = 0, by = 0;
-            for (uint32_t i = 0; i < l; ++i) {
-                bx |= ((code >> (2 * i)) & 1u) << i;
-                by |= ((code >> (2 * i + 1)) & 1u) << i;
-            }
-            const float size = ffrom((127u - l) << 23);          // 2^-l: every corner below is exact
-            const float lo[3] = {1.0F + (float)bx * size, 1.0F + (float)by * size, 1.0F + (float)(w & 0xFFFFu) * vox};
-            const float hi[3] = {lo[0] + size, lo[1] + size, 1.0F + (float)((w >> 16) + 1u) * vox};
-            if (__ballot(column_box_entered(r, lo, hi))) {
-                if (l == levels) return false;                  // a lane may enter a leaf block: walk
-                ++l;
-                m <<= 2;
-                continue;
-            }
-        }
-        ++m;                                                    // next sibling, up when the four are done
-        while (l != 0 && (m & 3u) == 0) {
-            --l;
-            m >>= 2;
-        }
-    }
-    return true;
-}
-
-// Setup, ORT/och_h_octree.h:294-338, then the first PUSH at the root.
+// Setup, ORT/och_h_octree.h:294-338, up to, not including, the root PUSH.
 // stack: this lane's LDS column, depth + 1 slots `stride` words apart.
-// kCull: a ray that ray_cull proves a miss ends here (ray_active false,
-// ray_result the miss record, 0 PUSHes); the kernel's loop tests ray_active
-// before iterating.  Launches that count PUSHes cull only at OCH_OPT_CULL = 2
-// (a diagnostic: how many PUSHes the culled launch walks), so their counts
-// stay the reference's.
-template <bool kCount, bool kCull, bool kColumns = false>
-__device__ __forceinline__ bool ray_setup(Ray &r, const DevPool &P, const float *o, const float *d, uint32_t *stack,
-                                          uint32_t stride);
-
-// kColumns: the column cull after the occupied-box cull (primary-ray grid
-// launches; column_cull_wave), under the cull's option: launches that count
-// PUSHes only at OCH_OPT_CULL = 2, the diagnostic.
-template <int kPacked, bool kCount, bool kCull = false, bool kAsm = false, bool kColumns = false>
-__device__ __forceinline__ void ray_init(Ray &r, const DevPool &P, const float *o, const float *d, uint32_t *stack,
-                                         uint32_t stride)
-{
-    if (!ray_setup<kCount, kCull, kColumns>(r, P, o, d, stack, stride)) return;
-    if (kPacked && OCH_MERGED_DESCEND)
-        ray_push_descend<kCount, kAsm, kPacked == kPackedSkip>(r, P, stride);
-    else
-        ray_push<kPacked, kCount>(r, P);
-}
-
-// ray_init's setup (:294-338) up to, not including, the root PUSH.  false:
-// the ray is culled (recorded as the MISS, 0 PUSHes, ray_active false).
-template <bool kCount, bool kCull, bool kColumns>
+// kCull: a ray that ray_cull proves a miss ends here (false: ray_active
+// false, ray_result the miss record, 0 PUSHes).  Launches that count PUSHes
+// cull only at OCH_OPT_CULL = 2 (a diagnostic: how many PUSHes the culled
+// launch walks), so their counts stay the reference's.
+template <bool kCount, bool kCull>
 __device__ __forceinline__ bool ray_setup(Ray &r, const DevPool &P, const float *o, const float *d, uint32_t *stack,
                                           uint32_t stride)
 {
@@ -387,73 +206,48 @@ __device__ __forceinline__ bool ray_setup(Ray &r, const DevPool &P, const float 
     r.sp = stack + stride;                                                  // slot 0: the miss POP's dummy read
     r.sp23 = stack + 23u * stride;                                          // slot 23 - ctz(dim)
     r.t_min = 0;                                                            // +0.0F
-    if (!OCH_DIM_LEVEL) r.level = 1;
     r.min_axis = 8;
-    set_mode(r, kAtPush);
+    r.mode = kAtPush;
     r.child = 0;
     r.push = 0;
-    r.box = 0;
-    bool exact = true;                                  // the per-node skip's precondition (ray_skip_node)
-#pragma unroll
-    for (int a = 0; a < 3; ++a) {
-        exact &= ((fbits(r.c[a]) >> 23) & 0xFFu) - 1u < 251u;
-        exact &= o[a] > 1.0F && o[a] < 2.0F;
-    }
-    r.skipmask = exact && P.boxes && skip_on(P, kCount) ? 0xFFFFu : 0u;
-    if (kCull && (kCount ? P.cull == 2 : P.cull != 0) &&
-        (ray_cull(r, P, o) || (kColumns && P.columns && col_try(d) && column_cull_wave(r, P, o)))) {
+    if (kCull && (kCount ? P.cull == 2 : P.cull != 0) && ray_cull(r, P, o)) {
         r.dim = 1u << 23;                                                   // finished: the MISS
-        set_mode(r, kStepping);
-        if (!OCH_DIM_LEVEL) r.level = 0;
+        r.mode = kStepping;
         return false;
     }
     return true;
 }
 
-// The PUSH / STEP / POP machine (ORT/och_h_octree.h:342-446,
-// ORT/och_octree.cpp:217-319) as three phases per iteration, software-
-// pipelined so that a slot load is in flight while other lanes STEP:
-//   step    -- lanes due to STEP do so, then advance to a sibling or POP;
-//   descend -- lanes whose PUSH found its child (slot word loaded by the
-//              previous iteration's push) hit or descend;
-//   push    -- every lane now at a PUSH tests its child and, if present,
-//              issues the load of the child's slot word.
-// The packed layout orders them step, descend, push.  The raw layout must
-// load every PUSH's slot to test it, so it resolves the slot first (descend,
-// step, push): an empty child then STEPs in the same iteration.
-// stride: words between two levels of one lane's LDS stack.
-// Ray::mode of a lane that backs out of the node it just entered (the
-// per-node skip, ray_push_descend), then STEPs: negative, so the STEP phase's
-// test (mode <= 0, signed) takes it with the lanes due to STEP.  In the mode
-// register rather than in box: a test of box in the STEP phase made the
-// compiler wait for every lane's box load there (vmcnt(0) at each STEP
-// phase), which undid the loads' overlap with the STEP phase.
-constexpr uint32_t kUndoDescent = 0x80000000u;
-__device__ __forceinline__ void ray_undo_descent(Ray &r, uint32_t stride);
-
-__device__ __forceinline__ bool due_to_step(Ray &r)
+// Setup, then the first PUSH at the root.
+template <int kPacked, bool kCount, bool kCull = false, bool kAsm = false>
+__device__ __forceinline__ void ray_init(Ray &r, const DevPool &P, const float *o, const float *d, uint32_t *stack,
+                                         uint32_t stride)
 {
-    asm volatile("" : "+v"(r.mode));
-    return (int32_t)r.mode <= 0;
+    if (!ray_setup<kCount, kCull>(r, P, o, d, stack, stride)) return;
+    if (kPacked)
+        ray_push_descend<kCount, kAsm>(r, P, stride);
+    else
+        ray_push_raw<kCount>(r, P);
 }
 
+// The PUSH / STEP / POP machine (ORT/och_h_octree.h:342-446,
+// ORT/och_octree.cpp:217-319) in phases per iteration, software-pipelined so
+// that a slot load is in flight while other lanes STEP:
+//   step    -- lanes due to STEP do so, then advance to a sibling or POP;
+//   push + descend (packed) -- lanes due to PUSH test the child in the held
+//              node word and, if present, descend and issue the load of the
+//              child's slot word (ray_push_descend).
+// The raw layout must load every PUSH's slot to test it, so it resolves the
+// slot first (descend, step, push): an empty child then STEPs in the same
+// iteration.  stride: words between two levels of one lane's LDS stack.
 template <int kPacked>
 __device__ __forceinline__ void ray_phase_step(Ray &r, uint32_t stride)
 {
-    if (OCH_NODE_SKIP && kPacked == kPackedSkip && r.mode == kUndoDescent)
-        ray_undo_descent(r, stride);                    // the per-node skip's POP (ray_push_descend)
     // STEP :378-419.  The reference's cascade (x if tx <= ty && tx <= tz,
     // else y if ty < tx && ty <= tz, else z) picks the first axis holding
     // the unsigned minimum.
-#if OCH_PK_FMA
-    // x and y as one packed FMA (v_pk_fma_f32: two lanes of f32, each rounded once, as v_fma_f32)
-    const float2v pxy = {ffrom(r.p[0]), ffrom(r.p[1])}, cxy = {r.c[0], r.c[1]}, bxy = {r.b[0], r.b[1]};
-    const float2v txy = __builtin_elementwise_fma(pxy, cxy, bxy);
-    const uint32_t tx = fbits(txy.x), ty = fbits(txy.y);
-#else
     const uint32_t tx = fbits(__builtin_fmaf(ffrom(r.p[0]), r.c[0], r.b[0]));
     const uint32_t ty = fbits(__builtin_fmaf(ffrom(r.p[1]), r.c[1], r.b[1]));
-#endif
     const uint32_t tz = fbits(__builtin_fmaf(ffrom(r.p[2]), r.c[2], r.b[2]));
     const uint32_t tm = min(min(tx, ty), tz);
     const bool sx = tx == tm;
@@ -462,8 +256,7 @@ __device__ __forceinline__ void ray_phase_step(Ray &r, uint32_t stride)
     const uint32_t axis = sx ? 1u : (sy ? 2u : 4u);
     r.min_axis = axis;
     r.t_min = tm;
-#if OCH_POP_CHAIN
-    if (kPacked && OCH_MERGED_DESCEND) {
+    if (kPacked) {
         // the phase register holds the advance test itself: nonzero (a PUSH is
         // due) after an advance, kStepping (0) while POPs are left to do
         r.mode = r.idx & axis;
@@ -476,31 +269,21 @@ __device__ __forceinline__ void ray_phase_step(Ray &r, uint32_t stride)
         // position bit of axis a is clear at that level.  So the walk POPs to
         // the level of the lowest set bit of p_a above the current one and
         // advances there on axis a -- or, with no such bit, POPs past the root
-        // (the MISS).  Nothing
-        // in between is counted or recorded; the chain lands in the state the
-        // POP-by-POP walk reaches, one STEP of it later.  Rays with a negative
-        // or NaN t (zero / denormal direction components, origins outside the
-        // root) take one POP as before.
+        // (the MISS).  Nothing in between is counted or recorded; the chain
+        // lands in the state the POP-by-POP walk reaches, one STEP of it later.
+        // Rays with a negative or NaN t (zero / denormal direction components,
+        // origins outside the root) take one POP as before.
         if (!r.mode) {
             const bool chain = max(max(tx, ty), tz) < 0x80000000u;
             const uint32_t pa = sx ? r.p[0] : (sy ? r.p[1] : r.p[2]);
             // bit 23 stands for "past the root": the MISS, also when p_a has no
-            // bit at 23 (an origin outside the root reflects to p = 0 or below 1)
-#if OCH_POP_SELECT
-            // branch-free: a single POP is the chain from pa = d2 (d2 & -d2 = d2)
+            // bit at 23 (an origin outside the root reflects to p = 0 or below 1).
+            // Branch-free: a single POP is the chain from pa = d2 (d2 & -d2 = d2).
             const uint32_t d2 = r.dim << 1;
             const uint32_t up = ((chain ? pa : d2) & (0u - d2)) | (1u << 23);
-#else
-            const uint32_t up = chain ? ((pa & (0u - (r.dim << 1))) | (1u << 23)) : (r.dim << 1);
-#endif
-#if OCH_POP_SELECT
             uint32_t k = __builtin_ctz(up);                                 // the new level's bit
             asm volatile("" : "+v"(k));        // 1 << k, not re-folded into up & -up (one VALU more)
             const uint32_t nd = 1u << k;                                    // new child-size bit
-#else
-            const uint32_t nd = up & (0u - up);                             // new child-size bit
-            const uint32_t k = __builtin_ctz(nd);
-#endif
             // one 24-bit multiply-add: k < 32, stride <= 1024 words
             r.sp = reinterpret_cast<uint32_t *>(reinterpret_cast<char *>(r.sp23) - __mul24((int)k, 4 * (int)stride));
             r.cur = *r.sp;                                                  // :434 (slot 0 after the MISS)
@@ -522,51 +305,44 @@ __device__ __forceinline__ void ray_phase_step(Ray &r, uint32_t stride)
         }
         return;
     }
-#endif
-    const uint32_t adv = r.idx & axis;
-    // merged loop: the phase is the advance test itself -- nonzero (a PUSH is
-    // due) after an advance, kStepping (0) after a POP; no write per branch
-    if (kPacked && OCH_MERGED_DESCEND) r.mode = adv;
-    if (adv) {                                                          // advance :413-419
+    if (r.idx & axis) {                                                     // advance :413-419
         // idx bit `axis` set <=> that axis's position has the dim bit set,
         // so clearing it (:415) is a toggle.
         r.p[0] ^= sx ? r.dim : 0u;
         r.p[1] ^= sy ? r.dim : 0u;
         r.p[2] ^= sz ? r.dim : 0u;
         r.idx ^= axis;
-        if (!(kPacked && OCH_MERGED_DESCEND)) set_mode(r, kAtPush);
+        r.mode = kAtPush;
         return;
     }
-    // POP :421-446.  At the root this is the MISS (:423-431): level 0 ends
-    // the ray, and the rest of the POP runs on dead state (its stack read
+    // POP :421-446.  At the root this is the MISS (:423-431): dim leaves the
+    // walk's range, and the rest of the POP runs on dead state (its stack read
     // lands in the column's spare slot 0) rather than behind a branch.
-    if (!OCH_DIM_LEVEL) --r.level;
     r.sp -= stride;
-    r.cur = *r.sp;                                                      // :434
+    r.cur = *r.sp;                                                          // :434
 #pragma unroll
-    for (int a = 0; a < 3; ++a) r.p[a] &= ~r.dim;                       // :436
-    r.dim <<= 1;                                                        // :438
-    const uint32_t k = __builtin_ctz(r.dim);                            // :440-444, bit k of each position
+    for (int a = 0; a < 3; ++a) r.p[a] &= ~r.dim;                           // :436
+    r.dim <<= 1;                                                            // :438
+    const uint32_t k = __builtin_ctz(r.dim);                                // :440-444, bit k of each position
     uint32_t zy = (__builtin_amdgcn_ubfe(r.p[2], k, 1) << 1) | __builtin_amdgcn_ubfe(r.p[1], k, 1);
     asm volatile("" : "+v"(zy));          // two shift-ors, not two shifts and an or3
     r.idx = (zy << 1) | __builtin_amdgcn_ubfe(r.p[0], k, 1);
 }
 
-template <int kPacked>
-__device__ __forceinline__ void ray_phase_descend(Ray &r, const DevPool &P, uint32_t stride)
+// The raw layout's descend phase: the PUSH's slot word has landed.
+__device__ __forceinline__ void ray_phase_descend_raw(Ray &r, uint32_t stride)
 {
-    set_mode(r, kAtPush);
+    r.mode = kAtPush;
     const uint32_t child = r.child;
-    if (!kPacked && child == 0) {                                           // raw layout: empty child
-        set_mode(r, kStepping);
+    if (child == 0) {                                                       // empty child
+        r.mode = kStepping;
         return;
     }
-    // HIT :346-355 when the PUSH was at the leaf level: level becomes
-    // depth + 1 (finished) exactly as a descent increments it, the voxel id
+    // HIT :346-355 when the PUSH was at the leaf level: dim drops below the
+    // walk's range (finished) exactly as a descent halves it, the voxel id
     // stays in r.child (no later load overwrites a finished lane's), and the
     // rest of the descent runs on dead state (its stack write lands in the
     // column's spare top slot) rather than behind a branch.
-    if (!OCH_DIM_LEVEL) ++r.level;
     *r.sp = r.cur;                                                          // :357
     r.sp += stride;
     r.cur = child;
@@ -583,69 +359,36 @@ __device__ __forceinline__ void ray_phase_descend(Ray &r, const DevPool &P, uint
     r.idx = nidx;
 }
 
-// Still walking: level in 1..depth (0 = missed, depth + 1 = hit).
+// Still walking: the child-size bit is in the range of levels 1..depth (a
+// MISS shifts it past 1 << 22, a HIT below 1 << (23 - depth)), so no level
+// counter is kept.
 __device__ __forceinline__ bool ray_active(const Ray &r, const DevPool &P)
 {
-    if (OCH_DIM_LEVEL) return r.dim - P.dim_lo <= P.dim_span;
-    return (uint32_t)(r.level - 1) < (uint32_t)P.depth;
+    return r.dim - P.dim_lo <= P.dim_span;
 }
 
-// Packed layout, PUSH and descent in one phase (OCH_MERGED_DESCEND): the
-// child's presence is a bit of the held node word and the descent's
-// geometry (:357-373) does not depend on the child's own slot word, so a
-// PUSH that finds its child descends at once; only the child's word -- the
-// node of the next PUSH, or the voxel id of a HIT -- is loaded, and the next
-// PUSH takes it (mode kPending) after the other lanes' STEP phase has hidden
-// the load.  Two phases per iteration instead of three.
-// The descent of a PUSH that found its child (packed, merged loop): the
-// parent to the stack, the child's slot word loaded into cur, the child
-// cell chosen (:357-373); at the leaf level this is the HIT.
-template <bool kCount>
-__device__ __forceinline__ void ray_descend(Ray &r, const DevPool &P, uint32_t stride)
-{
-    const uint32_t c24 = r.idx ^ r.inv;
-    const uint32_t off = slot_offset(r.cur, c24);
-    const uint32_t *src = reinterpret_cast<const uint32_t *>(reinterpret_cast<const char *>(P.nodes) - 96 + off);
-    *r.sp = r.cur;
-    r.sp += stride;
-    r.cur = *src;
-    r.dim >>= 1;
-    const float tm = ffrom(r.t_min);
-    uint32_t nidx = 0;
-#pragma unroll
-    for (int a = 0; a < 3; ++a) {
-        const uint32_t mid = r.p[a] | r.dim;
-        const bool upper = __builtin_fmaf(ffrom(mid), r.c[a], r.b[a]) >= tm;
-        nidx |= (uint32_t)upper << a;
-        r.p[a] = upper ? mid : r.p[a];
-    }
-    r.idx = nidx;
-}
-
-// OCH_ASM_LOAD: the descent's slot-word load into cur is issued by inline asm,
-// so the compiler's waitcnt pass does not see it in flight.  Its only
-// readers are the next PUSH and ray_result, each behind an explicit
-// `s_waitcnt vmcnt(0)` that takes cur as an operand (so no read of cur is
-// scheduled above it).  What the compiler's view saves is the vmcnt(0) it
-// puts at the POP chain: the chain writes cur (the popped word, an LDS read)
-// in lanes that are STEPping, and a load into cur may still be in flight for
-// the lanes that descended.  Those lanes are disjoint (a lane that descended
-// is due to PUSH and skips the STEP phase), and a load writes only the lanes
-// active at its issue, so no lane sees the other's write; the wave no longer
-// waits for its descents' loads before popping.
+// The descent's slot-word load into cur is issued by inline asm, so the
+// compiler's waitcnt pass does not see it in flight.  Its only readers are the
+// next PUSH and ray_result, each behind an explicit `s_waitcnt vmcnt(0)` that
+// takes cur as an operand (so no read of cur is scheduled above it).  What the
+// compiler's view saves is the vmcnt(0) it puts at the POP chain: the chain
+// writes cur (the popped word, an LDS read) in lanes that are STEPping, and a
+// load into cur may still be in flight for the lanes that descended.  Those
+// lanes are disjoint (a lane that descended is due to PUSH and skips the STEP
+// phase), and a load writes only the lanes active at its issue, so no lane
+// sees the other's write; the wave no longer waits for its descents' loads
+// before popping.
+// The build checks the compiler's output for what this relies on
+// (tools/isa_check.py, run by `make` and __graft_entry__.build()): in every
+// kernel that issues the load, the load and every wait name one register, and
+// on every path from a load to the next vmcnt(0) wait no instruction reads
+// that register before writing it (a read there would see the word before
+// the load lands -- a copy of cur at a join, a spill, a full-wave select).
+// Writes there are the lane-disjoint temporaries of the STEP phase above.
+// OCH_ASM_LOAD=0 builds the compiler's own load (tests/test_isa_check.py).
 #ifndef OCH_ASM_LOAD
 #define OCH_ASM_LOAD 1
 #endif
-// The grid and bounce kernels (one ray per lane, straight-line use of cur)
-// take it; the refill and persistent schedules keep the compiler's loads.
-// The build checks the compiler's output for what this relies on
-// (tools/isa_check.py, run by `make` and __graft_entry__.build()): in every
-// kernel that issues the load, the load and every wait name one register,
-// and on every path from a load to the next vmcnt(0) wait no instruction
-// reads that register before writing it (a read there would see the word
-// before the load lands -- a copy of cur at a join, a spill, a full-wave
-// select).  Writes there are the lane-disjoint temporaries of the STEP
-// phase described above.
 constexpr bool kAsmLoad = OCH_ASM_LOAD != 0;
 template <bool kAsm>
 __device__ __forceinline__ void wait_cur(Ray &r)
@@ -655,310 +398,111 @@ __device__ __forceinline__ void wait_cur(Ray &r)
     if (kAsm) asm volatile("s_waitcnt vmcnt(0) ; och_cur_wait %0" : "+v"(r.cur) : : "memory");
 }
 
-// OCH_NODE_SKIP: the per-node voxel-box skip (OCH_OPT_SKIP; DESIGN.md §4c has
-// the proof).  The occupied-box cull's invariant holds for every cell the walk
-// enters: max_a t_a(hi_a) <= t_min <= min_a t_a(lo_a), t_a(q) = fma(q, c_a,
-// b_a) non-increasing in q.  So a ray for which a box B holding every voxel
-// under node C fails  max_a t_a(B.hi_a) <= min_a t_a(B.lo_a) >= t_min  enters
-// no cell of C that holds a voxel, and cannot hit inside C.  Its excursion
-// through C ends by leaving C through C's exit plane at C's exit t -- the
-// plane and t the STEP right after treating C as empty picks (the POP
-// chain's argument: with every t a non-negative float the exit axis and
-// t_min repeat at each level on the way out).  So the walk that descends
-// into C, reads C's box (loaded with C's word) and steps straight back out
-// (ray_undo_descent: the parent's word from the stack, the level's bits
-// cleared -- one POP) is in the state the full excursion ends in, and every
-// record is the reference's.  Exact for rays with every c_a a negative
-// normal below 2^125 (finite t) and the origin inside (1, 2)^3 (skipmask);
-// launches that count PUSHes skip only at OCH_OPT_SKIP = 2 (a diagnostic).
-
-// bx: the box of the node the last descent entered (och_internal.h
-// DevPool::boxes): x, y in quarters of its cell, z in sixteenths, world
-// orientation, each as lo and Q - hi.  True when the ray provably enters no
-// cell of that box.
-__device__ __forceinline__ bool ray_skip_node(const Ray &r, uint32_t bx)
-{
-    const uint32_t size = r.dim << 1;                    // the node's cell, mantissa units
-    const float tm = ffrom(r.t_min);
-    float enter = -INFINITY, leave = INFINITY;
-#pragma unroll
-    for (int a = 0; a < 3; ++a) {
-        const uint32_t bits = a < 2 ? 2u : 4u, q = 1u << bits;
-        const uint32_t lo = __builtin_amdgcn_ubfe(bx, 4u * a, bits);
-        const uint32_t hc = __builtin_amdgcn_ubfe(bx, 4u * a + bits, bits);
-        const bool refl = (r.inv >> a) & 1u;             // reflected axis: [Q - hi, Q - lo)
-        const uint32_t rlo = refl ? hc : lo, rhi = q - (refl ? lo : hc);
-        const uint32_t step = size >> bits, corner = r.p[a] & ~r.dim;
-        // plane positions: corner + k * step, k <= 16, step < 2^22 -- a 24-bit multiply-add
-        const float tlo = __builtin_fmaf(ffrom(corner + __umul24(rlo, step)), r.c[a], r.b[a]);
-        const float thi = __builtin_fmaf(ffrom(corner + __umul24(rhi, step)), r.c[a], r.b[a]);
-        enter = fmaxf(enter, thi);                       // the near planes: the larger position
-        leave = fminf(leave, tlo);
-    }
-    return enter > leave || leave < tm;
-}
-
-// Back out of the node the last descent entered, as a POP does (:434-444).
-__device__ __forceinline__ void ray_undo_descent(Ray &r, uint32_t stride)
-{
-    r.sp -= stride;
-    r.cur = *r.sp;                                       // the parent's word, written by the descent
-    const uint32_t keep = ~r.dim;
-    r.p[0] &= keep;
-    r.p[1] &= keep;
-    r.p[2] &= keep;
-    r.dim <<= 1;
-    const uint32_t k = __builtin_ctz(r.dim);
-    uint32_t zy = (__builtin_amdgcn_ubfe(r.p[2], k, 1) << 1) | __builtin_amdgcn_ubfe(r.p[1], k, 1);
-    asm volatile("" : "+v"(zy));
-    r.idx = (zy << 1) | __builtin_amdgcn_ubfe(r.p[0], k, 1);
-    set_mode(r, kStepping);
-}
-
-template <bool kCount, bool kAsm, bool kBox>
-__device__ __forceinline__ void ray_push_descend(Ray &r, const DevPool &P, uint32_t stride, const uint32_t *top)
+// Packed layout, PUSH and descent in one phase: the child's presence is a bit
+// of the held node word and the descent's geometry (:357-373) does not depend
+// on the child's own slot word, so a PUSH that finds its child descends at
+// once: the parent to the stack, the child's slot word loaded straight into
+// cur -- the node of the next PUSH, or the voxel id of a HIT -- and the child
+// cell chosen.  The next PUSH takes the word after the other lanes' STEP phase
+// has hidden the load.
+template <bool kCount, bool kAsm>
+__device__ __forceinline__ void ray_push_descend(Ray &r, const DevPool &P, uint32_t stride)
 {
     wait_cur<kAsm>(r);
-    if (OCH_NODE_SKIP) {
-        // skipmask is 0 unless this launch skips and the skip is exact for the ray
-        const uint32_t bx = r.box & r.skipmask;
-        r.box = 0;
-        if (bx && ray_skip_node(r, bx)) {               // the node just entered holds nothing on this ray
-            // back out at the start of the next STEP phase (ray_phase_step):
-            // undone here, the new definition of cur made the compiler copy
-            // cur's register at the loop's latch while other lanes' loads into
-            // it were in flight (tools/isa_check.py)
-            set_mode(r, kUndoDescent);
-            return;
-        }
-    }
-    if (!OCH_LOAD_INTO_CUR) r.cur = in_mode(r, kPending) ? r.child : r.cur;
     if (kCount) ++r.push;
     const uint32_t c24 = r.idx ^ r.inv;                                     // 24 + child index
     const uint32_t present = __builtin_amdgcn_ubfe(r.cur, c24, 1u);
-    // kStepping (0) or, with the word loaded into cur, any nonzero "PUSH due"
-    set_mode(r, OCH_LOAD_INTO_CUR ? present : present * kPending);
+    r.mode = present;                       // kStepping (0), or nonzero: "PUSH due" after the descent
     const bool go = present != 0;           // compared before the barrier: present's register becomes mode's
     asm volatile("" : "+v"(r.mode));
     if (!go) return;
     // 32-bit byte offset from the uniform base: one scaled add, SGPR base address
     const uint32_t off = slot_offset(r.cur, c24);
-    const uint32_t *src = reinterpret_cast<const uint32_t *>(
-        reinterpret_cast<const char *>(OCH_LDS_TOP && top && (r.cur & kIdMask) < P.top_ids[OCH_LDS_TOP] ? top : P.nodes) -
-        96 + off);
-    // descent (:357-373); at the leaf level this is the HIT (:346-355): level
-    // becomes depth + 1, the stack write lands in the spare top slot
-    if (!OCH_DIM_LEVEL) ++r.level;
+    // descent (:357-373); at the leaf level this is the HIT (:346-355): dim
+    // drops below the walk's range, the stack write lands in the spare top slot
     *r.sp = r.cur;                          // the parent, before its register takes the child's word
     r.sp += stride;
-    // the child's voxel box (per-node skip), loaded beside its word: boxes
-    // - 48 B + off / 2 = boxes + 2 * (8 * id + child).  Issued whether or not
-    // the launch skips (the host points boxes at the node array when there
-    // are none, and skipmask masks the word): a load under a branch made the
-    // compiler copy the registers of loads in flight at the join (the build's
-    // ISA check, tools/isa_check.py, caught it).
-    if (OCH_NODE_SKIP && kBox)            // the compiler's own load: it waits for it before the box is read
-        r.box = *reinterpret_cast<const uint16_t *>(reinterpret_cast<const char *>(P.box_base) - 48 + (off >> 1));
-    if (OCH_LOAD_INTO_CUR && kAsm && !OCH_LDS_TOP)
-        asm volatile("global_load_dword %0, %1, %2 offset:-96 ; och_cur_load"   // src = P.nodes - 96 B + off
+    if (kAsm)
+        asm volatile("global_load_dword %0, %1, %2 offset:-96 ; och_cur_load"   // P.nodes - 96 B + off
                      : "+v"(r.cur)
                      : "v"(off), "s"(P.nodes)
                      : "memory");
-    else if (OCH_LOAD_INTO_CUR)
-        r.cur = *src;                       // the next PUSH's node, or the voxel id of a HIT
     else
-        r.child = *src;
+        r.cur = *reinterpret_cast<const uint32_t *>(reinterpret_cast<const char *>(P.nodes) - 96 + off);
     r.dim >>= 1;
     const float tm = ffrom(r.t_min);
     uint32_t nidx = 0;
-#if OCH_PK_FMA
-    const uint32_t mx = r.p[0] | r.dim, my = r.p[1] | r.dim, mz = r.p[2] | r.dim;
-    const float2v mxy = {ffrom(mx), ffrom(my)}, cxy = {r.c[0], r.c[1]}, bxy = {r.b[0], r.b[1]};
-    const float2v txy = __builtin_elementwise_fma(mxy, cxy, bxy);
-    const bool ux = txy.x >= tm, uy = txy.y >= tm, uz = __builtin_fmaf(ffrom(mz), r.c[2], r.b[2]) >= tm;
-    nidx = (uint32_t)ux | ((uint32_t)uy << 1) | ((uint32_t)uz << 2);
-    r.p[0] = ux ? mx : r.p[0];
-    r.p[1] = uy ? my : r.p[1];
-    r.p[2] = uz ? mz : r.p[2];
-#else
-    if (OCH_ADDC_IDX) {
-        // z, y, x: idx = 2 idx + upper as one v_addc_co_u32 with the compare's
-        // mask as carry-in (the compiler builds 3 v_cndmask + v_or3 instead).
-        // s_nop 1: the two wait states between a VALU write of vcc and its
-        // read as a lane mask, which the compiler inserts for its own code
+    // z, y, x: idx = 2 idx + upper as one v_addc_co_u32 with the compare's
+    // mask as carry-in (the compiler builds 3 v_cndmask + v_or3 instead).
+    // s_nop 1: the two wait states between a VALU write of vcc and its read as
+    // a lane mask, which the compiler inserts for its own code (tools/isa_check.py
+    // check 3 holds this asm to it)
 #pragma unroll
-        for (int a = 2; a >= 0; --a) {
-            const uint32_t mid = r.p[a] | r.dim;
-            const float t = __builtin_fmaf(ffrom(mid), r.c[a], r.b[a]);
-            if (a == 2)
-                asm volatile("v_cmp_ge_f32_e32 vcc, %2, %3\n\t"
-                             "s_nop 1\n\t"
-                             "v_cndmask_b32_e32 %0, %0, %4, vcc\n\t"
-                             "v_cndmask_b32_e64 %1, 0, 1, vcc"
-                             : "+v"(r.p[a]), "=v"(nidx)
-                             : "v"(t), "v"(tm), "v"(mid)
-                             : "vcc");
-            else
-                asm volatile("v_cmp_ge_f32_e32 vcc, %2, %3\n\t"
-                             "s_nop 1\n\t"
-                             "v_cndmask_b32_e32 %0, %0, %4, vcc\n\t"
-                             "v_addc_co_u32_e32 %1, vcc, %1, %1, vcc"
-                             : "+v"(r.p[a]), "+v"(nidx)
-                             : "v"(t), "v"(tm), "v"(mid)
-                             : "vcc");
-        }
-    } else {
-#pragma unroll
-        for (int a = 0; a < 3; ++a) {
-            const uint32_t mid = r.p[a] | r.dim;
-            const bool upper = __builtin_fmaf(ffrom(mid), r.c[a], r.b[a]) >= tm;
-            nidx |= (uint32_t)upper << a;
-            r.p[a] = upper ? mid : r.p[a];
-        }
+    for (int a = 2; a >= 0; --a) {
+        const uint32_t mid = r.p[a] | r.dim;
+        const float t = __builtin_fmaf(ffrom(mid), r.c[a], r.b[a]);
+        if (a == 2)
+            asm volatile("v_cmp_ge_f32_e32 vcc, %2, %3\n\t"
+                         "s_nop 1\n\t"
+                         "v_cndmask_b32_e32 %0, %0, %4, vcc\n\t"
+                         "v_cndmask_b32_e64 %1, 0, 1, vcc"
+                         : "+v"(r.p[a]), "=v"(nidx)
+                         : "v"(t), "v"(tm), "v"(mid)
+                         : "vcc");
+        else
+            asm volatile("v_cmp_ge_f32_e32 vcc, %2, %3\n\t"
+                         "s_nop 1\n\t"
+                         "v_cndmask_b32_e32 %0, %0, %4, vcc\n\t"
+                         "v_addc_co_u32_e32 %1, vcc, %1, %1, vcc"
+                         : "+v"(r.p[a]), "+v"(nidx)
+                         : "v"(t), "v"(tm), "v"(mid)
+                         : "vcc");
     }
-#endif
     r.idx = nidx;
 }
 
-// OCH_BOUNCE_RESTART: a config-5 secondary ray walked by the lane that
-// walked its primary starts on the primary's LDS stack instead of loading
-// its way down from the root.  The reference traces the secondary from the
-// root (sse_trace(o2, d2), ORT/och_h_octree.h:292-447): setup, then PUSH and
-// descend (:342-376) with t_min = +0 until a PUSH finds its child empty or
-// the leaf level is reached.  Which child each of those PUSHes tests follows
-// from the ray alone (setup's idx, then fma(mid, c, b) >= t_min per level);
-// only the node words come from memory.  As long as the tested child is the
-// one the primary descended into at that level, the node is the primary's
-// ancestor, whose word the primary's walk left in this lane's stack slot of
-// the next level (a descent writes the parent's word at its level; at the
-// primary's HIT, slots 1..depth hold its ancestors).  So those descents read
-// the word from LDS -- no dependent global load -- and everything else
-// (geometry, PUSH count, stack contents) is the from-root walk's, bit for
-// bit.  The first PUSH off the primary's path, or at the leaf level, is the
-// ordinary ray_push_descend.  Children are compared as slot indices (idx ^
-// the sign mask), since the mirrored axis reflects the two rays' frames
-// differently: prim_p / prim_inv are the primary's position bits and sign
-// mask at its HIT (packed merged layout only).
-// Measured and not kept on: the descents it saves are L1 hits
-// (the primary walked those nodes an instant earlier), an LDS read costs
-// about as much, and the on-path loop runs its wave in lockstep -- in place,
-// 0.211 -> 0.219 ms per config-5 step.  Build option only.
-#ifndef OCH_BOUNCE_RESTART
-#define OCH_BOUNCE_RESTART 0
-#endif
-template <bool kCount, bool kAsm, bool kBox>
-__device__ __forceinline__ void ray_init_on_primary(Ray &r, const DevPool &P, const float *o, const float *d,
-                                                    uint32_t *stack, uint32_t stride, const uint32_t prim_p[3],
-                                                    uint32_t prim_inv)
-{
-    if (!ray_setup<kCount, true>(r, P, o, d, stack, stride)) return;
-    // target position bits: the primary's slot bits in this ray's frame
-    const uint32_t flip = prim_inv ^ r.inv;
-    const uint32_t t0 = prim_p[0] ^ (0u - (flip & 1u));
-    const uint32_t t1 = prim_p[1] ^ (0u - ((flip >> 1) & 1u));
-    const uint32_t t2 = prim_p[2] ^ (0u - ((flip >> 2) & 1u));
-    for (;;) {
-        const uint32_t present = __builtin_amdgcn_ubfe(r.cur, r.idx ^ r.inv, 1u);
-        const bool on_path = (((r.p[0] ^ t0) | (r.p[1] ^ t1) | (r.p[2] ^ t2)) & r.dim) == 0;
-        if (!present || !on_path || r.dim == P.dim_lo) break;
-        if (kCount) ++r.push;                                               // PUSH :342-344
-        r.sp += stride;                                                     // :357 (the slot holds this word)
-        r.cur = *r.sp;                                                      // the primary's next ancestor
-        r.dim >>= 1;                                                        // :361
-        const float tm = ffrom(r.t_min);
-        uint32_t nidx = 0;
-#pragma unroll
-        for (int a = 0; a < 3; ++a) {                                       // :363-373
-            const uint32_t mid = r.p[a] | r.dim;
-            const bool upper = __builtin_fmaf(ffrom(mid), r.c[a], r.b[a]) >= tm;
-            nidx |= (uint32_t)upper << a;
-            r.p[a] = upper ? mid : r.p[a];
-        }
-        r.idx = nidx;
-    }
-    ray_push_descend<kCount, kAsm, kBox>(r, P, stride);                     // the PUSH off the primary's path
-}
-
 template <int kPacked, bool kCount, bool kAsm = false>
-__device__ __forceinline__ void ray_iterate(Ray &r, const DevPool &P, uint32_t stride, const uint32_t *top = nullptr)
+__device__ __forceinline__ void ray_iterate(Ray &r, const DevPool &P, uint32_t stride)
 {
-    if (kPacked && OCH_MERGED_DESCEND) {
-        if (due_to_step(r)) ray_phase_step<kPacked>(r, stride);
-        // no activity test: a miss leaves the lane kStepping, a HIT ends in this phase
-        // tested before an opaque barrier on mode, so the skipping lanes' mode
+    if (kPacked) {
+        if (in_mode(r, kStepping)) ray_phase_step<kPacked>(r, stride);
+        // no activity test: a miss leaves the lane kStepping, a HIT ends in this phase.
+        // Tested before an opaque barrier on mode, so the skipping lanes' mode
         // is not re-materialised as kStepping after the test (nor copied)
         const bool push = r.mode != kStepping;
         asm volatile("" : "+v"(r.mode));
-        if (push) ray_push_descend<kCount, kAsm, kPacked == kPackedSkip>(r, P, stride, top);
+        if (push) ray_push_descend<kCount, kAsm>(r, P, stride);
         return;
     }
-    if (!kPacked && in_mode(r, kPending)) ray_phase_descend<kPacked>(r, P, stride);
+    if (in_mode(r, kPending)) ray_phase_descend_raw(r, stride);
     if (in_mode(r, kStepping)) ray_phase_step<kPacked>(r, stride);
-    if (kPacked && in_mode(r, kPending)) ray_phase_descend<kPacked>(r, P, stride);
-    if (in_mode(r, kAtPush) && ray_active(r, P)) ray_push<kPacked, kCount>(r, P);   // PUSH :342-344
-}
-
-// OCH_STEP_RUN: the packed walk as one descent per iteration -- every lane
-// STEPs (advancing, or POP-chaining then advancing) until it stands at a
-// present child, then all lanes descend together.  The same PUSH / STEP / POP
-// sequence per ray as ray_iterate, in half the iterations (a lane that finds an
-// empty child steps on at once instead of waiting for the next iteration).
-#ifndef OCH_STEP_RUN
-#define OCH_STEP_RUN 0
-#endif
-__device__ __forceinline__ bool child_present(const Ray &r)
-{
-    return __builtin_amdgcn_ubfe(r.cur, r.idx ^ r.inv, 1u) != 0;
-}
-
-template <bool kCount>
-__device__ __forceinline__ void ray_walk_packed(Ray &r, const DevPool &P, uint32_t stride)
-{
-    while (ray_active(r, P)) {
-        // the child of the node the last descent loaded (or ray_init's root PUSH)
-        if (r.mode != kStepping) {
-            if (kCount) ++r.push;
-            if (!child_present(r)) r.mode = kStepping;
-        }
-        while (r.mode == kStepping && ray_active(r, P)) {
-            ray_phase_step<true>(r, stride);                    // advance, or POP chain + advance
-            if (r.mode != kStepping) {
-                if (kCount) ++r.push;                           // PUSH :342-344
-                if (!child_present(r)) r.mode = kStepping;
-            }
-        }
-        if (r.mode != kStepping) ray_descend<kCount>(r, P, stride);
-    }
+    if (in_mode(r, kAtPush) && ray_active(r, P)) ray_push_raw<kCount>(r, P);   // PUSH :342-344
 }
 
 // Walk an initialised ray to its HIT or MISS.
 template <int kPacked, bool kCount, bool kAsm = false>
-__device__ __forceinline__ void ray_run(Ray &r, const DevPool &P, uint32_t stride, const uint32_t *top = nullptr)
+__device__ __forceinline__ void ray_run(Ray &r, const DevPool &P, uint32_t stride)
 {
-    if (kPacked && OCH_STEP_RUN && OCH_MERGED_DESCEND && OCH_LOAD_INTO_CUR && OCH_POP_CHAIN && !OCH_LDS_TOP) {
-        ray_walk_packed<kCount>(r, P, stride);
-        return;
-    }
     if (ray_active(r, P)) do {
-        ray_iterate<kPacked, kCount, kAsm>(r, P, stride, top);
+        ray_iterate<kPacked, kCount, kAsm>(r, P, stride);
     } while (ray_active(r, P));
 }
 
-// The hit record of a finished ray (:346-355 hit, :423-431 miss).  The
-// merged loop (OCH_LOAD_INTO_CUR) leaves a HIT's voxel id in cur.
+// The hit record of a finished ray (:346-355 hit, :423-431 miss).  The packed
+// walk leaves a HIT's voxel id in cur, the raw walk in child.
 template <int kPacked, bool kAsm = false>
 __device__ __forceinline__ Hit ray_result(Ray &r, const DevPool &P)
 {
     Hit h;
-    wait_cur<kAsm>(r);                      // a HIT's voxel id load (OCH_ASM_LOAD)
+    wait_cur<kAsm>(r);                      // a HIT's voxel id load (the asm load)
     const uint32_t cur = r.cur;
-    if (OCH_DIM_LEVEL ? r.dim > (1u << 22) : r.level == 0) {
+    if (r.dim > (1u << 22)) {
         h.dir = OCH_EXIT;
         h.voxel = 0;
         h.t = P.miss_bits;
     } else {
         h.dir = (int32_t)((r.min_axis >> 1) + 3u * ((r.inv & r.min_axis & 7u) == 0));
-        h.voxel = (kPacked && OCH_MERGED_DESCEND && OCH_LOAD_INTO_CUR) ? cur : r.child;
+        h.voxel = kPacked ? cur : r.child;
         h.t = r.t_min;
     }
     h.push = r.push;
@@ -1002,21 +546,13 @@ struct ArraySource {
         out = i;
         return true;
     }
-    __device__ __forceinline__ bool get_wave(uint32_t wave_base, uint32_t lane, float *o, float *d, uint32_t &out) const
-    {
-        return get(wave_base + lane, o, d, out);
-    }
-    // Arbitrary rays: no shortcut (see CameraSource::get_wave_culled).
+    // Arbitrary rays: no camera shortcut (see CameraSource::get_wave_culled);
+    // ray_init's exact cull still applies.
     __device__ __forceinline__ bool get_wave_culled(uint32_t wave_base, uint32_t lane, const DevPool &, bool,
                                                     float *o, float *d, uint32_t &out, bool &miss) const
     {
         miss = false;
         return get(wave_base + lane, o, d, out);
-    }
-    // Refill: ray base + k, base wave-uniform, k < 64.
-    __device__ __forceinline__ bool get_refill(uint32_t base, uint32_t k, float *o, float *d, uint32_t &out) const
-    {
-        return get(base + k, o, d, out);
     }
 };
 
@@ -1088,10 +624,7 @@ __device__ __forceinline__ void camera_ray(const och_camera &C, int col, int row
 }
 
 // Pixel tile of one wave: kTileW x kTileH = 64 pixels.
-#ifndef OCH_TILE_W
-#define OCH_TILE_W 8
-#endif
-constexpr uint32_t kTileW = OCH_TILE_W, kTileH = 64 / OCH_TILE_W;
+constexpr uint32_t kTileW = 8, kTileH = 64 / kTileW;
 
 // Division by a launch constant: n / d = (mulhi(n, m) + n) >> s for every
 // 32-bit n, with m, s from the host (round-up multiplier; checked against
@@ -1141,24 +674,12 @@ struct TiledArraySource {
         out = i;
         return true;
     }
-    __device__ __forceinline__ bool get(uint32_t i, float *o, float *d, uint32_t &out) const
-    {
-        return at(i >> 6, i & 63u, o, d, out);
-    }
-    __device__ __forceinline__ bool get_wave(uint32_t wave_base, uint32_t lane, float *o, float *d, uint32_t &out) const
-    {
-        return at(__builtin_amdgcn_readfirstlane(wave_base >> 6), lane, o, d, out);
-    }
     // Arbitrary rays: no camera shortcut; ray_init's exact cull still applies.
     __device__ __forceinline__ bool get_wave_culled(uint32_t wave_base, uint32_t lane, const DevPool &, bool,
                                                     float *o, float *d, uint32_t &out, bool &miss) const
     {
         miss = false;
-        return get_wave(wave_base, lane, o, d, out);
-    }
-    __device__ __forceinline__ bool get_refill(uint32_t base, uint32_t k, float *o, float *d, uint32_t &out) const
-    {
-        return get(base + k, o, d, out);
+        return at(__builtin_amdgcn_readfirstlane(wave_base >> 6), lane, o, d, out);
     }
 };
 
@@ -1184,7 +705,7 @@ struct CameraSource {
         return g < 0 ? height : g * row_chunk + within;
     }
     __host__ __device__ __forceinline__ uint32_t count() const { return per_view * (uint32_t)n_views; }
-    // Tile of ray i (tile-granular index math, identical in get and get_wave).
+    // Tile of ray i.
     __device__ __forceinline__ void tile_of(uint32_t i, uint32_t &view, uint32_t &tx, uint32_t &ty) const
     {
         view = by_per_view.div(i);
@@ -1198,39 +719,10 @@ struct CameraSource {
             tx = tile - ty * tiles_x;
         }
     }
-    __device__ __forceinline__ bool finish(uint32_t view, int col, int srow, int row, float *o, float *d,
-                                           uint32_t &out) const
-    {
-        if (row >= height) return false;
-        const och_camera &C = cam[view];
-        o[0] = C.pos[0]; o[1] = C.pos[1]; o[2] = C.pos[2];
-        camera_ray(C, col, row, d);
-        out = view * slice_pixels + (uint32_t)srow * (uint32_t)width + (uint32_t)col;
-        return true;
-    }
-    // Any ray index (the persistent schedule hands out arbitrary indices).
-    __device__ __forceinline__ bool get(uint32_t i, float *o, float *d, uint32_t &out) const
-    {
-        uint32_t view, tx, ty;
-        tile_of(i, view, tx, ty);
-        const uint32_t lane = i & 63u;
-        const int col = (int)(tx * kTileW + lane % kTileW);
-        const int srow = (int)(ty * kTileH + lane / kTileW);
-        if (col >= width || srow >= slice_rows) return false;
-        const int chunk = (int)by_row_chunk.div((uint32_t)srow), within = srow - chunk * row_chunk;
-        return finish(view, col, srow, global_row(chunk, within), o, d, out);
-    }
-    // One wave's tile: wave_base (a multiple of 64, wave-uniform) moves the
-    // tile arithmetic, divisions included, to the scalar unit.
-    __device__ __forceinline__ bool get_wave(uint32_t wave_base, uint32_t lane, float *o, float *d, uint32_t &out) const
-    {
-        uint32_t view;
-        int col, srow, row;
-        if (!locate_wave(wave_base, lane, view, col, srow, row)) return false;
-        return finish(view, col, srow, row, o, d, out);
-    }
-    // get_wave, or miss = true without a ray when camera_proven_miss shows
-    // the ray ends as the MISS (cull: the launch may cull, OCH_OPT_CULL).
+    // One wave's tile, or miss = true without a ray when camera_proven_miss
+    // shows the ray ends as the MISS (cull: the launch may cull,
+    // OCH_OPT_CULL).  wave_base (a multiple of 64, wave-uniform) moves the tile
+    // arithmetic, divisions included, to the scalar unit.
     __device__ __forceinline__ bool get_wave_culled(uint32_t wave_base, uint32_t lane, const DevPool &P, bool cull,
                                                     float *o, float *d, uint32_t &out, bool &miss) const
     {
@@ -1271,41 +763,6 @@ struct CameraSource {
         }
         return row < height;
     }
-    // Refill (k_trace_refill): ray base + k, base wave-uniform, k < 64.  The
-    // rays span at most two tiles, A = base / 64 and A + 1, whose coordinates
-    // are wave-uniform (scalar unit); each lane selects its tile.  A chunk of
-    // the refill schedule never crosses a view (per_view is a multiple of the
-    // chunk), so both tiles share the view.
-    __device__ __forceinline__ bool get_refill(uint32_t base, uint32_t k, float *o, float *d, uint32_t &out) const
-    {
-        base = __builtin_amdgcn_readfirstlane(base);
-        uint32_t view, txa, tya, vb, txb, tyb;
-        tile_of(base, view, txa, tya);
-        tile_of(base + 64u, vb, txb, tyb);
-        view = __builtin_amdgcn_readfirstlane(view);
-        txa = __builtin_amdgcn_readfirstlane(txa);
-        tya = __builtin_amdgcn_readfirstlane(tya);
-        txb = __builtin_amdgcn_readfirstlane(txb);
-        tyb = __builtin_amdgcn_readfirstlane(tyb);
-        const uint32_t j = (base & 63u) + k;                  // < 128
-        const bool in_a = j < 64u;
-        const uint32_t pix = j & 63u;
-        const uint32_t tx = in_a ? txa : txb, ty = in_a ? tya : tyb;
-        const int col = (int)(tx * kTileW + pix % kTileW);
-        const int srow = (int)(ty * kTileH + pix / kTileW);
-        if (col >= width || srow >= slice_rows) return false;
-        int row;
-        if (row_chunk % (int)kTileH == 0) {                    // each tile lies inside one row chunk
-            const int ca = __builtin_amdgcn_readfirstlane((int)by_row_chunk.div(tya * kTileH));
-            const int cb = __builtin_amdgcn_readfirstlane((int)by_row_chunk.div(tyb * kTileH));
-            const int chunk = in_a ? ca : cb;
-            row = global_row(chunk, srow - chunk * row_chunk);
-        } else {
-            const int chunk = (int)by_row_chunk.div((uint32_t)srow);
-            row = global_row(chunk, srow - chunk * row_chunk);
-        }
-        return finish(view, col, srow, row, o, d, out);
-    }
 };
 
 // ---------------------------------------------------------------- sinks
@@ -1334,27 +791,11 @@ __device__ __forceinline__ uint32_t pixel_colour(const Hit &h, const uint32_t *p
     return palette[6u * (h.voxel - 1u) + (uint32_t)h.dir];
 }
 
-// OCH_NT_FRAME: the RGBA8 frame words are stored non-temporally (streamed
-// past L2 / MALL, which hold the DAG), as k_shade_unshard4 stores its frames.
-#ifndef OCH_NT_FRAME
-#define OCH_NT_FRAME 0
-#endif
-__device__ __forceinline__ void frame_store(uint32_t *out, uint32_t i, uint32_t c)
-{
-    if (OCH_NT_FRAME)
-        __builtin_nontemporal_store(c, out + i);
-    else
-        out[i] = c;
-}
-
 struct FrameSink {
     uint32_t *out;
     const uint32_t *palette;
     uint32_t n_voxels;
-    __device__ __forceinline__ void put(uint32_t i, const Hit &h) const
-    {
-        frame_store(out, i, pixel_colour(h, palette, n_voxels));
-    }
+    __device__ __forceinline__ void put(uint32_t i, const Hit &h) const { out[i] = pixel_colour(h, palette, n_voxels); }
 };
 
 // Config 5 sinks.  put_primary stores what is final for a ray without a
@@ -1367,12 +808,12 @@ struct BounceFrameSink {
     __device__ __forceinline__ uint32_t put_primary(uint32_t i, const Hit &h, bool bounced) const
     {
         const uint32_t c = pixel_colour(h, f.palette, f.n_voxels);
-        if (!bounced) frame_store(f.out, i, c);
+        if (!bounced) f.out[i] = c;
         return c;
     }
     __device__ __forceinline__ void put_secondary(uint32_t i, uint32_t c, const Hit &h2) const
     {
-        frame_store(f.out, i, h2.dir == OCH_EXIT ? c : (((c >> 1) & 0x007F7F7Fu) | (c & 0xFF000000u)));
+        f.out[i] = h2.dir == OCH_EXIT ? c : (((c >> 1) & 0x007F7F7Fu) | (c & 0xFF000000u));
     }
 };
 
@@ -1483,59 +924,15 @@ __device__ __forceinline__ uint32_t xcd_block(uint32_t b, uint32_t nb, uint32_t 
 // most expensive workgroups of the planning frame first, so the frame does not
 // end on a few late grazing tiles); cost: optional per-block duration in
 // shader clocks (the planning launch).  Placement only: results are the same.
-// OCH_GRID_VGPR: occupancy experiments -- the grid kernel claims VGPRs up to
-// this register (a clobber of it), so its allocation caps the waves per SIMD
-// (8 up to v63, 7 to v71, 6 to v79, 5 to v95, 4 to v127) and fewer waves
-// share a CU's L1.
-#define OCH_STR2(x) #x
-#define OCH_STR(x) OCH_STR2(x)
 template <class Src, class Sink, int kPacked, bool kCount>
 __global__ void k_trace_grid(DevPool P, Src S, Sink K, uint32_t xcd_group, const uint32_t *__restrict__ order,
                              uint32_t *__restrict__ cost, uint64_t *stamps, uint32_t stamp_cap)
 {
-#ifdef OCH_GRID_VGPR
-    asm volatile("; occupancy cap" ::: "v" OCH_STR(OCH_GRID_VGPR));
-#endif
     extern __shared__ uint32_t lds_stack[];
     const uint64_t t0 = stamps ? realtime() : 0;
     const uint64_t c0 = cost ? __builtin_amdgcn_s_memtime() : 0;
-    const uint32_t *top = nullptr;
-    if (OCH_LDS_TOP && kPacked) {
-        uint32_t *t = lds_stack + (P.depth + 1) * blockDim.x;
-        for (uint32_t i = threadIdx.x; i < 8u * P.top_ids[OCH_LDS_TOP]; i += blockDim.x) t[i] = P.nodes[i];
-        __syncthreads();
-        top = t;
-    }
     const uint32_t blk = order ? order[blockIdx.x] : xcd_block(blockIdx.x, gridDim.x, xcd_group);
     const uint32_t lane = threadIdx.x & 63u;
-#if OCH_DUAL
-    // Two rays per lane (experiment): the wave walks the tiles 2w and 2w + 1
-    // as two independent rays per lane, each with its own LDS stack column,
-    // so one ray's slot load is hidden behind the other's instructions.
-    {
-        const uint32_t wave = blk * (blockDim.x >> 6) + (threadIdx.x >> 6);
-        const uint32_t base_a = wave * 128u, base_b = base_a + 64u;
-        const uint32_t col = (P.depth + 1) * blockDim.x;
-        float oa[3], da[3], ob[3], db[3];
-        uint32_t out_a = 0, out_b = 0;
-        Ray ra, rb;
-        ra.dim = 0;
-        rb.dim = 0;
-        if (base_a + lane < S.count() && S.get_wave(base_a, lane, oa, da, out_a))
-            ray_init<kPacked, kCount>(ra, P, oa, da, lds_stack + threadIdx.x, blockDim.x);
-        if (base_b + lane < S.count() && S.get_wave(base_b, lane, ob, db, out_b))
-            ray_init<kPacked, kCount>(rb, P, ob, db, lds_stack + col + threadIdx.x, blockDim.x);
-        const bool had_a = ra.dim != 0, had_b = rb.dim != 0;
-        for (;;) {
-            const bool ea = ray_active(ra, P), eb = ray_active(rb, P);
-            if (!ea && !eb) break;
-            if (ea) ray_iterate<kPacked, kCount>(ra, P, blockDim.x, top);
-            if (eb) ray_iterate<kPacked, kCount>(rb, P, blockDim.x, top);
-        }
-        if (had_a) K.put(out_a, ray_result<kPacked>(ra, P));
-        if (had_b) K.put(out_b, ray_result<kPacked>(rb, P));
-    }
-#else
     const uint32_t wave_base = blk * blockDim.x + (threadIdx.x & ~63u);
     float o[3], d[3];
     uint32_t out;
@@ -1546,152 +943,13 @@ __global__ void k_trace_grid(DevPool P, Src S, Sink K, uint32_t xcd_group, const
             K.put(out, Hit{OCH_EXIT, 0u, P.miss_bits, 0u});
         } else {
             Ray r;
-            ray_init<kPacked, kCount, true, kAsmLoad, true>(r, P, o, d, lds_stack + threadIdx.x, blockDim.x);
-            ray_run<kPacked, kCount, kAsmLoad>(r, P, blockDim.x, top);
+            ray_init<kPacked, kCount, true, kAsmLoad>(r, P, o, d, lds_stack + threadIdx.x, blockDim.x);
+            ray_run<kPacked, kCount, kAsmLoad>(r, P, blockDim.x);
             K.put(out, ray_result<kPacked, kAsmLoad>(r, P));
         }
     }
-#endif
     if (cost && threadIdx.x == 0) cost[blk] = (uint32_t)(__builtin_amdgcn_s_memtime() - c0);
     if (stamps) stamp(stamps, stamp_cap, t0, 64);
-}
-
-// Grid schedule with in-block wave merging (OCH_OPT_MERGE = K; the lever
-// DESIGN.md §8's lockstep model priced at -6..-9 % VALU per wave).  A block of
-// several waves walks its rays K iterations at a time; between rounds the
-// waves retire their finished rays and count the rest, and when the rays left
-// fit in fewer waves, the highest waves hand theirs to the free lanes of the
-// lower ones and exit, so no wave keeps issuing for a handful of lanes.  A
-// moved ray keeps its LDS stack column (the block's LDS outlives its waves);
-// its registers travel as 13 words through the LDS column of the free lane
-// that adopts it (a finished ray's stack, idle until then).  Every exchange
-// is behind block barriers, which count only the waves still running.
-constexpr int kMergeWords = 13;
-
-__device__ __forceinline__ void merge_pack(const Ray &r, uint32_t out, uint32_t column, uint32_t w[kMergeWords])
-{
-    for (int a = 0; a < 3; ++a) {
-        w[a] = fbits(r.c[a]);
-        w[3 + a] = fbits(r.b[a]);
-        w[6 + a] = r.p[a];
-    }
-    w[9] = r.cur;
-    w[10] = r.t_min;
-    w[11] = out;
-    // ctz(dim) 5 bits | idx 3 | inv & 7 3 | min_axis 4 | mode 4 | stack column 13
-    w[12] = (uint32_t)__builtin_ctz(r.dim) | (r.idx << 5) | ((r.inv & 7u) << 8) | (r.min_axis << 11) |
-            (r.mode << 15) | (column << 19);
-}
-
-__device__ __forceinline__ void merge_unpack(Ray &r, uint32_t &out, const uint32_t w[kMergeWords], uint32_t *lds,
-                                             uint32_t stride)
-{
-    for (int a = 0; a < 3; ++a) {
-        r.c[a] = ffrom(w[a]);
-        r.b[a] = ffrom(w[3 + a]);
-        r.p[a] = w[6 + a];
-    }
-    r.cur = w[9];
-    r.t_min = w[10];
-    out = w[11];
-    const uint32_t m = w[12], k = m & 31u;
-    r.dim = 1u << k;
-    r.idx = (m >> 5) & 7u;
-    r.inv = 24u | ((m >> 8) & 7u);
-    r.min_axis = (m >> 11) & 15u;
-    r.mode = (m >> 15) & 15u;
-    r.sp23 = lds + (m >> 19) + 23u * stride;
-    r.sp = r.sp23 - k * stride;
-    r.box = 0;                  // a moved ray walks on without the per-node skip
-    r.skipmask = 0;
-}
-
-template <class Src, class Sink, int kPacked>
-__global__ void k_trace_grid_merge(DevPool P, Src S, Sink K, int merge_k, const uint32_t *__restrict__ order)
-{
-    extern __shared__ uint32_t lds_stack[];
-    __shared__ uint32_t wave_count[16];
-    __shared__ uint32_t free_list[1024];
-    const uint32_t nb = blockDim.x, n_waves = nb >> 6;
-    const uint32_t blk = order ? order[blockIdx.x] : blockIdx.x;
-    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
-    const uint64_t below = (1ull << lane) - 1ull;
-    const uint32_t wave_base = blk * nb + (threadIdx.x & ~63u);
-    float o[3], d[3];
-    uint32_t out = 0;
-    bool miss, has = false;
-    Ray r;
-    r.dim = 0;
-    if (wave_base + lane < S.count() && S.get_wave_culled(wave_base, lane, P, P.cull != 0, o, d, out, miss)) {
-        if (miss) {
-            K.put(out, Hit{OCH_EXIT, 0u, P.miss_bits, 0u});
-        } else {
-            ray_init<kPacked, false, true, kAsmLoad>(r, P, o, d, lds_stack + threadIdx.x, nb);
-            has = true;
-        }
-    }
-    uint32_t alive = n_waves;                                   // waves 0 .. alive-1 still run (block-uniform)
-    for (;;) {
-        for (int k = 0; k < merge_k; ++k) {                     // one round of walking
-            const bool walking = has && ray_active(r, P);
-            if (__ballot(walking) == 0) break;
-            if (walking) ray_iterate<kPacked, false, kAsmLoad>(r, P, nb);
-        }
-        if (has && !ray_active(r, P)) {                         // retire
-            K.put(out, ray_result<true, kAsmLoad>(r, P));
-            has = false;
-        }
-        const uint64_t bal = __ballot(has);
-        if (lane == 0) wave_count[wave] = (uint32_t)__popcll(bal);
-        __syncthreads();
-        uint32_t total = 0;
-        for (uint32_t w = 0; w < alive; ++w) total += wave_count[w];
-        if (total == 0) break;                                  // every surviving wave sees the same total
-        const uint32_t keep = (total + 63u) >> 6;               // waves the rays left fit in
-        if (keep < alive) {
-            // free lanes of the kept waves, ranked, publish their thread ids
-            if (wave < keep && !has) {
-                uint32_t rank = (uint32_t)__popcll(~bal & below);
-                for (uint32_t w = 0; w < wave; ++w) rank += 64u - wave_count[w];
-                free_list[rank] = threadIdx.x;
-            }
-            __syncthreads();
-            if (wave >= keep && has) {                          // the movers: write into the adopter's column
-                uint32_t rank = (uint32_t)__popcll(bal & below);
-                for (uint32_t w = keep; w < wave; ++w) rank += wave_count[w];
-                wait_cur<kAsmLoad>(r);
-                if (kPacked == kPackedSkip && r.mode == kUndoDescent)
-                    ray_undo_descent(r, nb);                    // the mode field has 4 bits
-                uint32_t st[kMergeWords];
-                // the ray's own stack column (not this lane's: a ray adopted
-                // earlier walks on the column it started in)
-                const uint32_t column = (uint32_t)(r.sp23 - lds_stack) - 23u * nb;
-                merge_pack(r, out, column, st);
-                uint32_t *dst = lds_stack + free_list[rank];
-                for (int i = 0; i < kMergeWords; ++i) dst[i * nb] = st[i];
-                has = false;
-            }
-            __syncthreads();
-            uint32_t movers = 0;
-            for (uint32_t w = keep; w < alive; ++w) movers += wave_count[w];
-            if (wave < keep && !has) {                          // the adopters
-                uint32_t rank = (uint32_t)__popcll(~bal & below);
-                for (uint32_t w = 0; w < wave; ++w) rank += 64u - wave_count[w];
-                if (rank < movers) {
-                    uint32_t st[kMergeWords];
-                    const uint32_t *src = lds_stack + threadIdx.x;
-                    for (int i = 0; i < kMergeWords; ++i) st[i] = src[i * nb];
-                    merge_unpack(r, out, st, lds_stack, nb);
-                    has = true;
-                }
-            }
-            __syncthreads();                                    // columns read; counts reusable
-            if (wave >= keep) return;                           // this wave's rays live on in the kept waves
-            alive = keep;
-        } else {
-            __syncthreads();                                    // counts read before the next round writes them
-        }
-    }
 }
 
 // Config 5: primary rays, then wavefront compaction -- the block's hit
@@ -1701,22 +959,17 @@ __global__ void k_trace_grid_merge(DevPool P, Src S, Sink K, int merge_k, const 
 // a few bounced lanes.  The queue (8 words per thread, SoA) reuses the
 // parent stacks' LDS between the passes.
 // compact (OCH_OPT_BOUNCE_COMPACT): 0 = every secondary ray in place (by the
-// lane that walked its primary; started on the primary's stack with
-// OCH_BOUNCE_RESTART); 1 = always through the queue; 2 = per block: through
-// the queue when it packs the block's secondary rays into fewer waves than
-// hold them in place, else in place.  On the bench's terrain 98.7 % of the
-// secondary rays sit in waves whose 64 lanes all bounce, so the queue frees
-// few waves; it is still the fastest of the three.
+// lane that walked its primary); 1 = always through the queue; 2 = per block:
+// through the queue when it packs the block's secondary rays into fewer waves
+// than hold them in place, else in place.  On the bench's terrain 98.7 % of
+// the secondary rays sit in waves whose 64 lanes all bounce, so the queue
+// frees few waves and the three modes are within about 1 %.
 template <int kPacked, bool kCount, class Sink>
 __device__ __forceinline__ void bounce_in_place(const DevPool &P, const Sink &K, uint32_t *stack, uint32_t nb,
-                                                const float *o2, const float *d2, uint32_t out, uint32_t payload,
-                                                const uint32_t prim_p[3], uint32_t prim_inv)
+                                                const float *o2, const float *d2, uint32_t out, uint32_t payload)
 {
     Ray r;
-    if (kPacked && OCH_MERGED_DESCEND && OCH_LOAD_INTO_CUR && OCH_BOUNCE_RESTART && !OCH_LDS_TOP)
-        ray_init_on_primary<kCount, kAsmLoad, kPacked == kPackedSkip>(r, P, o2, d2, stack, nb, prim_p, prim_inv);
-    else
-        ray_init<kPacked, kCount, true, kAsmLoad>(r, P, o2, d2, stack, nb);
+    ray_init<kPacked, kCount, true, kAsmLoad>(r, P, o2, d2, stack, nb);
     ray_run<kPacked, kCount, kAsmLoad>(r, P, nb);
     K.put_secondary(out, payload, ray_result<kPacked, kAsmLoad>(r, P));
 }
@@ -1735,7 +988,7 @@ __global__ void k_trace_bounce(DevPool P, Src S, Sink K, int compact, const uint
     const uint32_t nb = blockDim.x;
     const uint32_t wave_base = blk * nb + (threadIdx.x & ~63u);
     float o[3], d[3], o2[3], d2[3];
-    uint32_t out = 0, payload = 0, prim_p[3] = {0u, 0u, 0u}, prim_inv = 0;
+    uint32_t out = 0, payload = 0;
     bool want = false;
     bool miss;
     if (wave_base + (threadIdx.x & 63u) < S.count() &&
@@ -1750,12 +1003,8 @@ __global__ void k_trace_bounce(DevPool P, Src S, Sink K, int compact, const uint
             want = h1.dir < OCH_EXIT;
             if (want) bounce_ray(o, d, h1, P.half_voxel, o2, d2);
             payload = K.put_primary(out, h1, want);
-            prim_p[0] = r.p[0];
-            prim_p[1] = r.p[1];
-            prim_p[2] = r.p[2];
-            prim_inv = r.inv;
             if (want && compact == 0)                                       // in place, no compaction
-                bounce_in_place<kPacked, kCount>(P, K, stack, nb, o2, d2, out, payload, prim_p, prim_inv);
+                bounce_in_place<kPacked, kCount>(P, K, stack, nb, o2, d2, out, payload);
         }
     }
     if (compact == 0) {
@@ -1776,7 +1025,7 @@ __global__ void k_trace_bounce(DevPool P, Src S, Sink K, int compact, const uint
     }
     if (compact == 2 && (total + 63u) / 64u >= holding) {
         // the queue would not free a wave (block-uniform): in place
-        if (want) bounce_in_place<kPacked, kCount>(P, K, stack, nb, o2, d2, out, payload, prim_p, prim_inv);
+        if (want) bounce_in_place<kPacked, kCount>(P, K, stack, nb, o2, d2, out, payload);
         if (cost && threadIdx.x == 0) cost[blk] = (uint32_t)(__builtin_amdgcn_s_memtime() - c0);
         if (stamps) stamp(stamps, stamp_cap, t0, 0);
         return;
@@ -1812,115 +1061,6 @@ __global__ void k_trace_bounce(DevPool P, Src S, Sink K, int compact, const uint
     }
     if (cost && threadIdx.x == 0) cost[blk] = (uint32_t)(__builtin_amdgcn_s_memtime() - c0);
     if (stamps) stamp(stamps, stamp_cap, t0, total);
-}
-
-// Grid schedule with lane refill (north_star's wavefront compaction of
-// active rays): each wave owns a chunk of `chunk_rays` consecutive rays (a
-// few 8x8 tiles) and walks them with its 64 lanes.  Whenever at least
-// `refill_min` lanes have finished (ballot + popcount, wave-uniform), the
-// finished lanes write their records and the idle lanes take the chunk's
-// next rays in lane order (prefix popcount), so a wave's lanes stay busy
-// until its chunk runs dry instead of idling beside its slowest ray.  Ray
-// setup (raygen + ray_init) runs once per refill on the idle lanes only; the
-// tile arithmetic of a refill is wave-uniform (get_refill).
-constexpr uint32_t kNoRay = 0xFFFFFFFFu;
-
-template <class Src, class Sink, int kPacked, bool kCount>
-__global__ void k_trace_refill(DevPool P, Src S, Sink K, uint32_t chunk_rays, int refill_min, uint64_t *stamps,
-                               uint32_t stamp_cap)
-{
-    extern __shared__ uint32_t lds_stack[];
-    const uint64_t t0 = stamps ? realtime() : 0;
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t wave = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-    uint32_t *stack = lds_stack + threadIdx.x;
-    const uint32_t n = S.count();
-    uint32_t cursor = wave * chunk_rays;                            // wave-uniform
-    const uint32_t end = min(cursor + chunk_rays, n);
-    Ray r;
-    r.level = 0;                                                    // no ray: not active
-    r.dim = 0;
-    uint32_t out = kNoRay;
-    uint64_t finished = 0;
-    const uint64_t below = (1ull << lane) - 1ull;
-    for (;;) {
-        // Retire: finished lanes write their record.
-        if (out != kNoRay && !ray_active(r, P)) {
-            K.put(out, ray_result<kPacked>(r, P));
-            out = kNoRay;
-            ++finished;
-        }
-        // Refill the idle lanes from the chunk.
-        uint64_t idle = __ballot(out == kNoRay);
-        if (cursor < end) {
-            const uint32_t n_idle = (uint32_t)__popcll(idle);
-            const uint32_t take = min(n_idle, end - cursor);
-            if (out == kNoRay) {
-                const uint32_t k = (uint32_t)__popcll(idle & below);
-                float o[3], d[3];
-                if (k < take && S.get_refill(cursor, k, o, d, out))
-                    ray_init<kPacked, kCount>(r, P, o, d, stack, blockDim.x);
-                else
-                    out = kNoRay;
-            }
-            cursor += take;
-        }
-        if (cursor >= end && __ballot(out != kNoRay) == 0) break;
-        // Walk until refill_min lanes are idle (all of them once the chunk is dry).
-        const uint32_t keep = cursor < end ? 64u - (uint32_t)refill_min : 0u;
-        do {
-            if (ray_active(r, P)) ray_iterate<kPacked, kCount>(r, P, blockDim.x);
-        } while ((uint32_t)__popcll(__ballot(ray_active(r, P))) > keep);
-    }
-    if (stamps) stamp(stamps, stamp_cap, t0, finished);
-}
-
-template <class Src, class Sink, int kPacked, bool kCount>
-__global__ void k_trace_persistent(DevPool P, Src S, Sink K, uint32_t *counter, int refill_min, uint64_t *stamps,
-                                   uint32_t stamp_cap)
-{
-    extern __shared__ uint32_t lds_stack[];
-    const uint64_t t0 = stamps ? realtime() : 0;
-    uint32_t *stack = lds_stack + threadIdx.x;
-    const uint32_t n = S.count();
-    const int lane = threadIdx.x & 63;
-    const uint64_t below = (1ull << lane) - 1ull;
-    Ray r;
-    uint32_t out = 0;
-    bool active = false, drained = false;
-    uint64_t finished = 0;
-    for (;;) {
-        const uint64_t idle = __ballot(!active);
-        const int n_idle = __popcll(idle);
-        if (!drained && n_idle >= refill_min) {               // wave-uniform
-            const int leader = __ffsll((unsigned long long)idle) - 1;
-            uint32_t base = 0;
-            if (lane == leader) base = atomicAdd(counter, (uint32_t)n_idle);
-            base = __shfl(base, leader);
-            drained = base + (uint32_t)n_idle >= n;
-            if (!active) {
-                const uint32_t i = base + (uint32_t)__popcll(idle & below);
-                float o[3], d[3];
-                if (i < n && S.get(i, o, d, out)) {
-                    ray_init<kPacked, kCount>(r, P, o, d, stack, blockDim.x);
-                    active = true;
-                }
-            }
-        }
-        if (__ballot(active) == 0) {
-            if (drained) break;
-            continue;
-        }
-        if (active) {
-            ray_iterate<kPacked, kCount>(r, P, blockDim.x);
-            if (!ray_active(r, P)) {
-                K.put(out, ray_result<kPacked>(r, P));
-                active = false;
-                ++finished;
-            }
-        }
-    }
-    if (stamps) stamp(stamps, stamp_cap, t0, finished);
 }
 
 __global__ __launch_bounds__(256) void k_raygen(och_camera C, float *__restrict__ dirs)
@@ -2028,44 +1168,17 @@ size_t stack_bytes(int depth, int block) { return (size_t)(depth + 1) * block * 
 
 template <class Src, class Sink, int kPacked, bool kCount>
 hipError_t launch_as(const DevPool &p, const Src &s, const Sink &k, uint32_t n, const Schedule &sc, hipStream_t stream,
-                     uint32_t supertile_rays = 0)
+                     uint32_t supertile_rays)
 {
     if (n == 0) return hipSuccess;
     const int block = sc.block;
-#ifndef OCH_LDS_MIN
-#define OCH_LDS_MIN 0     // occupancy experiments: pad each block's LDS to this many bytes
-#endif
-    size_t lds = stack_bytes(p.depth, block) > OCH_LDS_MIN ? stack_bytes(p.depth, block) : OCH_LDS_MIN;
-    if (OCH_LDS_TOP && kPacked && sc.kind == 0) lds += 32u * p.top_ids[OCH_LDS_TOP];
-    if (sc.kind == 2) {
-        const uint32_t chunk = 64u * (uint32_t)sc.chunk_tiles;
-        const uint32_t waves = (n + chunk - 1) / chunk, wpb = (uint32_t)block / 64u;
-        OCH_LAUNCH_TIMED(sc, (k_trace_refill<Src, Sink, kPacked, kCount>), dim3((waves + wpb - 1) / wpb), dim3(block),
-                           lds, stream, p, s, k, chunk, sc.refill_min, sc.stamps, sc.stamp_cap);
-    } else if (sc.kind == 1) {
-        hipError_t e = hipMemsetAsync(sc.counter, 0, sizeof(uint32_t), stream);
-        if (e != hipSuccess) return e;
-        const uint32_t blocks_per_cu = (uint32_t)((sc.waves_per_cu * 64 + block - 1) / block);
-        uint32_t grid = (uint32_t)sc.cus * blocks_per_cu;
-        const uint32_t needed = (n + block - 1) / block;
-        if (grid > needed) grid = needed;
-        OCH_LAUNCH_TIMED(sc, (k_trace_persistent<Src, Sink, kPacked, kCount>), dim3(grid), dim3(block), lds, stream, p, s,
-                           k, sc.counter, sc.refill_min, sc.stamps, sc.stamp_cap);
-    } else if (sc.merge_k > 0 && kPacked && !kCount && block >= 128 && block <= 1024) {
-        const uint32_t grid = (n + block - 1) / block;
-        OCH_LAUNCH_TIMED(sc, (k_trace_grid_merge<Src, Sink, kPacked ? kPacked : 1>), dim3(grid), dim3(block),
-                           lds > kMergeWords * 4u * (size_t)block ? lds : kMergeWords * 4u * (size_t)block, stream, p,
-                           s, k, sc.merge_k, sc.order_n == grid ? sc.order : nullptr);
-    } else {
-        const uint32_t xcd_group = supertile_rays >= (uint32_t)block ? supertile_rays / (uint32_t)block : 0u;
-        const uint32_t per_block = OCH_DUAL ? 2u * (uint32_t)block : (uint32_t)block;
-        const uint32_t grid = (n + per_block - 1) / per_block;
-        // a plan is a permutation of exactly this grid's workgroups; any other
-        // (stale or for another block size) would index past it
-        OCH_LAUNCH_TIMED(sc, (k_trace_grid<Src, Sink, kPacked, kCount>), dim3(grid), dim3(block),
-                           OCH_DUAL ? 2 * lds : lds, stream, p, s, k, xcd_group, sc.order_n == grid ? sc.order : nullptr,
-                           sc.cost, sc.stamps, sc.stamp_cap);
-    }
+    const size_t lds = stack_bytes(p.depth, block);
+    const uint32_t xcd_group = supertile_rays >= (uint32_t)block ? supertile_rays / (uint32_t)block : 0u;
+    const uint32_t grid = (n + (uint32_t)block - 1) / (uint32_t)block;
+    // a plan is a permutation of exactly this grid's workgroups; any other
+    // (stale or for another block size) would index past it
+    OCH_LAUNCH_TIMED(sc, (k_trace_grid<Src, Sink, kPacked, kCount>), dim3(grid), dim3(block), lds, stream, p, s, k,
+                     xcd_group, sc.order_n == grid ? sc.order : nullptr, sc.cost, sc.stamps, sc.stamp_cap);
     return hipGetLastError();
 }
 
@@ -2073,11 +1186,9 @@ template <class Src, class Sink, bool kCount>
 hipError_t launch(const DevPool &p, const Src &s, const Sink &k, uint32_t n, const Schedule &sc, hipStream_t stream,
                   uint32_t supertile_rays = 0)
 {
-    if (!p.packed) return launch_as<Src, Sink, 0, kCount>(p, s, k, n, sc, stream, supertile_rays);
-    return skip_on(p, kCount) ? launch_as<Src, Sink, kPackedSkip, kCount>(p, s, k, n, sc, stream, supertile_rays)
-                              : launch_as<Src, Sink, 1, kCount>(p, s, k, n, sc, stream, supertile_rays);
+    return p.packed ? launch_as<Src, Sink, 1, kCount>(p, s, k, n, sc, stream, supertile_rays)
+                    : launch_as<Src, Sink, 0, kCount>(p, s, k, n, sc, stream, supertile_rays);
 }
-
 
 template <class Src, class Sink, bool kCount>
 hipError_t launch_bounce(const DevPool &p, const Src &s, const Sink &k, uint32_t n, const Schedule &sc, hipStream_t stream)
@@ -2088,15 +1199,12 @@ hipError_t launch_bounce(const DevPool &p, const Src &s, const Sink &k, uint32_t
     const size_t lds = stack_bytes(p.depth, block) > queue ? stack_bytes(p.depth, block) : queue;
     const dim3 grid((n + block - 1) / block);
     const uint32_t *order = sc.order_n == grid.x ? sc.order : nullptr;   // a plan of exactly this grid
-    if (p.packed && skip_on(p, kCount))
-        OCH_LAUNCH_TIMED(sc, (k_trace_bounce<Src, Sink, kPackedSkip, kCount>), grid, dim3(block), lds, stream, p, s, k,
-                           sc.bounce_compact, order, sc.cost, sc.stamps, sc.stamp_cap);
-    else if (p.packed)
+    if (p.packed)
         OCH_LAUNCH_TIMED(sc, (k_trace_bounce<Src, Sink, 1, kCount>), grid, dim3(block), lds, stream, p, s, k,
-                           sc.bounce_compact, order, sc.cost, sc.stamps, sc.stamp_cap);
+                         sc.bounce_compact, order, sc.cost, sc.stamps, sc.stamp_cap);
     else
         OCH_LAUNCH_TIMED(sc, (k_trace_bounce<Src, Sink, 0, kCount>), grid, dim3(block), lds, stream, p, s, k,
-                           sc.bounce_compact, order, sc.cost, sc.stamps, sc.stamp_cap);
+                         sc.bounce_compact, order, sc.cost, sc.stamps, sc.stamp_cap);
     return hipGetLastError();
 }
 
@@ -2116,10 +1224,6 @@ CameraSource camera_source(const DevFrame &f, const Schedule &sc)
     const uint32_t tiles_y = (uint32_t)(f.slice_rows + kTileH - 1) / kTileH;
     src.supertiles_x = (src.tiles_x + 7) / 8;
     src.per_view = sc.tile_order == 1 ? src.supertiles_x * ((tiles_y + 7) / 8) * 64u * 64u : src.tiles_x * tiles_y * 64u;
-    if (sc.kind == 2) {   // refill chunks never cross a view: pad each view to whole chunks (padding rays are invalid)
-        const uint32_t chunk = 64u * (uint32_t)sc.chunk_tiles;
-        src.per_view = (src.per_view + chunk - 1) / chunk * chunk;
-    }
     src.slice_pixels = (uint32_t)f.slice_rows * (uint32_t)src.width;
     src.by_per_view.init(src.per_view);
     src.by_tiles_x.init(src.tiles_x);
@@ -2136,12 +1240,9 @@ hipError_t occupancy_blocks_per_cu(int kind, int block, int depth, int *blocks)
     const size_t lds = stack_bytes(depth, block);
     switch (kind) {
     case 0:
-        return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, k_trace_grid<CameraSource, FrameSink, true, false>, block, lds);
-    case 1:
-        return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, k_trace_persistent<CameraSource, FrameSink, true, false>,
-                                                            block, lds);
+        return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, k_trace_grid<CameraSource, FrameSink, 1, false>, block, lds);
     case 2:
-        return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, k_trace_grid<ArraySource, HitSink<false>, true, false>,
+        return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, k_trace_grid<ArraySource, HitSink<false>, 1, false>,
                                                             block, lds);
     default:
         return hipErrorInvalidValue;

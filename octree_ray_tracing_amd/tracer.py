@@ -167,14 +167,12 @@ class GpuPool:
         nodes = np.ascontiguousarray(nodes, np.uint32).reshape(-1, 8)
         call("och_gpu_pool_update", self._h, int(first), nodes.shape[0], _np_ptr(nodes), int(root))
 
-    OPTIONS = {"schedule": 0, "block": 1, "waves_per_cu": 2, "refill": 3, "layout": 4, "tile_order": 5,
-               "bounce_compact": 6, "chunk_tiles": 7, "cull": 8, "merge": 9, "timing": 10, "plan": 11,
-               "skip": 12, "columns": 13}
+    # och_option (include/och_gpu.h); ids 0, 2, 3, 7, 9, 12, 13 were retired arms
+    OPTIONS = {"block": 1, "layout": 4, "tile_order": 5, "bounce_compact": 6, "cull": 8, "timing": 10, "plan": 11}
 
     def set_option(self, name: str, value: int):
-        """Launch options (och_gpu_set_option): schedule (0 grid / 1 persistent / 2 grid with lane
-        refill), block, waves_per_cu, refill, layout, tile_order, bounce_compact, chunk_tiles,
-        cull (1 = rays proven to miss the voxels' bounding box skip the walk; exact)."""
+        """Launch options (och_gpu_set_option): block, layout, tile_order, bounce_compact, cull
+        (1 = rays proven to miss the voxels' bounding box skip the walk; exact), timing, plan."""
         call("och_gpu_set_option", self._h, self.OPTIONS[name], int(value))
 
     def get_option(self, name: str) -> int:
@@ -187,7 +185,7 @@ class GpuPool:
         call("och_gpu_set_stamp_buffer", self._h, None if stamps is None else _dev_ptr(stamps), int(capacity_waves))
 
     def occupancy(self, kind: int = 0) -> int:
-        """HIP's workgroups-per-CU answer: 0 render grid, 1 render persistent, 2 trace grid."""
+        """HIP's workgroups-per-CU answer: 0 render grid, 2 trace grid."""
         v = C.c_int()
         call("och_gpu_occupancy", self._h, int(kind), C.byref(v))
         return v.value

@@ -42,14 +42,11 @@ def test_group_one_device_matches_oracle(ort, O, gpu_device, bounce):
         else:
             r = O.trace_batch(ref_pool, O.Rcp(None), ORIGIN, rays, nthreads=16)
             want.append(O.shade_fast(r["dir"], r["voxel"], pal).reshape(H, W))
-    for sched in (0, 2):
-        g.set_option("schedule", sched)
-        for chunk in (8, 5):
-            g.render(cams, row_chunk=chunk, bounce=bounce)
-            got = g.download(0)
-            for v in range(2):
-                assert np.array_equal(got[v], want[v]), (sched, chunk, v)
-    g.set_option("schedule", 0)
+    for chunk in (8, 5):
+        g.render(cams, row_chunk=chunk, bounce=bounce)
+        got = g.download(0)
+        for v in range(2):
+            assert np.array_equal(got[v], want[v]), (chunk, v)
     g.plan(cams, row_chunk=8)                   # planned launch order (tile_order 2)
     g.render(cams, row_chunk=8, bounce=bounce)
     got = g.download(0)

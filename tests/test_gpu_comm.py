@@ -206,25 +206,6 @@ def test_group_render_steps(ort, gpu_device, scene):
     g.close()
 
 
-def test_chunk_costs_with_merge_option(ort, gpu_device, scene):
-    """och_gpu_chunk_costs with OCH_OPT_MERGE on: the costs still come
-    from the plain grid kernel -- every chunk timed, none read from scratch --
-    and equal in shape to the merge-off costs."""
-    tree, pal, _ = scene
-    pool = ort.HOctree(tree.nodes, tree.root, DEPTH, device=0)
-    pool.set_palette(pal)
-    cams = [ort.camera(tuple(ORIGIN), 0.3, p, 1.25, W, H) for p in PITCHES]
-    base = pool.chunk_costs(cams, CHUNK)
-    pool.set_option("block", 256)
-    pool.set_option("merge", 8)
-    merged = pool.chunk_costs(cams, CHUNK)
-    assert merged.shape == base.shape
-    assert np.all(np.isfinite(merged)) and np.all(merged > 0)
-    # the costliest chunks are the terrain rows of the pitch -0.6 view in both
-    assert np.corrcoef(base, merged)[0, 1] > 0.5
-    pool.close()
-
-
 def test_row_deal_rejected_keeps_old_deal(ort, gpu_device, scene):
     """A bad och_gpu_set_row_deal leaves the pool's deal as it was."""
     tree, pal, _ = scene

@@ -66,7 +66,7 @@ def test_bench_instance_d12_1080p(ort, O, gpu_device, d12, d12_ref, pal):
     W, H = 1920, 1080
     pool = ort.HOctree(d12.nodes, d12.root, 12, device=0)
     pool.set_palette(pal)
-    assert pool.get_option("layout") == 1 and pool.get_option("schedule") == 0
+    assert pool.get_option("layout") == 1
     want = oracle_frames(O, d12_ref, pal, W, H)
     cams = [ort.camera(tuple(ORIGIN), YAW, p, FOV, W, H) for p in PITCHES]
     pool.plan_views(cams, 8, 0, 1)          # bench.py's launch order
@@ -191,17 +191,15 @@ def test_config5_d12_frames(ort, O, gpu_device, d12, d12_ref, pal, compact):
     pool.close()
 
 
-def test_d12_trace_records_all_schedules(ort, O, gpu_device, d12, d12_ref):
-    """configs[2] hit records and PUSH counts at depth 12 for both schedules and layouts."""
+def test_d12_trace_records_both_layouts(ort, O, gpu_device, d12, d12_ref):
+    """configs[2] hit records and PUSH counts at depth 12 for both layouts."""
     from test_gpu_parity import assert_same, gpu_trace_dev
     pool = ort.HOctree(d12.nodes, d12.root, 12, device=0)
     rays = O.raygen(YAW, -0.6, FOV, 1920, 1080)
     ref = O.trace_batch(d12_ref, O.Rcp(None), ORIGIN, rays, nthreads=16, want_push=True)
-    for sched in (0, 1, 2):
-        for layout in (1, 0):
-            pool.set_option("schedule", sched)
-            pool.set_option("layout", layout)
-            assert_same(gpu_trace_dev(pool, ORIGIN, rays), ref)
+    for layout in (1, 0):
+        pool.set_option("layout", layout)
+        assert_same(gpu_trace_dev(pool, ORIGIN, rays), ref)
     pool.close()
 
 

@@ -4,7 +4,7 @@ The capacity-sized _table that ORT/och_octree.cpp:14-160 leaves behind --
 free list threaded through children[0], empty nodes from set(..., 0), the
 root-emptied quirk -- uploaded unchanged (index_base 0, root 0, miss t 0,
 ORT/och_octree.cpp:207, :302) and traced through the C ABI, every layout,
-schedule and cull setting, against the oracle on the same table: direction,
+cull setting, against the oracle on the same table: direction,
 voxel, t bits and PUSH count per ray.  The tables come from the oracle's ORef
 restatement (tests/test_octree_table.py pins it)."""
 import numpy as np
@@ -43,16 +43,14 @@ def test_reference_octree_table(ort, O, gpu_device, fill):
     refs = [O.trace_batch(ref_pool, O.Rcp(None), o, d, nthreads=16, want_push=True) for o, d in cases]
     for layout in (0, 1):
         pool.set_option("layout", layout)
-        for sched in (0, 1, 2):
-            pool.set_option("schedule", sched)
-            for cull in (0, 1, 2):
-                pool.set_option("cull", cull)
-                for (o, d), ref in zip(cases, refs):
-                    got = gpu_trace_dev(pool, o, d)
-                    # PUSH counts are the reference's unless the diagnostic cull 2 is on
-                    assert_same(got, ref, push=cull != 2)
-                    hd, hv, ht = pool.trace_batch(o, d)            # no counts: culled when cull > 0
-                    assert_same({"dir": hd, "voxel": hv, "t": ht}, ref, push=False)
+        for cull in (0, 1, 2):
+            pool.set_option("cull", cull)
+            for (o, d), ref in zip(cases, refs):
+                got = gpu_trace_dev(pool, o, d)
+                # PUSH counts are the reference's unless the diagnostic cull 2 is on
+                assert_same(got, ref, push=cull != 2)
+                hd, hv, ht = pool.trace_batch(o, d)            # no counts: culled when cull > 0
+                assert_same({"dir": hd, "voxel": hv, "t": ht}, ref, push=False)
     pool.close()
 
 

@@ -93,11 +93,9 @@ def test_camera_frames_host_rcpps(ort, O, gpu_device, depth):
     for pitch in (0.0, -0.6):
         rays = O.raygen(0.3, pitch, 1.25, 1920, 1080)
         ref = O.trace_batch(ref_pool, O.Rcp(None), ORIGIN, rays, nthreads=16, want_push=True)
-        for sched in (0, 1, 2):
-            for layout in (0, 1):
-                pool.set_option("schedule", sched)
-                pool.set_option("layout", layout)
-                assert_same(gpu_trace_dev(pool, ORIGIN, rays), ref)
+        for layout in (0, 1):
+            pool.set_option("layout", layout)
+            assert_same(gpu_trace_dev(pool, ORIGIN, rays), ref)
     pool.close()
 
 
@@ -153,8 +151,7 @@ def test_deep_sparse_trees(ort, O, gpu_device, depth):
     for layout in (0, 1):
         pool.set_option("layout", layout)
         assert_same(gpu_trace_dev(pool, o, d), ref)
-    # config 5's secondary rays at these depths: the in-place walk restarts on
-    # stacks up to 23 levels deep (OCH_BOUNCE_RESTART)
+    # config 5's secondary rays at these depths, every compaction mode
     refb = O.trace_bounce_batch(ref_pool, O.Rcp(None), o, d, nthreads=16, want_push=True)
     pool.set_option("layout", 1)
     for compact in (0, 1, 2):
@@ -226,30 +223,28 @@ def test_raygen_bit_exact(ort, O, gpu_device, W, H, pitch):
 def test_edge_sizes(ort, O, gpu_device):
     """Batches of 0, 1, 63, 64, 65 and 4097 rays (empty, lone, ragged waves and
     blocks) and frames of 1x1, 7x9, 8x8, 9x7 and 65x3 pixels (partial tiles,
-    single rows), every schedule and both layouts, against the oracle."""
+    single rows), both layouts, against the oracle."""
     tree = ort.build_terrain(8)
     pal = ort.VoxelData().get_colours()
     pool = ort.HOctree(tree.nodes, tree.root, 8, device=0)
     pool.set_palette(pal)
     ref_pool = O.OraclePool(tree.nodes, tree.root, 8, 1)
     rng = np.random.default_rng(17)
-    for sched in (0, 1, 2):
-        for layout in (0, 1):
-            pool.set_option("schedule", sched)
-            pool.set_option("layout", layout)
-            for n in (0, 1, 63, 64, 65, 4097):
-                o = rng.uniform(1.05, 1.95, (n, 3)).astype(np.float32)
-                d = rng.uniform(-1, 1, (n, 3))
-                d = (d / np.maximum(np.linalg.norm(d, axis=1, keepdims=True), 1e-6)).astype(np.float32)
-                hd, hv, ht = pool.trace_batch(o, d)
-                assert hd.shape == (n,)
-                if n:
-                    want = O.trace_batch(ref_pool, O.Rcp(None), o, d)
-                    assert_same({"dir": hd, "voxel": hv, "t": ht}, want, push=False)
-            for W, H in ((1, 1), (7, 9), (8, 8), (9, 7), (65, 3)):
-                cam = ort.camera((1.5, 1.5, 1.5), 0.3, -0.6, 1.25, W, H)
-                r = O.trace_batch(ref_pool, O.Rcp(None), ORIGIN, O.raygen(0.3, -0.6, 1.25, W, H))
-                assert np.array_equal(pool.render(cam), O.shade(r["dir"], r["voxel"], pal).reshape(H, W)), (W, H)
+    for layout in (0, 1):
+        pool.set_option("layout", layout)
+        for n in (0, 1, 63, 64, 65, 4097):
+            o = rng.uniform(1.05, 1.95, (n, 3)).astype(np.float32)
+            d = rng.uniform(-1, 1, (n, 3))
+            d = (d / np.maximum(np.linalg.norm(d, axis=1, keepdims=True), 1e-6)).astype(np.float32)
+            hd, hv, ht = pool.trace_batch(o, d)
+            assert hd.shape == (n,)
+            if n:
+                want = O.trace_batch(ref_pool, O.Rcp(None), o, d)
+                assert_same({"dir": hd, "voxel": hv, "t": ht}, want, push=False)
+        for W, H in ((1, 1), (7, 9), (8, 8), (9, 7), (65, 3)):
+            cam = ort.camera((1.5, 1.5, 1.5), 0.3, -0.6, 1.25, W, H)
+            r = O.trace_batch(ref_pool, O.Rcp(None), ORIGIN, O.raygen(0.3, -0.6, 1.25, W, H))
+            assert np.array_equal(pool.render(cam), O.shade(r["dir"], r["voxel"], pal).reshape(H, W)), (W, H)
     pool.close()
 
 
@@ -291,23 +286,21 @@ def test_multi_view_render_and_unshard(ort, O, gpu_device):
     W, H = 320, 200
     cams = [ort.camera((1.5, 1.5, 1.5), y, p, 1.25, W, H) for y, p in ((0.3, 0.0), (0.3, -0.6), (1.9, -0.2))]
     single = [torch.from_numpy(pool.render(c).view(np.int32)) for c in cams]
-    for sched in (0, 1, 2):
-        pool.set_option("schedule", sched)
-        out = torch.zeros((3, H, W), dtype=torch.int32, device="cuda")
-        pool.render_views_dev(cams, out)
-        torch.cuda.synchronize()
-        for v in range(3):
-            assert torch.equal(out[v].cpu(), single[v])
-        n, chunk = 4, 8
-        rows = ort.shard_rows(H, chunk, n)
-        gathered = torch.zeros((n, 3, rows, W), dtype=torch.int32, device="cuda")
-        for s_ in range(n):
-            pool.render_views_dev(cams, gathered[s_], chunk, s_, n)
-        frames = torch.empty((3, H, W), dtype=torch.int32, device="cuda")
-        pool.unshard_dev(gathered, frames, W, H, chunk, n, 3)
-        torch.cuda.synchronize()
-        for v in range(3):
-            assert torch.equal(frames[v].cpu(), single[v])
+    out = torch.zeros((3, H, W), dtype=torch.int32, device="cuda")
+    pool.render_views_dev(cams, out)
+    torch.cuda.synchronize()
+    for v in range(3):
+        assert torch.equal(out[v].cpu(), single[v])
+    n, chunk = 4, 8
+    rows = ort.shard_rows(H, chunk, n)
+    gathered = torch.zeros((n, 3, rows, W), dtype=torch.int32, device="cuda")
+    for s_ in range(n):
+        pool.render_views_dev(cams, gathered[s_], chunk, s_, n)
+    frames = torch.empty((3, H, W), dtype=torch.int32, device="cuda")
+    pool.unshard_dev(gathered, frames, W, H, chunk, n, 3)
+    torch.cuda.synchronize()
+    for v in range(3):
+        assert torch.equal(frames[v].cpu(), single[v])
     pool.close()
 
 
@@ -506,53 +499,6 @@ def test_indexed_colour_frames(ort, O, gpu_device, bounce, W):
     pool.close()
 
 
-@pytest.mark.parametrize("chunk,refill", [(1, 1), (2, 64), (4, 16), (16, 8), (64, 32)])
-def test_refill_schedule_variants(ort, O, gpu_device, chunk, refill):
-    """Schedule 2 (grid with lane refill) at its extremes: one tile per wave
-    and refill after every finished lane, whole-wave refills, long chunks;
-    camera frames (odd sizes: partial tiles, padded chunks), sharded codes and
-    random rays, all bit-identical to the oracle."""
-    import torch
-    tree = ort.build_terrain(9)
-    pal = ort.VoxelData().get_colours()
-    pool = ort.HOctree(tree.nodes, tree.root, 9, device=0)
-    pool.set_palette(pal)
-    pool.set_stream(torch.cuda.current_stream())
-    pool.set_option("schedule", 2)
-    pool.set_option("chunk_tiles", chunk)
-    pool.set_option("refill", refill)
-    ref_pool = O.OraclePool(tree.nodes, tree.root, 9, 1)
-    rng = np.random.default_rng(chunk * 100 + refill)
-    o = rng.uniform(1.01, 1.99, (30001, 3)).astype(np.float32)
-    d = rng.uniform(-1, 1, (30001, 3)).astype(np.float32)
-    d /= np.linalg.norm(d, axis=1, keepdims=True)
-    assert_same(gpu_trace_dev(pool, o, d), O.trace_batch(ref_pool, O.Rcp(None), o, d, nthreads=16, want_push=True))
-    W, H = 803, 451
-    cams = [ort.camera((1.5, 1.5, 1.5), 0.3, p, 1.25, W, H) for p in (0.0, -0.6)]
-    want = []
-    for p in (0.0, -0.6):
-        r = O.trace_batch(ref_pool, O.Rcp(None), ORIGIN, O.raygen(0.3, p, 1.25, W, H), nthreads=16)
-        want.append(O.shade(r["dir"], r["voxel"], pal).reshape(H, W))
-    for n, rc in ((1, H), (3, 8), (2, 5)):
-        rows = ort.shard_rows(H, rc, n)
-        gathered = torch.full((n, 2, rows, W), 255, dtype=torch.uint8, device="cuda")
-        for s_ in range(n):
-            pool.render_codes_views_dev(cams, gathered[s_], rc, s_, n)
-        full = torch.empty((2, H, W), dtype=torch.int32, device="cuda")
-        pool.shade_unshard_dev(gathered, full, W, H, rc, n, 2)
-        torch.cuda.synchronize()
-        for v in range(2):
-            assert np.array_equal(full[v].cpu().numpy().view(np.uint32), want[v]), (n, rc, v)
-    for order in (0, 1):
-        pool.set_option("tile_order", order)
-        frames = torch.zeros((2, H, W), dtype=torch.int32, device="cuda")
-        pool.render_views_dev(cams, frames)
-        torch.cuda.synchronize()
-        for v in range(2):
-            assert np.array_equal(frames[v].cpu().numpy().view(np.uint32), want[v]), (order, v)
-    pool.close()
-
-
 @pytest.mark.parametrize("order,shape", [(2, 10), (3, 10), (2, 0), (2, 100)])
 def test_planned_launch_order(ort, O, gpu_device, order, shape):
     """OCH_OPT_TILE_ORDER = 2: the costliest tiles of a planning frame go first
@@ -642,4 +588,26 @@ def test_eight_views_per_launch(ort, O, gpu_device):
         pool.render_views_dev(cams + cams[:1], nine)
     with pytest.raises(ort.OchError):
         pool.render_views_dev([cams[0], ort.camera((1.5, 1.5, 1.5), 0.3, 0.0, 1.25, W + 1, H)], frames)
+    pool.close()
+
+
+def test_retired_options_refused(ort, gpu_device):
+    """The option ids of the arms retired in round 5 (persistent / refill
+    schedules, wave merging, the per-node skip, the column cull) fail loudly
+    instead of being stored and ignored; the supported options round-trip."""
+    import ctypes as C
+    from octree_ray_tracing_amd._lib import load
+    tree = ort.build_terrain(5)
+    pool = ort.HOctree(tree.nodes, tree.root, 5, device=0)
+    lib = load()
+    v = C.c_int()
+    for opt in (0, 2, 3, 7, 9, 12, 13):
+        assert lib.och_gpu_set_option(pool._h, opt, 0) != 0
+        assert "retired" in lib.och_last_error().decode()
+        assert lib.och_gpu_get_option(pool._h, opt, C.byref(v)) != 0
+    for name, value in (("block", 128), ("layout", 0), ("tile_order", 1), ("bounce_compact", 2), ("cull", 0),
+                        ("timing", 2), ("plan", 0)):
+        pool.set_option(name, value)
+        assert pool.get_option(name) == value
+    assert set(pool.OPTIONS) == {"block", "layout", "tile_order", "bounce_compact", "cull", "timing", "plan"}
     pool.close()

@@ -2,7 +2,7 @@
 per pixel) over resident rays laid out as a row-major image, one 8x8 tile of
 neighbouring rays per wavefront, optionally in a planned launch order.
 Records and PUSH counts in the caller's order, bit for bit against the oracle
-and against the untiled batch, for every schedule, layout and cull setting,
+and against the untiled batch, for both layouts and every cull setting,
 ragged widths and sizes, shared and per-ray origins."""
 import numpy as np
 import pytest
@@ -36,7 +36,7 @@ def tiled_dev(pool, origins, dirs, width, want_push=True, n=None):
 @pytest.mark.parametrize("depth", [10, 12])
 def test_tiled_camera_rays(ort, O, gpu_device, depth):
     """A 1920x1080 camera frame's rays, both survey pitches, width 1920 (the
-    frame), 1000 and 37 (tiles straddling rows), every schedule and layout."""
+    frame), 1000 and 37 (tiles straddling rows), both layouts."""
     tree = ort.build_terrain(depth, use_gpu=True)
     pool = ort.HOctree(tree.nodes, tree.root, depth, device=0)
     ref_pool = O.OraclePool(tree.nodes, tree.root, depth, 1)
@@ -45,14 +45,10 @@ def test_tiled_camera_rays(ort, O, gpu_device, depth):
         ref = O.trace_batch(ref_pool, O.Rcp(None), ORIGIN, rays, nthreads=16, want_push=True)
         for layout in (1, 0):
             pool.set_option("layout", layout)
-            for sched in (0, 1, 2):
-                pool.set_option("schedule", sched)
-                for width in (1920, 1000, 37):
-                    if depth == 12 and (sched, width) not in ((0, 1920), (0, 37), (1, 1920), (2, 1000)):
-                        continue
-                    assert_same(tiled_dev(pool, ORIGIN, rays, width), ref)
-                    # no PUSH counts: the exact cull runs
-                    assert_same(tiled_dev(pool, ORIGIN, rays, width, want_push=False), ref, push=False)
+            for width in (1920, 1000, 37):
+                assert_same(tiled_dev(pool, ORIGIN, rays, width), ref)
+                # no PUSH counts: the exact cull runs
+                assert_same(tiled_dev(pool, ORIGIN, rays, width, want_push=False), ref, push=False)
     pool.close()
 
 

@@ -92,7 +92,7 @@ def mask_check(body: str):
 
 def test_mask_wait_states():
     """Check 3: a VALU-written lane mask read as a mask needs 2 wait states
-    (the descent's hand-placed child index, OCH_ADDC_IDX, keeps them)."""
+    (the descent's hand-placed child index in ray_push_descend keeps them)."""
     good = """\tv_cmp_ge_f32_e32 vcc, v23, v21
 \ts_nop 1
 \tv_cndmask_b32_e32 v13, v13, v22, vcc

@@ -22,7 +22,7 @@ with the product's flags and checks, in every function that issues the load
      block; a carry-out read as the next carry-in, the 64-bit add chain, is not
      this hazard).  The compiler keeps that distance in
      its own code (its minimum over these kernels is 2); the check holds the
-     hand-placed VALU of the descent's child index (OCH_ADDC_IDX) to it.
+     hand-placed VALU of the descent's child index (ray_push_descend) to it.
 Exit status 0 and a one-line summary when every kernel passes; 1 with the
 offending instruction otherwise.  Run by the csrc Makefile (`make isa-check`),
 __graft_entry__.build() and tests/test_isa_check.py.
