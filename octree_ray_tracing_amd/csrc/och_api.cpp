@@ -1432,9 +1432,16 @@ OCH_API int och_gpu_set_row_deal(och_gpu_pool *p, int height, int row_chunk, int
             return fail(OCH_E_HIP, "row deal tables: %s", hipGetErrorString(e));
         }
     }
-    OCH_HIP(hipDeviceSynchronize());          // frames in flight may still read the old tables
-    if (p->d_chunk_map) OCH_HIP(hipFree(p->d_chunk_map));
-    if (p->d_owner) OCH_HIP(hipFree(p->d_owner));
+    // frames in flight may still read the old tables; on failure the new ones
+    // are freed and the old deal stays
+    const hipError_t se = hipDeviceSynchronize();
+    if (se != hipSuccess) {
+        if (d_map) (void)hipFree(d_map);
+        if (d_own) (void)hipFree(d_own);
+        return fail(OCH_E_HIP, "row deal: hipDeviceSynchronize: %s", hipGetErrorString(se));
+    }
+    if (p->d_chunk_map) (void)hipFree(p->d_chunk_map);
+    if (p->d_owner) (void)hipFree(p->d_owner);
     p->d_chunk_map = d_map;
     p->d_owner = d_own;
     ++p->deal_serial;
@@ -1615,11 +1622,19 @@ OCH_API int och_gpu_render_sharded_steps_dev(och_gpu_pool *p, och_comm *comm, co
     if (device != p->device) return fail(OCH_E_INVALID, "communicator on device %d, pool on device %d", device, p->device);
     const bool receives = exchange != OCH_EXCHANGE_GATHER || rank == 0;
     const bool shades = exchange == OCH_EXCHANGE_ALL_GATHER || rank == 0;
+    // Everything a frame needs is checked before the first is queued: a rank
+    // that stops part way leaves its peers' collectives without a partner.
     for (int b = 0; b < n_buffers; ++b) {
         if (!slices[b]) return fail(OCH_E_INVALID, "slices[%d] is NULL", b);
         if (receives && (!gathered || !gathered[b])) return fail(OCH_E_INVALID, "rank %d needs gathered[%d]", rank, b);
         if (shades && (!frames || !frames[b])) return fail(OCH_E_INVALID, "rank %d needs frames[%d]", rank, b);
     }
+    for (int v = 0; v < n_views; ++v)
+        if (cams[v].width != cams[0].width || cams[v].height != cams[0].height || cams[v].width <= 0 ||
+            cams[v].height <= 0)
+            return fail(OCH_E_INVALID, "views must share one positive width and height");
+    if (shades && !p->d_code_table)
+        return fail(OCH_E_INVALID, "no code table: set a palette of at most %d voxel ids", OCH_CODE_MAX_VOXELS);
     const int W = cams[0].width, H = cams[0].height;
     const size_t count = (size_t)n_views * p->slice_rows(H, row_chunk, n_ranks) * W;
     DeviceGuard g(p->device);
@@ -1629,6 +1644,7 @@ OCH_API int och_gpu_render_sharded_steps_dev(och_gpu_pool *p, och_comm *comm, co
     const bool had_ext = p->use_ext;
     const hipStream_t prev = p->ext_stream;
     int st = OCH_OK;
+    bool issued = false;                     // a collective of this window is queued
     for (int k = 0; k < n_steps && st == OCH_OK; ++k) {
         const int b = k % n_buffers;
         const hipStream_t s = static_cast<hipStream_t>(streams[b]);
@@ -1639,16 +1655,24 @@ OCH_API int och_gpu_render_sharded_steps_dev(och_gpu_pool *p, och_comm *comm, co
             p->next_ev_stop = static_cast<hipEvent_t>(stop_events[k]);
         }
         st = render_views(p, cams, n_views, nullptr, row_chunk, rank, n_ranks, bounce != 0, slices[b]);
-        if (st == OCH_OK)
+        if (st == OCH_OK) {
             st = exchange == OCH_EXCHANGE_GATHER
                      ? och::comm_gather(comm, slices[b], receives ? gathered[b] : nullptr, count, 0, s)
                      : och::comm_all_gather(comm, slices[b], gathered[b], count, s);
+            issued = issued || st == OCH_OK;
+        }
         if (st == OCH_OK && shades)
             st = och_gpu_shade_unshard_views_dev(p, gathered[b], frames[b], W, H, row_chunk, n_ranks, n_views);
     }
     p->next_ev_start = p->next_ev_stop = nullptr;
     p->ext_stream = prev;
     p->use_ext = had_ext;
+    if (st != OCH_OK && (issued || n_ranks > 1)) {
+        // the peers' collectives of this window can no longer all complete
+        const std::string msg = och_last_error();
+        och::comm_abort(comm);
+        return fail(st, "%s (communicator aborted: the window stopped part way)", msg.c_str());
+    }
     return st;
 }
 

@@ -145,6 +145,18 @@ int comm_gather(och_comm *c, const void *send, void *recv, size_t bytes, int roo
     return r == ncclSuccess ? OCH_OK : rccl_fail("ncclSend", r);
 }
 
+// After a failure that follows an issued collective (a rank whose window
+// stopped part way leaves its peers' collectives without a partner): abort
+// the communicator so no stream waits on it forever, and mark it destroyed,
+// so every later call on it fails instead of issuing.
+void comm_abort(och_comm *c)
+{
+    if (!c || !c->comm) return;
+    DevGuard g(c->device);
+    (void)rccl().comm_abort(c->comm);
+    c->comm = nullptr;
+}
+
 }  // namespace och
 
 extern "C" {

@@ -121,6 +121,9 @@ struct och_frame_group {
     int last_set = 0;        // the buffer set of the last frame
     bool rendered = false;
     bool codes = true;       // exchange format of the last render
+    // a device's frame failed after others may have queued their all-gathers:
+    // the communicators were aborted and the group refuses further frames
+    bool broken = false;
 };
 
 namespace {
@@ -265,12 +268,31 @@ int device_frame(och_frame_group *g, int r, int b, const och_camera *cams, int n
                                              H, row_chunk, g->n, n_views);
 }
 
+// Abort every device's communicator (ncclCommAbort): after one device's
+// frame failed, the others' all-gathers of that frame have no partner and
+// would hold their streams forever.
+void abort_comms(och_frame_group *g)
+{
+    const och::Rccl &R = och::rccl();
+    int prev = -1;
+    (void)hipGetDevice(&prev);
+    for (int r = 0; r < (int)g->comms.size(); ++r)
+        if (g->comms[r] && R.ok) {
+            (void)hipSetDevice(g->devices[r]);
+            (void)R.comm_abort(g->comms[r]);
+            g->comms[r] = nullptr;
+        }
+    if (prev >= 0) (void)hipSetDevice(prev);
+    g->broken = true;
+}
+
 int render_steps(och_frame_group *g, const och_camera *cams, int n_views, int n_steps, int n_sets, int row_chunk,
                  int bounce)
 {
     if (!g || !cams || n_views < 1 || n_views > OCH_MAX_VIEWS || row_chunk < 1 || n_steps < 0 || n_sets < 1 ||
         n_sets > kMaxSets)
         return group_fail(OCH_E_INVALID, "bad frame group render arguments");
+    if (g->broken) return group_fail(OCH_E_HIP, "frame group unusable after a failed frame (communicators aborted)");
     const int W = cams[0].width, H = cams[0].height;
     for (int v = 0; v < n_views; ++v)
         if (cams[v].width != W || cams[v].height != H || W <= 0 || H <= 0)
@@ -287,13 +309,24 @@ int render_steps(och_frame_group *g, const och_camera *cams, int n_views, int n_
     if (st != OCH_OK) return st;
     const size_t count = (size_t)n_views * slice_rows * W;
     if (n_steps == 0) return OCH_OK;
+    // the shade of every device needs its code table (checked before any frame is queued)
+    if (codes)
+        for (int r = 0; r < g->n; ++r) {
+            int nv = 0;
+            if (och::pool_palette_size(g->pools[r], &nv) != OCH_OK || nv < 1)
+                return group_fail(OCH_E_INVALID, "device " + std::to_string(g->devices[r]) + " has no palette");
+        }
     st = run_on_devices(g, [&](int r) {
         int s = OCH_OK;
         for (int k = 0; k < n_steps && s == OCH_OK; ++k)
             s = device_frame(g, r, k % n_sets, cams, n_views, row_chunk, bounce, codes, count);
         return s;
     });
-    if (st != OCH_OK) return st;
+    if (st != OCH_OK) {
+        const std::string msg = och_last_error();
+        abort_comms(g);
+        return group_fail(st, msg + " (communicators aborted; destroy the group)");
+    }
     g->width = W;
     g->height = H;
     g->n_views = n_views;
@@ -368,10 +401,12 @@ OCH_API int och_frame_group_destroy(och_frame_group *g)
     const och::Rccl &R = och::rccl();
     for (ncclComm_t c : g->comms)
         if (c && R.ok) (void)R.comm_destroy(c);
-    free_buffers(g);
-    free_streams(g);
+    // the pools first: each may still point at one of the group's streams
+    // (device_frame sets it), which pool destroy synchronises
     for (och_gpu_pool *p : g->pools)
         if (p) och_gpu_pool_destroy(p);
+    free_buffers(g);
+    free_streams(g);
     delete g;
     return OCH_OK;
 }
@@ -413,6 +448,7 @@ OCH_API int och_frame_group_set_option(och_frame_group *g, int option, int value
 OCH_API int och_frame_group_plan(och_frame_group *g, const och_camera *cams, int n_views, int row_chunk)
 {
     if (!g || !cams || row_chunk < 1 || n_views < 1) return group_fail(OCH_E_INVALID, "bad plan arguments");
+    if (g->broken) return group_fail(OCH_E_HIP, "frame group unusable after a failed frame (communicators aborted)");
     if (int st = sync_all(g)) return st;     // frames in flight may read the deal and the plans
     if (g->n > 1) {
         // deal the row chunks by their cost in one timed render of these views

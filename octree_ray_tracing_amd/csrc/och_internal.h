@@ -108,6 +108,9 @@ uint64_t pool_last_writer(const och_gpu_pool *pool);
 int comm_ranks(const och_comm *comm, int *n_ranks, int *rank, int *device);
 int comm_all_gather(och_comm *comm, const void *send, void *recv, size_t bytes, hipStream_t stream);
 int comm_gather(och_comm *comm, const void *send, void *recv, size_t bytes, int root, hipStream_t stream);
+// ncclCommAbort after a failure that followed an issued collective; the
+// communicator then reports itself destroyed.
+void comm_abort(och_comm *comm);
 
 struct DevFrame {
     och_camera cams[OCH_MAX_VIEWS];   // equal width / height

@@ -74,3 +74,25 @@ def test_group_rejects_duplicates(ort, gpu_device):
     import torch
     with pytest.raises(ort.OchError):
         ort.FrameGroup(tree.nodes, tree.root, 4, devices=[torch.cuda.device_count()])
+
+
+@pytest.mark.gpu
+def test_group_checks_before_queueing(ort, O, gpu_device):
+    """A frame the group cannot complete is refused before any device queues
+    its render or all-gather (a palette-less group cannot shade): the group
+    stays usable -- no communicator aborted -- and renders once a palette is
+    set; destroy releases the pools before the streams they point at."""
+    tree = ort.build_terrain(6)
+    g = ort.FrameGroup(tree.nodes, tree.root, 6, devices=[0])
+    cams = [ort.camera(tuple(ORIGIN), 0.3, p, 1.25, 64, 40) for p in PITCHES]
+    with pytest.raises(ort.OchError, match="palette"):
+        g.render(cams)
+    pal = ort.VoxelData().get_colours()
+    g.set_palette(pal)
+    g.render_steps(cams, 3, n_buffers=2)
+    got = g.download(0)
+    ref_pool = O.OraclePool(tree.nodes, tree.root, 6, 1)
+    for v, p in enumerate(PITCHES):
+        r = O.trace_batch(ref_pool, O.Rcp(None), ORIGIN, O.raygen(0.3, p, 1.25, 64, 40))
+        assert np.array_equal(got[v], O.shade(r["dir"], r["voxel"], pal).reshape(40, 64))
+    g.close()
