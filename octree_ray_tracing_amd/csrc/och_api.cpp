@@ -208,6 +208,7 @@ struct och_gpu_pool {
         och::DevPool p;
         const bool pk = opt_layout == 1 && d_packed;
         p.nodes = pk ? d_packed : d_nodes;
+        p.n_slots = 8u * (pk ? packed_nodes : n_nodes);
         p.packed = pk ? 1 : 0;
         p.lut = d_lut;
         p.root = pk ? packed_root : root;

@@ -22,6 +22,7 @@ namespace och {
 //             descent or a hit touches memory.
 struct DevPool {
     const uint32_t *nodes;  // raw or packed, per `packed`
+    uint32_t n_slots;       // 8 x the nodes in `nodes`: the descent's buffer loads are bounds-checked against it
     const uint32_t *lut;    // RCPPS table, 1 << (23 - lut_shift) entries
     uint32_t root;          // raw: root index; packed: root_id | root_mask << 24
     int32_t packed;

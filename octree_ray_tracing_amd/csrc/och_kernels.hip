@@ -108,15 +108,26 @@ __device__ __forceinline__ bool in_mode(Ray &r, uint32_t m)
     return r.mode == m;
 }
 
-// Byte offset of child slot c24 - 24 of the node whose slot word is w, from
-// the node pool's base plus 96: (id * 8 + c24) * 4, id = w's low 24 bits.  One
-// v_mad_u32_u24 and a shift (the compiler turns the mul24 by 8 into a shift
-// and a mask, one VALU more per descent).
-__device__ __forceinline__ uint32_t slot_offset(uint32_t w, uint32_t c24)
+// Word index of child slot c24 - 24 of the node whose slot word is w, from
+// the node pool's base minus 24 words: id * 8 + c24, id = w's low 24 bits --
+// one v_mad_u32_u24 (the compiler turns the mul24 by 8 into a shift and a
+// mask, one VALU more per descent).  The descent's buffer load scales it by
+// the descriptor's 4-byte stride, so no shift to bytes either.
+__device__ __forceinline__ uint32_t slot_index(uint32_t w, uint32_t c24)
 {
     uint32_t t;
     asm("v_mad_u32_u24 %0, %1, 8, %2" : "=v"(t) : "v"(w), "v"(c24));
-    return t << 2;
+    return t;
+}
+
+// The node array as a structured buffer of 4-byte records starting 24 words
+// before it (so slot_index needs no bias), bounds-checked against the array:
+// an index past it reads 0 instead of faulting.  Built from kernel arguments
+// only, so it stays in SGPRs.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t slot_buffer(const DevPool &P)
+{
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t *>(P.nodes - 24), 4, (int)(P.n_slots + 24u),
+                                             0x00020000);
 }
 
 // The raw layout's PUSH (ORT/och_h_octree.h:342-344): the slot must be loaded
@@ -168,10 +179,13 @@ __device__ __forceinline__ bool ray_cull(const Ray &r, const DevPool &P, const f
 // kCull: a ray that ray_cull proves a miss ends here (false: ray_active
 // false, ray_result the miss record, 0 PUSHes).  Launches that count PUSHes
 // cull only at OCH_OPT_CULL = 2 (a diagnostic: how many PUSHes the culled
-// launch walks), so their counts stay the reference's.
+// launch walks), so their counts stay the reference's.  exact = false
+// (wave-uniform) leaves the ray to walk: a camera ray that camera_proven_miss
+// already tested (DevPool::cam_cull) -- the two tests differ only for rays
+// grazing the box within that test's margin, which then walk to the same MISS.
 template <bool kCount, bool kCull>
 __device__ __forceinline__ bool ray_setup(Ray &r, const DevPool &P, const float *o, const float *d, uint32_t *stack,
-                                          uint32_t stride)
+                                          uint32_t stride, bool exact = true)
 {
     r.inv = 24;
     r.idx = 0;
@@ -210,7 +224,7 @@ __device__ __forceinline__ bool ray_setup(Ray &r, const DevPool &P, const float 
     r.mode = kAtPush;
     r.child = 0;
     r.push = 0;
-    if (kCull && (kCount ? P.cull == 2 : P.cull != 0) && ray_cull(r, P, o)) {
+    if (kCull && exact && (kCount ? P.cull == 2 : P.cull != 0) && ray_cull(r, P, o)) {
         r.dim = 1u << 23;                                                   // finished: the MISS
         r.mode = kStepping;
         return false;
@@ -221,9 +235,9 @@ __device__ __forceinline__ bool ray_setup(Ray &r, const DevPool &P, const float 
 // Setup, then the first PUSH at the root.
 template <int kPacked, bool kCount, bool kCull = false, bool kAsm = false>
 __device__ __forceinline__ void ray_init(Ray &r, const DevPool &P, const float *o, const float *d, uint32_t *stack,
-                                         uint32_t stride)
+                                         uint32_t stride, bool exact = true)
 {
-    if (!ray_setup<kCount, kCull>(r, P, o, d, stack, stride)) return;
+    if (!ray_setup<kCount, kCull>(r, P, o, d, stack, stride, exact)) return;
     if (kPacked)
         ray_push_descend<kCount, kAsm>(r, P, stride);
     else
@@ -416,19 +430,20 @@ __device__ __forceinline__ void ray_push_descend(Ray &r, const DevPool &P, uint3
     const bool go = present != 0;           // compared before the barrier: present's register becomes mode's
     asm volatile("" : "+v"(r.mode));
     if (!go) return;
-    // 32-bit byte offset from the uniform base: one scaled add, SGPR base address
-    const uint32_t off = slot_offset(r.cur, c24);
+    // the child's slot: one 24-bit multiply-add gives its index in the
+    // structured buffer (slot_buffer), the descriptor's stride scales it
+    const uint32_t slot = slot_index(r.cur, c24);
     // descent (:357-373); at the leaf level this is the HIT (:346-355): dim
     // drops below the walk's range, the stack write lands in the spare top slot
     *r.sp = r.cur;                          // the parent, before its register takes the child's word
     r.sp += stride;
     if (kAsm)
-        asm volatile("global_load_dword %0, %1, %2 offset:-96 ; och_cur_load"   // P.nodes - 96 B + off
+        asm volatile("buffer_load_dword %0, %1, %2, 0 idxen ; och_cur_load"
                      : "+v"(r.cur)
-                     : "v"(off), "s"(P.nodes)
+                     : "v"(slot), "s"(slot_buffer(P))
                      : "memory");
     else
-        r.cur = *reinterpret_cast<const uint32_t *>(reinterpret_cast<const char *>(P.nodes) - 96 + off);
+        r.cur = (P.nodes - 24)[slot];       // the compiler's own load (OCH_ASM_LOAD=0 builds)
     r.dim >>= 1;
     const float tm = ffrom(r.t_min);
     uint32_t nidx = 0;
@@ -532,6 +547,7 @@ __device__ __forceinline__ void bounce_ray(const float *o, const float *d, const
 
 // Rays from arrays: shared (stride 0) or per-ray (stride 3) origin, AoS float3 dirs.
 struct ArraySource {
+    static constexpr bool kProvenMiss = false;    // no camera_proven_miss before setup
     const float *origin;
     const float *dirs;
     int origin_stride;
@@ -654,6 +670,7 @@ struct FastDiv {
 // i = row * width + col, records in the caller's order.  The tile arithmetic
 // of a wave runs on the scalar unit.
 struct TiledArraySource {
+    static constexpr bool kProvenMiss = false;
     const float *origin;
     const float *dirs;
     int origin_stride;
@@ -690,6 +707,7 @@ struct TiledArraySource {
 // which the grid kernel hands to one XCD as a unit (see xcd_block).  The
 // output token is view * slice_pixels + slice pixel.
 struct CameraSource {
+    static constexpr bool kProvenMiss = true;     // get_wave_culled runs camera_proven_miss when P.cam_cull
     och_camera cam[kMaxViews];
     int32_t n_views, row_chunk, shard, n_shards, slice_rows, width, height, order;
     uint32_t tiles_x, supertiles_x, per_view, slice_pixels;
@@ -943,7 +961,8 @@ __global__ void k_trace_grid(DevPool P, Src S, Sink K, uint32_t xcd_group, const
             K.put(out, Hit{OCH_EXIT, 0u, P.miss_bits, 0u});
         } else {
             Ray r;
-            ray_init<kPacked, kCount, true, kAsmLoad>(r, P, o, d, lds_stack + threadIdx.x, blockDim.x);
+            ray_init<kPacked, kCount, true, kAsmLoad>(r, P, o, d, lds_stack + threadIdx.x, blockDim.x,
+                                                      !(Src::kProvenMiss && P.cam_cull));
             ray_run<kPacked, kCount, kAsmLoad>(r, P, blockDim.x);
             K.put(out, ray_result<kPacked, kAsmLoad>(r, P));
         }
@@ -997,7 +1016,7 @@ __global__ void k_trace_bounce(DevPool P, Src S, Sink K, int compact, const uint
             K.put_primary(out, Hit{OCH_EXIT, 0u, P.miss_bits, 0u}, false);
         } else {
             Ray r;
-            ray_init<kPacked, kCount, true, kAsmLoad>(r, P, o, d, stack, nb);
+            ray_init<kPacked, kCount, true, kAsmLoad>(r, P, o, d, stack, nb, !(Src::kProvenMiss && P.cam_cull));
             ray_run<kPacked, kCount, kAsmLoad>(r, P, nb);
             const Hit h1 = ray_result<kPacked, kAsmLoad>(r, P);
             want = h1.dir < OCH_EXIT;
