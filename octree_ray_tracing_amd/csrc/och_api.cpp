@@ -126,6 +126,7 @@ struct och_gpu_pool {
     float miss_t = INFINITY;
     uint32_t *d_lut = nullptr;
     int lut_log2 = 0;
+    uint32_t rcp_xlo = 0, rcp_xspan = 0;   // DevPool::rcp_xlo / rcp_xspan of the uploaded table
     double lut_error = INFINITY;    // maximum relative error of the table (lut_max_rel_error)
     uint32_t *d_palette = nullptr;
     uint32_t n_voxels = 0;
@@ -211,6 +212,8 @@ struct och_gpu_pool {
         p.n_slots = 8u * (pk ? packed_nodes : n_nodes);
         p.packed = pk ? 1 : 0;
         p.lut = d_lut;
+        p.rcp_xlo = rcp_xlo;
+        p.rcp_xspan = rcp_xspan;
         p.root = pk ? packed_root : root;
         p.depth = depth;
         p.lut_shift = 23 - lut_log2;
@@ -464,8 +467,28 @@ int upload_lut(och_gpu_pool *p, const uint32_t *lut, int log2_entries)
     if (p->d_lut) OCH_HIP(hipFree(p->d_lut));
     p->d_lut = nullptr;
     const size_t bytes = sizeof(uint32_t) << log2_entries;
+    // The device table holds every entry + (127 << 23): the kernels' RCPPS of
+    // x = -|d| is then entry - (x's exponent bits) wherever the model's result
+    // exponent ent_e + 127 - e stays in 1..254 and the entry is negative -- for
+    // e in [max(1, max_e - 127), min_e + 126] over this table's entries (och_kernels.hip
+    // rcpps); other x, and every x of a table with a non-negative entry, take
+    // the model itself.
+    const uint32_t n = 1u << log2_entries;
+    std::vector<uint32_t> adj(n);
+    int min_e = 255, max_e = 0;
+    bool negative = true;
+    for (uint32_t k = 0; k < n; ++k) {
+        const int e = (int)((lut[k] >> 23) & 0xFFu);
+        min_e = std::min(min_e, e);
+        max_e = std::max(max_e, e);
+        negative = negative && (lut[k] >> 31) != 0;
+        adj[k] = lut[k] + (127u << 23);
+    }
+    const int e_lo = std::max(1, max_e - 127), e_hi = std::min(254, min_e + 126);
+    p->rcp_xlo = (uint32_t)e_lo << 23;
+    p->rcp_xspan = negative && e_hi >= e_lo ? (uint32_t)(e_hi - e_lo + 1) << 23 : 0u;
     OCH_HIP(hipMalloc(&p->d_lut, bytes));
-    OCH_HIP(hipMemcpy(p->d_lut, lut, bytes, hipMemcpyHostToDevice));
+    OCH_HIP(hipMemcpy(p->d_lut, adj.data(), bytes, hipMemcpyHostToDevice));
     p->lut_log2 = log2_entries;
     // camera_proven_miss budgets the table's error; a coarser table leaves
     // every camera ray to the exact ray_cull

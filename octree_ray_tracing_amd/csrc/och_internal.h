@@ -23,7 +23,9 @@ namespace och {
 struct DevPool {
     const uint32_t *nodes;  // raw or packed, per `packed`
     uint32_t n_slots;       // 8 x the nodes in `nodes`: the descent's buffer loads are bounds-checked against it
-    const uint32_t *lut;    // RCPPS table, 1 << (23 - lut_shift) entries
+    const uint32_t *lut;    // RCPPS table, 1 << (23 - lut_shift) entries, each + (127 << 23) (upload_lut)
+    uint32_t rcp_xlo;       // exponent bits of the smallest x the one-subtraction RCPPS serves (rcpps)
+    uint32_t rcp_xspan;     // and the span of that range (0: the model for every x)
     uint32_t root;          // raw: root index; packed: root_id | root_mask << 24
     int32_t packed;
     int32_t depth;

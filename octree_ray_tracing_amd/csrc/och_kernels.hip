@@ -56,13 +56,27 @@ __device__ __forceinline__ float ffrom(uint32_t u) { return __uint_as_float(u); 
 // for exponent-127 inputs; other exponents move the result exponent.
 // ent = lut[(x & 0x7FFFFF) >> shift], read by the caller for every input (the
 // index is in range for any x), so a ray's three lookups are in flight together.
-__device__ __forceinline__ uint32_t rcpps(uint32_t x, uint32_t ent)
+__device__ __forceinline__ uint32_t rcpps_model(uint32_t x, uint32_t ent)
 {
     const uint32_t sign = x & 0x80000000u, e = (x >> 23) & 0xFFu;
     const int ne = (int)((ent >> 23) & 0xFFu) + 127 - (int)e;
     uint32_t r = ne <= 0 ? sign : (sign | ((uint32_t)ne << 23) | (ent & 0x7FFFFFu));
     r = e == 0 ? (sign | 0x7F800000u) : r;                              // +-0, denormal -> inf
     r = e == 0xFFu ? ((x & 0x7FFFFFu) ? (x | 0x400000u) : sign) : r;    // NaN (quietened), inf -> 0
+    return r;
+}
+
+// The same for x = -|d| (sign set) from the device table, whose entries carry
+// + 127 << 23 (och_api.cpp upload_lut): while the result exponent ent_e + 127 - e
+// stays in 1..254 -- every x whose exponent bits lie in [xlo, xlo + xspan), a
+// range the host derives from the table (DevPool::rcp_xlo / rcp_xspan) -- the
+// model is one subtraction of x's exponent bits from the entry.  Other x
+// (zero, denormal, huge, inf, NaN; none of the bench's rays) take the model.
+__device__ __forceinline__ uint32_t rcpps(uint32_t x, uint32_t adj, uint32_t xlo, uint32_t xspan)
+{
+    const uint32_t xe = x & 0x7F800000u;
+    uint32_t r = adj - xe;
+    if (xe - xlo >= xspan) r = rcpps_model(x, adj - (127u << 23));
     return r;
 }
 
@@ -199,7 +213,7 @@ __device__ __forceinline__ bool ray_setup(Ray &r, const DevPool &P, const float 
         const bool positive = (int32_t)db > 0 && db <= 0x7F800000u;          // 0 < d, :310
         r.inv |= (uint32_t)positive << a;
         const float refl = fabsf(__fsub_rn(positive ? 3.0F : 0.0F, o[a]));   // :314
-        const uint32_t cb = rcpps(db | 0x80000000u, ent[a]);                 // :312, :316
+        const uint32_t cb = rcpps(db | 0x80000000u, ent[a], P.rcp_xlo, P.rcp_xspan);   // :312, :316
         r.c[a] = ffrom(cb);
         r.b[a] = ffrom(fbits(__fmul_rn(r.c[a], refl)) ^ 0x80000000u);       // :318
         // A zero or denormal d gives c = -inf, b = +inf and t = fma(p, -inf,

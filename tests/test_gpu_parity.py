@@ -611,3 +611,36 @@ def test_retired_options_refused(ort, gpu_device):
         assert pool.get_option(name) == value
     assert set(pool.OPTIONS) == {"block", "layout", "tile_order", "bounce_compact", "cull", "timing", "plan"}
     pool.close()
+
+
+def test_rcpps_every_exponent(ort, O, gpu_device):
+    """The kernels' RCPPS takes one subtraction from the device table (entries
+    + 127 << 23) where the model's result exponent stays in range, and the
+    model itself elsewhere.  Directions with one component at every exponent
+    (zero, denormals, 2^-126 .. 2^127, inf, NaN) walk the same records as the
+    oracle, under this host's table, the Intel table, and a table with one
+    non-negative entry (every x through the model)."""
+    tree = ort.build_terrain(7)
+    pool = ort.HOctree(tree.nodes, tree.root, 7, device=0)
+    ref_pool = O.OraclePool(tree.nodes, tree.root, 7, 1)
+    rng = np.random.default_rng(31)
+    base = rng.uniform(-1, 1, (256 * 24, 3)).astype(np.float32)
+    base /= np.linalg.norm(base, axis=1, keepdims=True)
+    exps = np.repeat(np.arange(256, dtype=np.uint32), 24)
+    mant = rng.integers(0, 1 << 23, exps.size, dtype=np.uint32)
+    mant[::6] = 0                                                       # powers of two, inf
+    bits = (exps << 23) | mant | (rng.integers(0, 2, exps.size, dtype=np.uint32) << 31)
+    axis = rng.integers(0, 3, exps.size)
+    base[np.arange(exps.size), axis] = bits.view(np.float32)
+    o = rng.uniform(1.01, 1.99, (exps.size, 3)).astype(np.float32)
+    intel = np.fromfile(GOLD / "rcp_lut_intel.bin", dtype=np.uint32)
+    odd = intel.copy()
+    odd[5] &= 0x7FFFFFFF
+    for lut in (None, intel, odd):
+        if lut is not None:
+            pool.set_rcp_lut(lut)
+        ref = O.trace_batch(ref_pool, O.Rcp(lut), o, base, nthreads=16, want_push=True)
+        for layout in (1, 0):
+            pool.set_option("layout", layout)
+            assert_same(gpu_trace_dev(pool, o, base), ref)
+    pool.close()
