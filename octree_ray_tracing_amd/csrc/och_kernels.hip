@@ -626,29 +626,68 @@ __device__ __forceinline__ void camera_rot(const och_camera &C, int col, int row
 // ray_cull: origin inside (1, 2)^3, no component below 2^-60 of the largest
 // (so every c_a is a normal float below 2^61).  Rays that fail the test take
 // the full setup and ray_cull decides them exactly.
-__device__ __forceinline__ bool camera_proven_miss(const och_camera &C, float ru, float rv, float rw, const DevPool &P)
+// The camera's terms of the test are the view's, computed once per launch on
+// the host in the same float operations (CameraView, camera_source): the
+// grown box's planes relative to the camera, and whether the camera lies
+// inside the root.
+struct CameraView {
+    float lo[3], hi[3];   // (cull_lo - 2^-16) - pos, (cull_hi + 2^-16) - pos
+    int32_t pos_ok;       // 1 < pos < 2 on every axis
+};
+
+__device__ __forceinline__ bool camera_proven_miss(const CameraView &V, float ru, float rv, float rw)
 {
     const float D[3] = {rw, ru, -rv};
     const float dmax = fmaxf(fmaxf(fabsf(D[0]), fabsf(D[1])), fabsf(D[2]));
-    bool ok = dmax > 0x1p-100F;
+    bool ok = V.pos_ok != 0 && dmax > 0x1p-100F;
     float tn = -INFINITY, tf = INFINITY;
 #pragma unroll
     for (int a = 0; a < 3; ++a) {
-        const float o = C.pos[a];
-        ok &= o > 1.0F && o < 2.0F && fabsf(D[a]) >= dmax * 0x1p-60F;
+        ok &= fabsf(D[a]) >= dmax * 0x1p-60F;
         const float inv = __builtin_amdgcn_rcpf(D[a]);
-        const float t1 = (P.cull_lo[a] - 0x1p-16F - o) * inv, t2 = (P.cull_hi[a] + 0x1p-16F - o) * inv;
+        const float t1 = V.lo[a] * inv, t2 = V.hi[a] * inv;
         tn = fmaxf(tn, fminf(t1, t2));
         tf = fminf(tf, fmaxf(t1, t2));
     }
     return ok && (tf < 0.0F || tn > tf * (1.0F + 0x1p-7F));
 }
 
+// Correctly rounded sqrt(x) for x in [2^-96, 2^96): v_sqrt_f32 (1 ulp) and
+// the residual test of its two neighbours -- __builtin_sqrtf's expansion
+// without the scaling of small inputs and the zero / inf class test.
+__device__ __forceinline__ float sqrt_rn_mid(float x)
+{
+    const float s = __builtin_amdgcn_sqrtf(x);
+    const float sm = ffrom(fbits(s) - 1u), sp = ffrom(fbits(s) + 1u);
+    const float rm = __builtin_fmaf(-sm, s, x), rp = __builtin_fmaf(-sp, s, x);
+    float y = rm <= 0.0F ? sm : s;
+    y = rp > 0.0F ? sp : y;
+    return y;
+}
+
+// Correctly rounded 1 / s for s in [2^-60, 2^60): v_rcp_f32 and one Newton
+// step, r + r (1 - s r) with one fma each -- in place of the divide's scale,
+// four fmas and fixup.  Both verified bit for bit against __builtin_sqrtf /
+// __fdiv_rn over every float of those ranges on gfx950
+// (tools/probes/rcp_probe.hip, profiles/r05/r05f/rcp_probe.txt).
+__device__ __forceinline__ float rcp_rn_mid(float s)
+{
+    const float r = __builtin_amdgcn_rcpf(s);
+    return __builtin_fmaf(__builtin_fmaf(-s, r, 1.0F), r, r);
+}
+
 __device__ __forceinline__ void camera_ray_from(float ru, float rv, float rw, float *d)
 {
     const float mag2 = __fadd_rn(__fadd_rn(__fmul_rn(ru, ru), __fmul_rn(rv, rv)), __fmul_rn(rw, rw));
-    // __builtin_sqrtf lowers to the correctly rounded expansion; __fsqrt_rn is a bare v_sqrt_f32 (1 ulp).
-    const float rmag = __fdiv_rn(1.0F, __builtin_sqrtf(mag2));
+    // RN(1 / RN(sqrt(mag2))): the short forms wherever they are verified exact
+    // (every camera ray of a non-degenerate camera: |(u, v, fov factor)|^2), the
+    // general expansions elsewhere.  __builtin_sqrtf lowers to the correctly
+    // rounded expansion; __fsqrt_rn is a bare v_sqrt_f32 (1 ulp).
+    float rmag;
+    if (mag2 >= 0x1p-96F && mag2 < 0x1p96F)
+        rmag = rcp_rn_mid(sqrt_rn_mid(mag2));
+    else
+        rmag = __fdiv_rn(1.0F, __builtin_sqrtf(mag2));
     d[0] = __fmul_rn(rw, rmag);
     d[1] = __fmul_rn(ru, rmag);
     d[2] = __fmul_rn(-rv, rmag);
@@ -731,6 +770,7 @@ struct TiledArraySource {
 struct CameraSource {
     static constexpr bool kProvenMiss = true;     // get_wave_culled runs camera_proven_miss when P.cam_cull
     och_camera cam[kMaxViews];
+    CameraView view[kMaxViews];
     int32_t n_views, row_chunk, shard, n_shards, slice_rows, width, height, order;
     uint32_t tiles_x, supertiles_x, per_view, slice_pixels;
     FastDiv by_per_view, by_tiles_x, by_supertiles_x, by_row_chunk;
@@ -774,7 +814,7 @@ struct CameraSource {
         out = view * slice_pixels + (uint32_t)srow * (uint32_t)width + (uint32_t)col;
         float ru, rv, rw;
         camera_rot(C, col, row, ru, rv, rw);
-        if (cull && P.cam_cull && camera_proven_miss(C, ru, rv, rw, P)) {
+        if (cull && P.cam_cull && camera_proven_miss(this->view[view], ru, rv, rw)) {
             miss = true;
             return true;
         }
@@ -1249,10 +1289,22 @@ hipError_t launch_bounce(const DevPool &p, const Src &s, const Sink &k, uint32_t
     return hipGetLastError();
 }
 
-CameraSource camera_source(const DevFrame &f, const Schedule &sc)
+CameraSource camera_source(const DevPool &p, const DevFrame &f, const Schedule &sc)
 {
     CameraSource src;
-    for (int v = 0; v < f.n_views; ++v) src.cam[v] = f.cams[v];
+    for (int v = 0; v < f.n_views; ++v) {
+        src.cam[v] = f.cams[v];
+        CameraView &V = src.view[v];
+        V.pos_ok = 1;
+        for (int a = 0; a < 3; ++a) {
+            const float o = f.cams[v].pos[a];
+            // the device's operations in IEEE single, one rounding each (no contraction)
+            const float lo = p.cull_lo[a] - 0x1p-16F, hi = p.cull_hi[a] + 0x1p-16F;
+            V.lo[a] = lo - o;
+            V.hi[a] = hi - o;
+            V.pos_ok &= (o > 1.0F && o < 2.0F) ? 1 : 0;
+        }
+    }
     src.n_views = f.n_views;
     src.row_chunk = f.row_chunk;
     src.shard = f.shard;
@@ -1333,7 +1385,7 @@ hipError_t launch_raygen(const och_camera &cam, float *dirs, hipStream_t stream)
 hipError_t launch_render(const DevPool &p, const DevFrame &f, const Schedule &sc, hipStream_t stream)
 {
     if (f.n_views < 1 || f.n_views > kMaxViews) return hipErrorInvalidValue;
-    const CameraSource src = camera_source(f, sc);
+    const CameraSource src = camera_source(p, f, sc);
     return launch<CameraSource, FrameSink, false>(p, src, FrameSink{f.out, f.palette, f.n_voxels}, src.count(), sc,
                                                   stream, sc.tile_order == 1 ? 64u * 64u : 0u);
 }
@@ -1341,7 +1393,7 @@ hipError_t launch_render(const DevPool &p, const DevFrame &f, const Schedule &sc
 hipError_t launch_render_bounce(const DevPool &p, const DevFrame &f, const Schedule &sc, hipStream_t stream)
 {
     if (f.n_views < 1 || f.n_views > kMaxViews) return hipErrorInvalidValue;
-    const CameraSource src = camera_source(f, sc);
+    const CameraSource src = camera_source(p, f, sc);
     return launch_bounce<CameraSource, BounceFrameSink, false>(
         p, src, BounceFrameSink{FrameSink{f.out, f.palette, f.n_voxels}}, src.count(), sc, stream);
 }
@@ -1349,7 +1401,7 @@ hipError_t launch_render_bounce(const DevPool &p, const DevFrame &f, const Sched
 hipError_t launch_render_codes(const DevPool &p, const DevFrame &f, const Schedule &sc, bool bounce, hipStream_t stream)
 {
     if (f.n_views < 1 || f.n_views > kMaxViews) return hipErrorInvalidValue;
-    const CameraSource src = camera_source(f, sc);
+    const CameraSource src = camera_source(p, f, sc);
     const CodeSink k{f.codes, f.n_voxels};
     if (bounce) return launch_bounce<CameraSource, BounceCodeSink, false>(p, src, BounceCodeSink{k}, src.count(), sc, stream);
     return launch<CameraSource, CodeSink, false>(p, src, k, src.count(), sc, stream,
