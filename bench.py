@@ -1237,6 +1237,10 @@ def main():
     frames_host = sfs[last].frames.cpu().numpy() if rank == 0 else None
     pool.set_stream(stream)
     kms = np.array([x.elapsed_time(y) for x, y in ev])
+    # the window's GPU span: the first launch's start to the last launch's end
+    # (dispatch-recorded events); the rest of the host window is issue latency
+    # before the first kernel and completion detection after the last
+    gpu_span_ms = max(ev[0][0].elapsed_time(y) for _, y in ev) if ev else None
     frames = a.steps * len(cams)
     total_rays = W * H * frames
     value = total_rays / elapsed / 1e6
@@ -1450,6 +1454,8 @@ def main():
     roof = {"kernel": f"k_trace_grid<CameraSource,{'FrameSink' if rgba_launch else 'CodeSink'}> (2 views per launch)",
             "kernel_ms": round(k_avg_ms, 4), "kernel_ms_serial": round(latency_ms, 4),
             "host_issue_ms": host_issue_ms,
+            "window_gpu_span_ms": None if gpu_span_ms is None else round(gpu_span_ms, 4),
+            "window_overhead_ms": None if gpu_span_ms is None else round(elapsed * 1e3 - gpu_span_ms, 4),
             "host_issue_ms_per_step": round(host_issue_ms / max(a.steps, 1), 5),
             "ms_per_step": round(step_s * 1e3, 4), "frames_in_flight": len(streams),
             "push_per_ray": round(push_total / rays_rank, 3), "rays_per_launch": rays_rank,
