@@ -96,13 +96,14 @@ struct Ray {
     uint32_t idx;         // child index bits at the current level
     uint32_t dim;         // mantissa bit of the current child size: level L <-> 1 << (23 - L)
     uint32_t cur;         // the current node: packed slot word (id | child mask << 24), or raw index
-    uint32_t *sp;         // this lane's LDS stack slot for the current level (parents below it)
-    uint32_t *sp23;       // sp at dim = 1 (slot 23): sp = sp23 - ctz(dim) * stride (the POP chain)
+    uint32_t sp;          // LDS byte address of this lane's stack slot for the current level (parents below it)
+    uint32_t sp23;        // sp at dim = 1 (slot 23): sp = sp23 - ctz(dim) * 4 * stride (the POP chain)
     uint32_t t_min;       // bits of the entry t of the current cell
     uint32_t min_axis;    // 1, 2, 4 (last STEP axis) or 8 (none yet)
     uint32_t child;       // raw layout: slot word loaded by the last PUSH (pending); the voxel id after a hit
     uint32_t mode;        // see below
     uint32_t push;
+    bool root_idx_ok;     // setup's idx (:324) is the position bits at the root level (stack_idx)
 };
 
 // Ray phase.  Packed layout (one merged PUSH + descend phase): kStepping (0)
@@ -120,6 +121,28 @@ __device__ __forceinline__ bool in_mode(Ray &r, uint32_t m)
 {
     asm volatile("" : "+v"(r.mode));
     return r.mode == m;
+}
+
+// The parent stacks (stack_column): per lane, depth + 1 word slots `stride`
+// words apart in the block's LDS, and beside each word slot, at its byte
+// address / 4, one byte holding the child index the walk took at that level.
+// A descent writes both; a POP reads both, so it needs no rebuild of idx from
+// the position bits (three bit extracts and two shift-ors per POP).
+typedef __attribute__((address_space(3))) uint32_t lds_word;
+typedef __attribute__((address_space(3))) uint8_t lds_byte;
+__device__ __forceinline__ lds_word *stack_word(uint32_t a) { return (lds_word *)(uintptr_t)a; }
+__device__ __forceinline__ lds_byte *stack_idx(uint32_t a) { return (lds_byte *)(uintptr_t)(a >> 2); }
+
+// This lane's stack column (the LDS byte address of its slot 0).  The word
+// plane starts at wb with wb / 4 >= the dynamic area's start (the idx plane
+// stays clear of static LDS) and wb / 4 + e <= wb (it stays below the word
+// plane): e = (depth + 1) * blockDim slots.  stack_lds_bytes sizes the area.
+__device__ __forceinline__ uint32_t stack_column(const uint32_t *lds, uint32_t depth)
+{
+    const uint32_t base = (uint32_t)(uintptr_t)(const lds_word *)lds;
+    const uint32_t e = (depth + 1u) * blockDim.x;
+    const uint32_t wb = 4u * max(base, (e + 2u) / 3u);
+    return wb + 4u * threadIdx.x;
 }
 
 // Word index of child slot c24 - 24 of the node whose slot word is w, from
@@ -155,7 +178,7 @@ __device__ __forceinline__ void ray_push_raw(Ray &r, const DevPool &P)
     r.child = (P.nodes - 24)[8u * r.cur + c24];
 }
 
-template <bool kCount, bool kAsm>
+template <bool kCount, bool kAsm, bool kIdxPlane>
 __device__ __forceinline__ void ray_push_descend(Ray &r, const DevPool &P, uint32_t stride);
 
 // Occupied-box cull (OCH_OPT_CULL; DESIGN.md §4b has the proof).  With
@@ -189,7 +212,7 @@ __device__ __forceinline__ bool ray_cull(const Ray &r, const DevPool &P, const f
 }
 
 // Setup, ORT/och_h_octree.h:294-338, up to, not including, the root PUSH.
-// stack: this lane's LDS column, depth + 1 slots `stride` words apart.
+// stack: this lane's LDS column (stack_column), depth + 1 slots `stride` words apart.
 // kCull: a ray that ray_cull proves a miss ends here (false: ray_active
 // false, ray_result the miss record, 0 PUSHes).  Launches that count PUSHes
 // cull only at OCH_OPT_CULL = 2 (a diagnostic: how many PUSHes the culled
@@ -198,11 +221,12 @@ __device__ __forceinline__ bool ray_cull(const Ray &r, const DevPool &P, const f
 // already tested (DevPool::cam_cull) -- the two tests differ only for rays
 // grazing the box within that test's margin, which then walk to the same MISS.
 template <bool kCount, bool kCull>
-__device__ __forceinline__ bool ray_setup(Ray &r, const DevPool &P, const float *o, const float *d, uint32_t *stack,
+__device__ __forceinline__ bool ray_setup(Ray &r, const DevPool &P, const float *o, const float *d, uint32_t stack,
                                           uint32_t stride, bool exact = true)
 {
     r.inv = 24;
     r.idx = 0;
+    uint32_t root_bits = 0;
     uint32_t ent[3];
 #pragma unroll
     for (int a = 0; a < 3; ++a) ent[a] = P.lut[(fbits(d[a]) & 0x7FFFFFu) >> P.lut_shift];
@@ -228,11 +252,18 @@ __device__ __forceinline__ bool ray_setup(Ray &r, const DevPool &P, const float 
         }
         r.p[a] = fbits(refl) & 0x3FC00000u;                                 // :320
         r.idx |= (uint32_t)(r.p[a] == 0x3FC00000u) << a;                    // :324
+        root_bits |= ((r.p[a] >> 22) & 1u) << a;
     }
+    // A POP rebuilds idx from the position bits (:440-444).  Below the root
+    // those are the bits the descent took, which the stack's idx plane holds;
+    // at the root they are bit 22, which setup's idx matches unless the origin
+    // lies outside the root (p is then not 1.x).  A wave holding such a ray
+    // walks with the rebuild (ray_trace).
+    r.root_idx_ok = __ballot(r.idx != root_bits) == 0;
     r.dim = 1u << 22;                                                       // :326
     r.cur = P.root;
-    r.sp = stack + stride;                                                  // slot 0: the miss POP's dummy read
-    r.sp23 = stack + 23u * stride;                                          // slot 23 - ctz(dim)
+    r.sp = stack + 4u * stride;                                             // slot 0: the miss POP's dummy read
+    r.sp23 = stack + 92u * stride;                                          // slot 23 - ctz(dim)
     r.t_min = 0;                                                            // +0.0F
     r.min_axis = 8;
     r.mode = kAtPush;
@@ -246,17 +277,6 @@ __device__ __forceinline__ bool ray_setup(Ray &r, const DevPool &P, const float 
     return true;
 }
 
-// Setup, then the first PUSH at the root.
-template <int kPacked, bool kCount, bool kCull = false, bool kAsm = false>
-__device__ __forceinline__ void ray_init(Ray &r, const DevPool &P, const float *o, const float *d, uint32_t *stack,
-                                         uint32_t stride, bool exact = true)
-{
-    if (!ray_setup<kCount, kCull>(r, P, o, d, stack, stride, exact)) return;
-    if (kPacked)
-        ray_push_descend<kCount, kAsm>(r, P, stride);
-    else
-        ray_push_raw<kCount>(r, P);
-}
 
 // The PUSH / STEP / POP machine (ORT/och_h_octree.h:342-446,
 // ORT/och_octree.cpp:217-319) in phases per iteration, software-pipelined so
@@ -268,7 +288,9 @@ __device__ __forceinline__ void ray_init(Ray &r, const DevPool &P, const float *
 // The raw layout must load every PUSH's slot to test it, so it resolves the
 // slot first (descend, step, push): an empty child then STEPs in the same
 // iteration.  stride: words between two levels of one lane's LDS stack.
-template <int kPacked>
+// kIdxPlane: a POP reads idx from the stack's idx plane (every ray of the
+// wave has root_idx_ok), else rebuilds it from the position bits.
+template <int kPacked, bool kIdxPlane>
 __device__ __forceinline__ void ray_phase_step(Ray &r, uint32_t stride)
 {
     // STEP :378-419.  The reference's cascade (x if tx <= ty && tx <= tz,
@@ -316,18 +338,23 @@ __device__ __forceinline__ void ray_phase_step(Ray &r, uint32_t stride)
             uint32_t k = __builtin_ctz(up);                                 // the new level's bit
             asm volatile("" : "+v"(k));        // 1 << k, not re-folded into up & -up (one VALU more)
             const uint32_t nd = 1u << k;                                    // new child-size bit
-            // one 24-bit multiply-add: k < 32, stride <= 1024 words
-            r.sp = reinterpret_cast<uint32_t *>(reinterpret_cast<char *>(r.sp23) - __mul24((int)k, 4 * (int)stride));
-            r.cur = *r.sp;                                                  // :434 (slot 0 after the MISS)
+            // sp23 - k * 4 stride in one 24-bit multiply-add (k < 32, stride <= 1024 words);
+            // written out, as the compiler re-derives sp23 from the setup and
+            // takes a 64-bit multiply-add
+            asm("v_mad_i32_i24 %0, %1, %2, %3" : "=v"(r.sp) : "v"(k), "s"(-4 * (int)stride), "v"(r.sp23));
+            r.cur = *stack_word(r.sp);                                      // :434 (slot 0 after the MISS)
+            if (kIdxPlane) r.idx = *stack_idx(r.sp);                        // :440-444, as the descent left it
             const uint32_t keep = 0u - nd;                                  // clears the levels popped, :436
             r.p[0] &= keep;
             r.p[1] &= keep;
             r.p[2] &= keep;
             r.dim = nd;
             const bool past = nd > (1u << 22);                              // past the root: the MISS
-            uint32_t zy = (__builtin_amdgcn_ubfe(r.p[2], k, 1) << 1) | __builtin_amdgcn_ubfe(r.p[1], k, 1);
-            asm volatile("" : "+v"(zy));
-            r.idx = (zy << 1) | __builtin_amdgcn_ubfe(r.p[0], k, 1);        // :440-444
+            if (!kIdxPlane) {
+                uint32_t zy = (__builtin_amdgcn_ubfe(r.p[2], k, 1) << 1) | __builtin_amdgcn_ubfe(r.p[1], k, 1);
+                asm volatile("" : "+v"(zy));
+                r.idx = (zy << 1) | __builtin_amdgcn_ubfe(r.p[0], k, 1);    // :440-444
+            }
             r.mode = chain && !past ? axis : 0u;                            // the advance at that level
         }
         if (r.mode) {                                                       // advance :413-419
@@ -351,8 +378,8 @@ __device__ __forceinline__ void ray_phase_step(Ray &r, uint32_t stride)
     // POP :421-446.  At the root this is the MISS (:423-431): dim leaves the
     // walk's range, and the rest of the POP runs on dead state (its stack read
     // lands in the column's spare slot 0) rather than behind a branch.
-    r.sp -= stride;
-    r.cur = *r.sp;                                                          // :434
+    r.sp -= 4u * stride;
+    r.cur = *stack_word(r.sp);                                              // :434
 #pragma unroll
     for (int a = 0; a < 3; ++a) r.p[a] &= ~r.dim;                           // :436
     r.dim <<= 1;                                                            // :438
@@ -376,8 +403,8 @@ __device__ __forceinline__ void ray_phase_descend_raw(Ray &r, uint32_t stride)
     // stays in r.child (no later load overwrites a finished lane's), and the
     // rest of the descent runs on dead state (its stack write lands in the
     // column's spare top slot) rather than behind a branch.
-    *r.sp = r.cur;                                                          // :357
-    r.sp += stride;
+    *stack_word(r.sp) = r.cur;                                              // :357
+    r.sp += 4u * stride;
     r.cur = child;
     r.dim >>= 1;                                                            // :361
     const float tm = ffrom(r.t_min);
@@ -438,7 +465,7 @@ __device__ __forceinline__ void wait_cur(Ray &r)
 // cur -- the node of the next PUSH, or the voxel id of a HIT -- and the child
 // cell chosen.  The next PUSH takes the word after the other lanes' STEP phase
 // has hidden the load.
-template <bool kCount, bool kAsm>
+template <bool kCount, bool kAsm, bool kIdxPlane>
 __device__ __forceinline__ void ray_push_descend(Ray &r, const DevPool &P, uint32_t stride)
 {
     wait_cur<kAsm>(r);
@@ -454,8 +481,9 @@ __device__ __forceinline__ void ray_push_descend(Ray &r, const DevPool &P, uint3
     const uint32_t slot = slot_index(r.cur, c24);
     // descent (:357-373); at the leaf level this is the HIT (:346-355): dim
     // drops below the walk's range, the stack write lands in the spare top slot
-    *r.sp = r.cur;                          // the parent, before its register takes the child's word
-    r.sp += stride;
+    *stack_word(r.sp) = r.cur;              // the parent, before its register takes the child's word
+    if (kIdxPlane) *stack_idx(r.sp) = (uint8_t)r.idx;   // and the child index taken, for the POP back here
+    r.sp += 4u * stride;
     if (kAsm)
         asm volatile("buffer_load_dword %0, %1, %2, 0 idxen ; och_cur_load"
                      : "+v"(r.cur)
@@ -495,34 +523,53 @@ __device__ __forceinline__ void ray_push_descend(Ray &r, const DevPool &P, uint3
     r.idx = nidx;
 }
 
-template <int kPacked, bool kCount, bool kAsm = false>
+template <int kPacked, bool kCount, bool kAsm = false, bool kIdxPlane = false>
 __device__ __forceinline__ void ray_iterate(Ray &r, const DevPool &P, uint32_t stride)
 {
     if (kPacked) {
-        if (in_mode(r, kStepping)) ray_phase_step<kPacked>(r, stride);
+        if (in_mode(r, kStepping)) ray_phase_step<kPacked, kIdxPlane>(r, stride);
         // no activity test: a miss leaves the lane kStepping, a HIT ends in this phase.
         // Tested before an opaque barrier on mode, so the skipping lanes' mode
         // is not re-materialised as kStepping after the test (nor copied)
         const bool push = r.mode != kStepping;
         asm volatile("" : "+v"(r.mode));
-        if (push) ray_push_descend<kCount, kAsm>(r, P, stride);
+        if (push) ray_push_descend<kCount, kAsm, kIdxPlane>(r, P, stride);
         return;
     }
     if (in_mode(r, kPending)) ray_phase_descend_raw(r, stride);
-    if (in_mode(r, kStepping)) ray_phase_step<kPacked>(r, stride);
+    if (in_mode(r, kStepping)) ray_phase_step<kPacked, false>(r, stride);
     if (in_mode(r, kAtPush) && ray_active(r, P)) ray_push_raw<kCount>(r, P);   // PUSH :342-344
 }
 
-// Walk an initialised ray to its HIT or MISS.
+// The root PUSH (ray_setup leaves the ray due to PUSH at the root), then the
+// walk to its HIT or MISS.
 // (A lane mask of active lanes cleared by the MISS and HIT compares instead
-// of this test -- two VALU per iteration -- measured 5 % slower: it added a
-// compare to the descent and SALU to every block, profiles/r05/r05e/.)
-template <int kPacked, bool kCount, bool kAsm = false>
-__device__ __forceinline__ void ray_run(Ray &r, const DevPool &P, uint32_t stride)
+// of the activity test -- two VALU per iteration -- measured 5 % slower: it
+// added a compare to the descent and SALU to every block, profiles/r05/r05e/.)
+template <int kPacked, bool kCount, bool kAsm, bool kIdxPlane>
+__device__ __forceinline__ void ray_walk(Ray &r, const DevPool &P, uint32_t stride)
 {
+    if (kPacked)
+        ray_push_descend<kCount, kAsm, kIdxPlane>(r, P, stride);
+    else
+        ray_push_raw<kCount>(r, P);
     if (ray_active(r, P)) do {
-        ray_iterate<kPacked, kCount, kAsm>(r, P, stride);
+        ray_iterate<kPacked, kCount, kAsm, kIdxPlane>(r, P, stride);
     } while (ray_active(r, P));
+}
+
+// Setup, then the walk.  The branch on root_idx_ok (wave-uniform) comes
+// before the root PUSH issues its asm load, so no copy of cur is made at a
+// join while a load is in flight (tools/isa_check.py).
+template <int kPacked, bool kCount, bool kCull = false, bool kAsm = false>
+__device__ __forceinline__ void ray_trace(Ray &r, const DevPool &P, const float *o, const float *d, uint32_t stack,
+                                          uint32_t stride, bool exact = true)
+{
+    if (!ray_setup<kCount, kCull>(r, P, o, d, stack, stride, exact)) return;
+    if (kPacked && r.root_idx_ok)
+        ray_walk<kPacked, kCount, kAsm, true>(r, P, stride);
+    else
+        ray_walk<kPacked, kCount, kAsm, false>(r, P, stride);
 }
 
 // The hit record of a finished ray (:346-355 hit, :423-431 miss).  The packed
@@ -585,7 +632,7 @@ struct ArraySource {
         return true;
     }
     // Arbitrary rays: no camera shortcut (see CameraSource::get_wave_culled);
-    // ray_init's exact cull still applies.
+    // ray_setup's exact cull still applies.
     __device__ __forceinline__ bool get_wave_culled(uint32_t wave_base, uint32_t lane, const DevPool &, bool,
                                                     float *o, float *d, uint32_t &out, bool &miss) const
     {
@@ -752,7 +799,7 @@ struct TiledArraySource {
         out = i;
         return true;
     }
-    // Arbitrary rays: no camera shortcut; ray_init's exact cull still applies.
+    // Arbitrary rays: no camera shortcut; ray_setup's exact cull still applies.
     __device__ __forceinline__ bool get_wave_culled(uint32_t wave_base, uint32_t lane, const DevPool &, bool,
                                                     float *o, float *d, uint32_t &out, bool &miss) const
     {
@@ -1023,9 +1070,8 @@ __global__ void k_trace_grid(DevPool P, Src S, Sink K, uint32_t xcd_group, const
             K.put(out, Hit{OCH_EXIT, 0u, P.miss_bits, 0u});
         } else {
             Ray r;
-            ray_init<kPacked, kCount, true, kAsmLoad>(r, P, o, d, lds_stack + threadIdx.x, blockDim.x,
+            ray_trace<kPacked, kCount, true, kAsmLoad>(r, P, o, d, stack_column(lds_stack, P.depth), blockDim.x,
                                                       !(Src::kProvenMiss && P.cam_cull));
-            ray_run<kPacked, kCount, kAsmLoad>(r, P, blockDim.x);
             K.put(out, ray_result<kPacked, kAsmLoad>(r, P));
         }
     }
@@ -1046,12 +1092,11 @@ __global__ void k_trace_grid(DevPool P, Src S, Sink K, uint32_t xcd_group, const
 // the secondary rays sit in waves whose 64 lanes all bounce, so the queue
 // frees few waves and the three modes are within about 1 %.
 template <int kPacked, bool kCount, class Sink>
-__device__ __forceinline__ void bounce_in_place(const DevPool &P, const Sink &K, uint32_t *stack, uint32_t nb,
+__device__ __forceinline__ void bounce_in_place(const DevPool &P, const Sink &K, uint32_t stack, uint32_t nb,
                                                 const float *o2, const float *d2, uint32_t out, uint32_t payload)
 {
     Ray r;
-    ray_init<kPacked, kCount, true, kAsmLoad>(r, P, o2, d2, stack, nb);
-    ray_run<kPacked, kCount, kAsmLoad>(r, P, nb);
+    ray_trace<kPacked, kCount, true, kAsmLoad>(r, P, o2, d2, stack, nb);
     K.put_secondary(out, payload, ray_result<kPacked, kAsmLoad>(r, P));
 }
 
@@ -1064,7 +1109,7 @@ __global__ void k_trace_bounce(DevPool P, Src S, Sink K, int compact, const uint
     const uint64_t c0 = cost ? __builtin_amdgcn_s_memtime() : 0;
     const uint32_t blk = order ? order[blockIdx.x] : blockIdx.x;
     const uint64_t t0 = stamps ? realtime() : 0;
-    uint32_t *stack = lds_stack + threadIdx.x;
+    const uint32_t stack = stack_column(lds_stack, P.depth);
     uint32_t *queue = lds_stack;
     const uint32_t nb = blockDim.x;
     const uint32_t wave_base = blk * nb + (threadIdx.x & ~63u);
@@ -1078,8 +1123,7 @@ __global__ void k_trace_bounce(DevPool P, Src S, Sink K, int compact, const uint
             K.put_primary(out, Hit{OCH_EXIT, 0u, P.miss_bits, 0u}, false);
         } else {
             Ray r;
-            ray_init<kPacked, kCount, true, kAsmLoad>(r, P, o, d, stack, nb, !(Src::kProvenMiss && P.cam_cull));
-            ray_run<kPacked, kCount, kAsmLoad>(r, P, nb);
+            ray_trace<kPacked, kCount, true, kAsmLoad>(r, P, o, d, stack, nb, !(Src::kProvenMiss && P.cam_cull));
             const Hit h1 = ray_result<kPacked, kAsmLoad>(r, P);
             want = h1.dir < OCH_EXIT;
             if (want) bounce_ray(o, d, h1, P.half_voxel, o2, d2);
@@ -1136,8 +1180,7 @@ __global__ void k_trace_bounce(DevPool P, Src S, Sink K, int compact, const uint
     __syncthreads();                                  // the queue is read: its LDS becomes stacks again
     if (has) {
         Ray r;
-        ray_init<kPacked, kCount, true, kAsmLoad>(r, P, so, sd, stack, nb);
-        ray_run<kPacked, kCount, kAsmLoad>(r, P, nb);
+        ray_trace<kPacked, kCount, true, kAsmLoad>(r, P, so, sd, stack, nb);
         K.put_secondary(sout, spay, ray_result<kPacked, kAsmLoad>(r, P));
     }
     if (cost && threadIdx.x == 0) cost[blk] = (uint32_t)(__builtin_amdgcn_s_memtime() - c0);
@@ -1244,8 +1287,15 @@ __global__ __launch_bounds__(256) void k_scatter_slots(const uint32_t *__restric
 }
 
 // Per lane: parents of levels 1..depth-1 in slots 1..depth-1, plus a spare
-// slot below (the miss POP's read) and above (the hit descent's write).
-size_t stack_bytes(int depth, int block) { return (size_t)(depth + 1) * block * sizeof(uint32_t); }
+// slot below (the miss POP's read) and above (the hit descent's write); the
+// word plane, and below it the idx plane (stack_column), for a dynamic LDS
+// area that starts at most kStaticLds bytes in (k_trace_bounce's wave counts).
+constexpr size_t kStaticLds = 64;
+size_t stack_bytes(int depth, int block)
+{
+    const size_t e = (size_t)(depth + 1) * block, c = (e + 2) / 3;
+    return 4 * (c > kStaticLds ? c : kStaticLds) + 4 * e;
+}
 
 template <class Src, class Sink, int kPacked, bool kCount>
 hipError_t launch_as(const DevPool &p, const Src &s, const Sink &k, uint32_t n, const Schedule &sc, hipStream_t stream,

@@ -225,11 +225,13 @@ RENDER_KERNEL = "k_trace_gridINS0_12CameraSourceENS0_9FrameSinkELi1ELb0"   # the
 
 
 def walk_loop_counts(lines: list[str]):
-    """Static VALU / SALU of the walk loop (the loop holding the descent's
-    asm load) of one function: from its header to the descent's branch back
-    to the latch, plus the latch.  None when the layout is not recognised."""
+    """Static VALU / SALU of each walk loop (a loop holding the descent's asm
+    load) of one function: from its header to the descent's branch back to the
+    latch, plus the latch.  A list of (valu, salu, reads the stack's idx plane);
+    empty when the layout is not recognised."""
     ins = [l.split(";")[0].rstrip() if not l.lstrip().startswith(".LBB") else l for l in lines]
     pos = {m.group(1): i for i, l in enumerate(ins) if (m := re.match(r"^(\.LBB\d+_\d+):", l.strip()))}
+    loops = []
     for i, l in enumerate(lines):
         if "Inner Loop Header: Depth=1" not in l:
             continue
@@ -237,12 +239,13 @@ def walk_loop_counts(lines: list[str]):
             m = re.match(r"\s*s_branch\s+(\.LBB\d+_\d+)", lines[k])
             if m and pos.get(m.group(1), len(lines)) < i:
                 body = lines[i:k + 1] + lines[pos[m.group(1)]:i]
-                if not any("och_cur_load" in b for b in body):
-                    break
-                valu = sum(1 for b in body if re.match(r"\s*v_", b))
-                salu = sum(1 for b in body if re.match(r"\s*s_", b) and not re.match(r"\s*s_(nop|waitcnt|cbranch|branch)", b))
-                return valu, salu
-    return None
+                if any("och_cur_load" in b for b in body):
+                    valu = sum(1 for b in body if re.match(r"\s*v_", b))
+                    salu = sum(1 for b in body if re.match(r"\s*s_", b)
+                               and not re.match(r"\s*s_(nop|waitcnt|cbranch|branch)", b))
+                    loops.append((valu, salu, any(re.match(r"\s*ds_read_u8", b) for b in body)))
+                break
+    return loops
 
 
 def main(argv=None) -> int:
@@ -267,9 +270,13 @@ def main(argv=None) -> int:
     summary = {"functions": len(fns), "checked": len(checked), "asm_loads": loads, "problems": len(problems),
                "asm_load_enabled": asm_on}
     render = [n for n in fns if RENDER_KERNEL in n]
-    counts = walk_loop_counts(fns[render[0]]) if render else None
-    if counts:
-        summary["render_loop_valu"], summary["render_loop_salu"] = counts
+    loops = walk_loop_counts(fns[render[0]]) if render else []
+    if loops:
+        # the walk that reads idx from the stack (every wave whose rays start inside
+        # the root) first; the rebuilding walk of the other waves beside it
+        loops.sort(key=lambda t: not t[2])
+        summary["render_loop_valu"], summary["render_loop_salu"] = loops[0][:2]
+        summary["render_loops"] = [{"valu": v, "salu": s_, "idx_plane": ip} for v, s_, ip in loops]
     if asm_on and missing:
         problems.append(f"no asm load found in {missing}")
     if problems:
