@@ -103,7 +103,7 @@ struct Ray {
     uint32_t child;       // raw layout: slot word loaded by the last PUSH (pending); the voxel id after a hit
     uint32_t mode;        // see below
     uint32_t push;
-    bool root_idx_ok;     // setup's idx (:324) is the position bits at the root level (stack_idx)
+    bool inside;          // wave-uniform: every ray of the wave starts inside the root (ray_trace)
 };
 
 // Ray phase.  Packed layout (one merged PUSH + descend phase): kStepping (0)
@@ -226,7 +226,7 @@ __device__ __forceinline__ bool ray_setup(Ray &r, const DevPool &P, const float 
 {
     r.inv = 24;
     r.idx = 0;
-    uint32_t root_bits = 0;
+    uint32_t outside = 0;
     uint32_t ent[3];
 #pragma unroll
     for (int a = 0; a < 3; ++a) ent[a] = P.lut[(fbits(d[a]) & 0x7FFFFFu) >> P.lut_shift];
@@ -252,14 +252,16 @@ __device__ __forceinline__ bool ray_setup(Ray &r, const DevPool &P, const float 
         }
         r.p[a] = fbits(refl) & 0x3FC00000u;                                 // :320
         r.idx |= (uint32_t)(r.p[a] == 0x3FC00000u) << a;                    // :324
-        root_bits |= ((r.p[a] >> 22) & 1u) << a;
+        outside |= (r.p[a] >> 23) ^ 0x7Fu;                                  // p not 1.0 or 1.5
     }
-    // A POP rebuilds idx from the position bits (:440-444).  Below the root
-    // those are the bits the descent took, which the stack's idx plane holds;
-    // at the root they are bit 22, which setup's idx matches unless the origin
-    // lies outside the root (p is then not 1.x).  A wave holding such a ray
-    // walks with the rebuild (ray_trace).
-    r.root_idx_ok = __ballot(r.idx != root_bits) == 0;
+    // An origin inside the root, (1, 2)^3, reflects to p = 1.0 or 1.5 on every
+    // axis.  Then a POP's child index (:440-444, the position bits at the new
+    // level) is the one the descent took there, which the stack's idx plane
+    // holds (setup's idx at the root included), and every position has bit 23
+    // set (the exponent's), so the POP chain finds a bit at or below 23 without
+    // forcing one in.  A wave holding a ray from outside the root walks with the
+    // rebuild and the forced bit (ray_trace).
+    r.inside = __ballot(outside != 0) == 0;
     r.dim = 1u << 22;                                                       // :326
     r.cur = P.root;
     r.sp = stack + 4u * stride;                                             // slot 0: the miss POP's dummy read
@@ -288,8 +290,9 @@ __device__ __forceinline__ bool ray_setup(Ray &r, const DevPool &P, const float 
 // The raw layout must load every PUSH's slot to test it, so it resolves the
 // slot first (descend, step, push): an empty child then STEPs in the same
 // iteration.  stride: words between two levels of one lane's LDS stack.
-// kIdxPlane: a POP reads idx from the stack's idx plane (every ray of the
-// wave has root_idx_ok), else rebuilds it from the position bits.
+// kIdxPlane: every ray of the wave starts inside the root (Ray::inside), so a
+// POP reads idx from the stack's idx plane, else it rebuilds it from the
+// position bits.
 template <int kPacked, bool kIdxPlane>
 __device__ __forceinline__ void ray_phase_step(Ray &r, uint32_t stride)
 {
@@ -334,7 +337,7 @@ __device__ __forceinline__ void ray_phase_step(Ray &r, uint32_t stride)
             // the chain from -2 dim itself, whose lowest set bit is 2 dim
             uint32_t nd2;
             asm("v_mul_i32_i24 %0, -2, %1" : "=v"(nd2) : "v"(r.dim));
-            const uint32_t up = ((chain ? pa : nd2) & nd2) | (1u << 23);
+            const uint32_t up = ((chain ? pa : nd2) & nd2) | (kIdxPlane ? 0u : 1u << 23);
             uint32_t k = __builtin_ctz(up);                                 // the new level's bit
             asm volatile("" : "+v"(k));        // 1 << k, not re-folded into up & -up (one VALU more)
             const uint32_t nd = 1u << k;                                    // new child-size bit
@@ -483,7 +486,8 @@ __device__ __forceinline__ void ray_push_descend(Ray &r, const DevPool &P, uint3
     // drops below the walk's range, the stack write lands in the spare top slot
     *stack_word(r.sp) = r.cur;              // the parent, before its register takes the child's word
     if (kIdxPlane) *stack_idx(r.sp) = (uint8_t)r.idx;   // and the child index taken, for the POP back here
-    r.sp += 4u * stride;
+    // sp += 4 stride as sp - (-4 stride): the POP chain's SGPR, not one more
+    asm("v_subrev_u32 %0, %1, %0" : "+v"(r.sp) : "s"(-4 * (int)stride));
     if (kAsm)
         asm volatile("buffer_load_dword %0, %1, %2, 0 idxen ; och_cur_load"
                      : "+v"(r.cur)
@@ -553,12 +557,17 @@ __device__ __forceinline__ void ray_walk(Ray &r, const DevPool &P, uint32_t stri
         ray_push_descend<kCount, kAsm, kIdxPlane>(r, P, stride);
     else
         ray_push_raw<kCount>(r, P);
-    if (ray_active(r, P)) do {
+    // the activity test's two constants in VGPRs: as SGPRs the compiler re-loads
+    // them from the kernel arguments in every iteration when the kernel's SGPR
+    // budget (80, for 8 waves per SIMD) is tight
+    uint32_t lo = P.dim_lo, span = P.dim_span;
+    asm volatile("" : "+v"(lo), "+v"(span));
+    if (r.dim - lo <= span) do {
         ray_iterate<kPacked, kCount, kAsm, kIdxPlane>(r, P, stride);
-    } while (ray_active(r, P));
+    } while (r.dim - lo <= span);
 }
 
-// Setup, then the walk.  The branch on root_idx_ok (wave-uniform) comes
+// Setup, then the walk.  The branch on inside (wave-uniform) comes
 // before the root PUSH issues its asm load, so no copy of cur is made at a
 // join while a load is in flight (tools/isa_check.py).
 template <int kPacked, bool kCount, bool kCull = false, bool kAsm = false>
@@ -566,7 +575,7 @@ __device__ __forceinline__ void ray_trace(Ray &r, const DevPool &P, const float 
                                           uint32_t stride, bool exact = true)
 {
     if (!ray_setup<kCount, kCull>(r, P, o, d, stack, stride, exact)) return;
-    if (kPacked && r.root_idx_ok)
+    if (kPacked && r.inside)
         ray_walk<kPacked, kCount, kAsm, true>(r, P, stride);
     else
         ray_walk<kPacked, kCount, kAsm, false>(r, P, stride);
@@ -1052,7 +1061,7 @@ __device__ __forceinline__ uint32_t xcd_block(uint32_t b, uint32_t nb, uint32_t 
 // end on a few late grazing tiles); cost: optional per-block duration in
 // shader clocks (the planning launch).  Placement only: results are the same.
 template <class Src, class Sink, int kPacked, bool kCount>
-__global__ void k_trace_grid(DevPool P, Src S, Sink K, uint32_t xcd_group, const uint32_t *__restrict__ order,
+__global__ __attribute__((amdgpu_num_sgpr(80))) void k_trace_grid(DevPool P, Src S, Sink K, uint32_t xcd_group, const uint32_t *__restrict__ order,
                              uint32_t *__restrict__ cost, uint64_t *stamps, uint32_t stamp_cap)
 {
     extern __shared__ uint32_t lds_stack[];
@@ -1101,7 +1110,7 @@ __device__ __forceinline__ void bounce_in_place(const DevPool &P, const Sink &K,
 }
 
 template <class Src, class Sink, int kPacked, bool kCount>
-__global__ void k_trace_bounce(DevPool P, Src S, Sink K, int compact, const uint32_t *__restrict__ order,
+__global__ __attribute__((amdgpu_num_sgpr(80))) void k_trace_bounce(DevPool P, Src S, Sink K, int compact, const uint32_t *__restrict__ order,
                                uint32_t *__restrict__ cost, uint64_t *stamps, uint32_t stamp_cap)
 {
     extern __shared__ uint32_t lds_stack[];

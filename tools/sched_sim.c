@@ -262,6 +262,74 @@ static void wave_merged(Ray *R, int n, Stats *S, int popwhile)
 
 static void wave_merged_init(Ray *R, int n, Stats *S, int popwhile) { wave_merged(R, n, S, popwhile); }
 
+/* schedule 5: the round-5 kernel -- merged PUSH + descend, STEP with the POP
+ * chain (a POP goes straight to the level of p_a's lowest set bit above the
+ * current one and advances there; t < 0 or NaN: one POP).  Counts, per
+ * iteration, whether any lane runs each block of the loop (the wave issues a
+ * block's VALU when one lane needs it), and the lanes in it. */
+static double CH_IT, CH_STEP, CH_POP, CH_ADV, CH_PUSH, CH_DESC, CH_LSTEP, CH_LPOP, CH_LADV, CH_LPUSH, CH_LDESC, CH_ACT;
+static int ctz32(uint32_t x) { return __builtin_ctz(x); }
+static void wave_chain(Ray *R, int n, Stats *S)
+{
+    int mode[64];   /* 0 STEP due, 1 PUSH due */
+    for (int i = 0; i < n; ++i) mode[i] = R[i].stepping ? 0 : 1;
+    for (;;) {
+        int act = 0;
+        for (int i = 0; i < n; ++i) act += active(&R[i]);
+        if (!act) break;
+        CH_IT += 1; CH_ACT += act;
+        int ns = 0, npop = 0, nadv = 0, np = 0, nd = 0;
+        for (int i = 0; i < n; ++i) {
+            Ray *r = &R[i];
+            if (!active(r) || mode[i] != 0) continue;
+            ++ns; ++r->iters;
+            uint32_t t[3];
+            for (int a = 0; a < 3; ++a) t[a] = f2u(fmaf(u2f(r->p[a]), r->c[a], r->b[a]));
+            uint32_t tm = t[0] < t[1] ? t[0] : t[1]; tm = tm < t[2] ? tm : t[2];
+            const int ax = t[0] == tm ? 0 : (t[1] == tm ? 1 : 2);
+            r->axis = 1u << ax; r->t_min = tm;
+            if (r->idx & r->axis) { ++nadv; r->p[ax] ^= r->dim; r->idx ^= r->axis; mode[i] = 1; continue; }
+            ++npop;
+            uint32_t mx = t[0] > t[1] ? t[0] : t[1]; mx = mx > t[2] ? mx : t[2];
+            const int chain = mx < 0x80000000u;
+            const uint32_t nd2 = 0u - 2u * r->dim;
+            const uint32_t up = ((chain ? r->p[ax] : nd2) & nd2) | (1u << 23);
+            const int k = ctz32(up);
+            const int lv_new = 23 - k;          /* node level of the popped-to cell: dim = 1 << k */
+            if (k >= 23) { r->level = 0; continue; }   /* MISS */
+            r->sp -= r->level - lv_new; r->level = lv_new;
+            r->cur = r->stack[r->sp];
+            for (int a = 0; a < 3; ++a) r->p[a] &= 0u - (1u << k);
+            r->dim = 1u << k;
+            r->idx = 0;
+            for (int a = 0; a < 3; ++a) r->idx |= ((r->p[a] >> k) & 1u) << a;
+            if (chain) { ++nadv; r->p[ax] ^= r->dim; r->idx ^= r->axis; mode[i] = 1; }
+        }
+        for (int i = 0; i < n; ++i) {
+            Ray *r = &R[i];
+            if (!active(r) || mode[i] != 1) continue;
+            ++np; ++r->push;
+            const uint32_t ch = N[(size_t)(r->cur - 1) * 8 + ((r->idx ^ r->inv) & 7)];
+            if (!ch) { mode[i] = 0; continue; }
+            ++nd;
+            if (r->level == DEPTH) { r->level = DEPTH + 1; continue; }
+            r->stack[r->sp++] = r->cur; ++r->level; r->cur = ch; r->dim >>= 1;
+            uint32_t ni = 0;
+            for (int a = 0; a < 3; ++a) {
+                const uint32_t mid = r->p[a] | r->dim;
+                const int up = fmaf(u2f(mid), r->c[a], r->b[a]) >= u2f(r->t_min);
+                ni |= up << a; if (up) r->p[a] = mid;
+            }
+            r->idx = ni;
+        }
+        CH_STEP += ns > 0; CH_POP += npop > 0; CH_ADV += nadv > 0; CH_PUSH += np > 0; CH_DESC += nd > 0;
+        CH_LSTEP += ns; CH_LPOP += npop; CH_LADV += nadv; CH_LPUSH += np; CH_LDESC += nd;
+        S->iters += 1;
+    }
+    for (int i = 0; i < n; ++i) S->rays_it += R[i].iters;
+    S->waves += 1;
+}
+
 /* schedule 4: wave merging inside a block of NB waves (NB tiles).  Every
  * MERGE_K iterations the block's unfinished rays are packed in order into the
  * fewest waves (finished lanes dropped), as a block-level ballot + LDS
@@ -426,7 +494,7 @@ int main(int argc, char **argv)
                 /* mode from the root PUSH: stepping lanes start in phase A */
                 Ray tmp[64];
                 memcpy(tmp, R, sizeof tmp);
-                wave_merged_init(R, 64, &S, SCHED == 3);
+                if (SCHED == 5) wave_chain(R, 64, &S); else wave_merged_init(R, 64, &S, SCHED == 3);
             } else
                 wave_sched0(R, 64, &S);
         }
@@ -443,5 +511,11 @@ int main(int argc, char **argv)
         for (int l = 1; l <= DEPTH; ++l) fprintf(stderr, " %.0f", LOADS_AT[l]);
         fprintf(stderr, "\n");
     }
+    if (SCHED == 5)
+        printf("{\"iters\": %.0f, \"active_lanes\": %.2f, \"wave_frac\": {\"step\": %.3f, \"pop\": %.3f, \"advance\": %.3f, "
+               "\"push\": %.3f, \"descent\": %.3f}, \"lanes_when_run\": {\"step\": %.1f, \"pop\": %.1f, \"advance\": %.1f, "
+               "\"push\": %.1f, \"descent\": %.1f}}\n",
+               CH_IT, CH_ACT / CH_IT, CH_STEP / CH_IT, CH_POP / CH_IT, CH_ADV / CH_IT, CH_PUSH / CH_IT, CH_DESC / CH_IT,
+               CH_LSTEP / CH_STEP, CH_LPOP / CH_POP, CH_LADV / CH_ADV, CH_LPUSH / CH_PUSH, CH_LDESC / CH_DESC);
     return 0;
 }
