@@ -23,6 +23,9 @@ with the product's flags and checks, in every function that issues the load
      this hazard).  The compiler keeps that distance in
      its own code (its minimum over these kernels is 2); the check holds the
      hand-placed VALU of the descent's child index (ray_push_descend) to it.
+  4. every traversal kernel (k_trace_grid, k_trace_bounce) admits 8 waves per
+     SIMD by its SGPR and VGPR counts (above 80 SGPRs a SIMD takes 7, although
+     the compiler's occupancy note still says 8).
 Exit status 0 and a one-line summary when every kernel passes; 1 with the
 offending instruction otherwise.  Run by the csrc Makefile (`make isa-check`),
 __graft_entry__.build() and tests/test_isa_check.py.
@@ -248,6 +251,29 @@ def walk_loop_counts(lines: list[str]):
     return loops
 
 
+def kernel_resources(asm: str):
+    """{kernel name: (sgpr_count, vgpr_count)} from the code object's metadata."""
+    names = [(m.start(), m.group(1)) for m in re.finditer(r"^\s+\.name:\s+(\S+)", asm, re.M)]
+    out = {}
+    for i, (pos, name) in enumerate(names):
+        end = names[i + 1][0] if i + 1 < len(names) else len(asm)
+        blk = asm[pos:end]
+        sg = re.search(r"\.sgpr_count:\s+(\d+)", blk)
+        vg = re.search(r"\.vgpr_count:\s+(\d+)", blk)
+        if sg and vg:
+            out[name] = (int(sg.group(1)), int(vg.group(1)))
+    return out
+
+
+def waves_per_simd(sgpr: int, vgpr: int) -> int:
+    """Waves a SIMD admits for these registers (MI355X_MICROARCH.md: residency,
+    register files): SGPRs in granules of 16 plus 16 from an 800-entry file,
+    VGPRs in granules of 8 from 512, at most 8."""
+    by_sgpr = 800 // (((sgpr + 15) // 16) * 16 + 16)
+    by_vgpr = 512 // (((vgpr + 7) // 8) * 8)
+    return min(8, by_sgpr, by_vgpr)
+
+
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--source", default=str(CSRC / "och_kernels.hip"))
@@ -279,6 +305,16 @@ def main(argv=None) -> int:
         summary["render_loops"] = [{"valu": v, "salu": s_, "idx_plane": ip} for v, s_, ip in loops]
     if asm_on and missing:
         problems.append(f"no asm load found in {missing}")
+    # 4. the traversal kernels keep 8 waves per SIMD (82 SGPRs admitted 7 and cost
+    #    5 % sustained); the compiler's own occupancy note says 8 there
+    res = kernel_resources(asm)
+    occ = {n: waves_per_simd(*r) for n, r in res.items() if "k_trace_grid" in n or "k_trace_bounce" in n}
+    if render and render[0] in res:
+        summary["render_sgpr"], summary["render_vgpr"] = res[render[0]]
+    summary["traversal_waves_per_simd"] = min(occ.values()) if occ else None
+    for n, w in occ.items():
+        if w < 8:
+            problems.append(f"{n}: {res[n][0]} SGPRs / {res[n][1]} VGPRs admit {w} waves per SIMD, not 8")
     if problems:
         print("isa_check: FAILED " + json.dumps(summary))
         for p in problems[:20]:
