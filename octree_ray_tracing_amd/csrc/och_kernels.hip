@@ -472,11 +472,16 @@ template <bool kCount, bool kAsm, bool kIdxPlane>
 __device__ __forceinline__ void ray_push_descend(Ray &r, const DevPool &P, uint32_t stride)
 {
     wait_cur<kAsm>(r);
-    if (kCount) ++r.push;
+    // Every lane runs the PUSH test (no branch around it: the PUSH phase runs in
+    // 96-99 % of a wave's iterations anyway, tools/sched_sim.c schedule 5); a lane
+    // due to STEP (mode 0) keeps mode 0 and does not descend.  Two SALU and a
+    // branch fewer per iteration: +2.4 % over 20 steps, a lone launch -7 %
+    // (profiles/r05/r05r/).
+    if (kCount) r.push += r.mode != kStepping;
     const uint32_t c24 = r.idx ^ r.inv;                                     // 24 + child index
     const uint32_t present = __builtin_amdgcn_ubfe(r.cur, c24, 1u);
-    r.mode = present;                       // kStepping (0), or nonzero: "PUSH due" after the descent
-    const bool go = present != 0;           // compared before the barrier: present's register becomes mode's
+    r.mode = min(r.mode, present);          // kStepping (0), or 1: "PUSH due" after the descent
+    const bool go = r.mode != kStepping;    // compared before the barrier: no copy of mode
     asm volatile("" : "+v"(r.mode));
     if (!go) return;
     // the child's slot: one 24-bit multiply-add gives its index in the
@@ -532,12 +537,10 @@ __device__ __forceinline__ void ray_iterate(Ray &r, const DevPool &P, uint32_t s
 {
     if (kPacked) {
         if (in_mode(r, kStepping)) ray_phase_step<kPacked, kIdxPlane>(r, stride);
-        // no activity test: a miss leaves the lane kStepping, a HIT ends in this phase.
-        // Tested before an opaque barrier on mode, so the skipping lanes' mode
-        // is not re-materialised as kStepping after the test (nor copied)
-        const bool push = r.mode != kStepping;
+        // no activity test: a miss leaves the lane kStepping, a HIT ends in this
+        // phase; every lane takes the PUSH test (ray_push_descend)
         asm volatile("" : "+v"(r.mode));
-        if (push) ray_push_descend<kCount, kAsm, kIdxPlane>(r, P, stride);
+        ray_push_descend<kCount, kAsm, kIdxPlane>(r, P, stride);
         return;
     }
     if (in_mode(r, kPending)) ray_phase_descend_raw(r, stride);

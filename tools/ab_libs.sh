@@ -3,18 +3,19 @@
 # round, every run a fresh bench.py process (HIP maps streams to hardware queues
 # in creation order, so arms never share a process).
 #   bash tools/ab_libs.sh TAG ROUNDS "BENCH ARGS" ARM [ARM ...]
-# ARM is LABEL:LIB, LIB a build_variants/liboch_gpu_LIB.so name or "default"
-# (the in-tree library).  Outputs gpurun_out/TAG/bench_LABELr.json (r = round),
+# ARM is LABEL:LIB[:EXTRA BENCH ARGS], LIB a build_variants/liboch_gpu_LIB.so name
+# or "default" (the in-tree library).  Outputs gpurun_out/TAG/bench_LABELr.json (r = round),
 # and a one-line summary per run on stdout.  The first failing run ends it.
 set -o pipefail
 TAG=${1:?tag}; R=${2:?rounds}; ARGS=${3:?bench args}; shift 3
 O=gpurun_out/$TAG; mkdir -p "$O"
 for r in $(seq 1 "$R"); do
   for arm in "$@"; do
-    label=${arm%%:*}; lib=${arm#*:}
+    label=${arm%%:*}; rest=${arm#*:}; lib=${rest%%:*}; extra=""
+    [[ "$rest" == *:* ]] && extra=${rest#*:}
     if [[ "$lib" == default ]]; then unset OCH_GPU_LIB; else export OCH_GPU_LIB=build_variants/liboch_gpu_$lib.so; fi
     # shellcheck disable=SC2086
-    timeout -k 10 300 python -u bench.py $ARGS > "$O/bench_$label$r.json" 2> "$O/bench_$label$r.err" \
+    timeout -k 10 300 python -u bench.py $ARGS $extra > "$O/bench_$label$r.json" 2> "$O/bench_$label$r.err" \
       || { echo "run $label$r failed"; tail -20 "$O/bench_$label$r.err"; exit 1; }
     python - "$O/bench_$label$r.json" "$label$r" <<'EOF'
 import json, sys
