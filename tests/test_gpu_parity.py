@@ -204,6 +204,35 @@ def test_random_and_edge_rays_d10(ort, O, gpu_device):
     pool.close()
 
 
+def test_idx_plane_and_rebuild_waves(ort, O, gpu_device):
+    """The walk's two loops (och_kernels.hip ray_trace): a wave whose rays all
+    start inside the root reads each POP's child index from the stack's byte
+    plane; a wave holding one ray from outside rebuilds it from the position
+    bits, as :440-444 does.  Alternate the two kinds wave by wave (64 rays per
+    wave in the trace kernel), with origins on the mid-planes (the default
+    camera's 1.5, and 1.25 / 1.75) and just outside the cube's faces."""
+    tree = ort.build_terrain(8)
+    pool = ort.HOctree(tree.nodes, tree.root, 8, device=0)
+    ref_pool = O.OraclePool(tree.nodes, tree.root, 8, 1)
+    rng = np.random.default_rng(7)
+    n_waves = 400
+    o = rng.uniform(1.01, 1.99, (n_waves, 64, 3)).astype(np.float32)
+    planes = np.array([1.25, 1.5, 1.75], np.float32)
+    on_plane = rng.random((n_waves, 64, 3)) < 0.3
+    o[on_plane] = rng.choice(planes, on_plane.sum())
+    outside = np.array([2.0000768, 0.95, 2.5, 3.5], np.float32)
+    for w in range(1, n_waves, 2):                       # odd waves: one ray from outside the root
+        lane, axis = rng.integers(0, 64), rng.integers(0, 3)
+        o[w, lane, axis] = outside[w % outside.size]
+    d = rng.uniform(-1, 1, (n_waves, 64, 3)).astype(np.float32)
+    d /= np.linalg.norm(d, axis=2, keepdims=True)
+    o, d = o.reshape(-1, 3), d.reshape(-1, 3)
+    for layout in (1, 0):
+        pool.set_option("layout", layout)
+        assert_same(gpu_trace_dev(pool, o, d), O.trace_batch(ref_pool, O.Rcp(None), o, d, nthreads=16, want_push=True))
+    pool.close()
+
+
 @pytest.mark.parametrize("W,H,pitch", [(1920, 1080, 0.0), (1920, 1080, -0.6), (641, 359, 0.4), (64, 36, -1.2)])
 def test_raygen_bit_exact(ort, O, gpu_device, W, H, pitch):
     import torch
