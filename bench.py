@@ -634,6 +634,9 @@ def main():
                     help="N > 1: skip the checksum check of one exchanged frame before the timed window")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--warm-issue", choices=("native", "step"), default="native",
+                    help="how the W warmup steps are issued: as the window issues its steps (default), "
+                         "or one C-ABI render call per step")
     ap.add_argument("--depth", type=int, default=12)
     ap.add_argument("--width", type=int, default=None)
     ap.add_argument("--height", type=int, default=None)
@@ -1121,6 +1124,17 @@ def main():
                     pool.get_option("cull")
             pool.set_stream(stream)
 
+    def warm(n, bounce=False, events=True):
+        """The W untimed steps before a window, issued the way the window issues
+        its steps (one library call for all of them when the window is issued
+        natively, its dispatches recording event pairs as the window's do), so
+        the window's first call is not the process's first of that path."""
+        if native_issue and a.warm_issue == "native" and n > 0:
+            (prepare_sharded if sharded_steps is not None else prepare_native)(n, bounce, [] if events else None)()
+        else:
+            for k in range(n):
+                step(k, None, bounce)
+
     def timed(n, bounce=False, ev=None, marked=False):
         """n steps between barrier + synchronize; max over ranks of the wall time."""
         if marked:
@@ -1227,8 +1241,7 @@ def main():
             "untiled_two_views": round(trace_only["two_views"]["ms_per_launch"] / (2 * n_px) / lone, 3),
             "tiled_two_views": round(trace_only["tiled"]["two_views"]["ms_per_launch"] / (2 * n_px) / lone, 3)}
     # warmup, then the timed steps
-    for k in range(a.warmup):
-        step(k)
+    warm(a.warmup, events=not a.no_step_events)
     ev = None if a.no_step_events else []
     elapsed = timed(a.steps, ev=ev, marked=True)
     ev = ev or []
@@ -1248,11 +1261,9 @@ def main():
     extra, extra_noev = [], []
     for _ in range(a.extra_windows):
         # alternately with and without the per-step timing events
-        for k in range(a.warmup):
-            step(k)
+        warm(a.warmup)
         extra.append(round(total_rays / timed(a.steps, ev=[]) / 1e6, 1))
-        for k in range(a.warmup):
-            step(k)
+        warm(a.warmup, events=False)
         extra_noev.append(round(total_rays / timed(a.steps) / 1e6, 1))
 
     # Sustained: >= a.sustain seconds of steps, three runs, median.
@@ -1297,8 +1308,7 @@ def main():
         pool.set_option("cull", 0)
         if pool.get_option("tile_order") >= 2:
             pool.plan_views(cams, a.row_chunk, rank, world)       # the plan is per cull setting
-        for k in range(a.warmup):
-            step(k)
+        warm(a.warmup, events=False)
         el_off = timed(a.steps)
         cull_off = {"value": round(total_rays / el_off / 1e6, 2), "ms_per_step": round(el_off / a.steps * 1e3, 4),
                     "note": "same warmup and window, OCH_OPT_CULL = 0: every ray walks from the root"}
@@ -1369,8 +1379,7 @@ def main():
         def bounce_run(n):
             # warmup as for the primary line, then the median of three timed runs
             # (one 20-step window alone swings by +-10 %)
-            for k in range(max(a.warmup, 2)):
-                step(k, None, True)
+            warm(max(a.warmup, 2), bounce=True)
             els, kms_ = [], []
             for _ in range(3):
                 bev = []
