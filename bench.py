@@ -620,6 +620,32 @@ def check_exchange(frame, world: int, rank: int, receives: bool):
     return int(bad.item())
 
 
+def agreed_comm(make, world: int, dev, log=print):
+    """The library's communicator, or None on every rank if any rank failed to
+    create it (`make` raised): the ranks agree over torch.distributed (MIN of an
+    ok flag), and a rank that did create one closes it, so all of them fall back
+    to torch.distributed's all-gather together instead of one rank waiting in a
+    collective the others never join."""
+    import torch
+    import torch.distributed as dist
+
+    comm, ok = None, 1
+    try:
+        comm = make()
+    except Exception as e:                         # OchError, or RCCL missing on the box
+        log(f"bench: the library's RCCL communicator failed on this rank ({e}); "
+            "falling back to torch.distributed all_gather_into_tensor")
+        ok = 0
+    if world > 1:
+        flag = torch.tensor([ok], dtype=torch.int32, device=dev)
+        coll(dist.all_reduce, flag, op=dist.ReduceOp.MIN)
+        ok = int(flag.item())
+    if not ok and comm is not None:
+        comm.close()
+        comm = None
+    return comm
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -790,7 +816,8 @@ def main():
     # on every rank.  The gloo rehearsal (several ranks per GPU) keeps torch's.
     comm = None
     if sharded and indexed and backend == "nccl" and a.exchange in ("rccl", "gather"):
-        comm = RcclComm.from_process_group() if dist.is_initialized() else RcclComm.local(local)
+        comm = agreed_comm(RcclComm.from_process_group if dist.is_initialized() else (lambda: RcclComm.local(local)),
+                           world, dev, log)
     exch_mode = "gather" if (comm is not None and a.exchange == "gather") else "all_gather"
     if exch_mode == "gather" and a.shade != "display":
         raise SystemExit("--exchange gather needs --shade display")

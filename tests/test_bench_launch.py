@@ -103,3 +103,44 @@ def test_check_exchange_gloo_world2(corrupt, receives_all, want):
         p.join(timeout=60)
         assert p.exitcode == 0
     assert got == {0: want, 1: want}
+
+
+class _FakeComm:
+    closed = False
+
+    def close(self):
+        _FakeComm.closed = True
+
+
+def _comm_worker(rank, world, port, fail_rank, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+
+    def make():
+        if rank == fail_rank:
+            raise RuntimeError("ncclCommInitRank failed (test)")
+        return _FakeComm()
+    comm = bench.agreed_comm(make, world, torch.device("cpu"), log=lambda *a: None)
+    q.put((rank, comm is not None, _FakeComm.closed))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("fail_rank", [-1, 1])
+def test_agreed_comm_gloo_world2(fail_rank):
+    """The library communicator is used only if every rank made one: when rank 1
+    fails, rank 0 closes its own and both fall back together."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 33700 + os.getpid() % 1000 + 5 * (fail_rank + 1)
+    procs = [ctx.Process(target=_comm_worker, args=(r, 2, port, fail_rank, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = dict((r, (has, closed)) for r, has, closed in (q.get(timeout=120) for _ in range(2)))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    if fail_rank < 0:
+        assert got == {0: (True, False), 1: (True, False)}
+    else:
+        assert got == {0: (False, True), 1: (False, False)}
