@@ -491,8 +491,6 @@ __device__ __forceinline__ void ray_push_descend(Ray &r, const DevPool &P, uint3
     // drops below the walk's range, the stack write lands in the spare top slot
     *stack_word(r.sp) = r.cur;              // the parent, before its register takes the child's word
     if (kIdxPlane) *stack_idx(r.sp) = (uint8_t)r.idx;   // and the child index taken, for the POP back here
-    // sp += 4 stride as sp - (-4 stride): the POP chain's SGPR, not one more
-    asm("v_subrev_u32 %0, %1, %0" : "+v"(r.sp) : "s"(-4 * (int)stride));
     if (kAsm)
         asm volatile("buffer_load_dword %0, %1, %2, 0 idxen ; och_cur_load"
                      : "+v"(r.cur)
@@ -502,33 +500,37 @@ __device__ __forceinline__ void ray_push_descend(Ray &r, const DevPool &P, uint3
         r.cur = (P.nodes - 24)[slot];       // the compiler's own load (OCH_ASM_LOAD=0 builds)
     r.dim >>= 1;
     const float tm = ffrom(r.t_min);
-    uint32_t nidx = 0;
+    uint32_t nidx;
     // z, y, x: idx = 2 idx + upper as one v_addc_co_u32 with the compare's
-    // mask as carry-in (the compiler builds 3 v_cndmask + v_or3 instead).
-    // s_nop 1: the two wait states between a VALU write of vcc and its read as
-    // a lane mask, which the compiler inserts for its own code (tools/isa_check.py
-    // check 3 holds this asm to it)
-#pragma unroll
-    for (int a = 2; a >= 0; --a) {
-        const uint32_t mid = r.p[a] | r.dim;
-        const float t = __builtin_fmaf(ffrom(mid), r.c[a], r.b[a]);
-        if (a == 2)
-            asm volatile("v_cmp_ge_f32_e32 vcc, %2, %3\n\t"
-                         "s_nop 1\n\t"
-                         "v_cndmask_b32_e32 %0, %0, %4, vcc\n\t"
-                         "v_cndmask_b32_e64 %1, 0, 1, vcc"
-                         : "+v"(r.p[a]), "=v"(nidx)
-                         : "v"(t), "v"(tm), "v"(mid)
-                         : "vcc");
-        else
-            asm volatile("v_cmp_ge_f32_e32 vcc, %2, %3\n\t"
-                         "s_nop 1\n\t"
-                         "v_cndmask_b32_e32 %0, %0, %4, vcc\n\t"
-                         "v_addc_co_u32_e32 %1, vcc, %1, %1, vcc"
-                         : "+v"(r.p[a]), "+v"(nidx)
-                         : "v"(t), "v"(tm), "v"(mid)
-                         : "vcc");
-    }
+    // mask as carry-in (the compiler builds 3 v_cndmask + v_or3 instead).  A VALU
+    // write of vcc is read as a lane mask two wait states later at the soonest
+    // (the compiler's own code keeps that distance; tools/isa_check.py check 3
+    // holds this asm to it): the next axis's mid-plane and t fill the two states
+    // after the z and y compares, and the stack pointer's step (sp += 4 stride as
+    // sp - (-4 stride): the POP chain's SGPR, not one more) one after the x compare.
+    const uint32_t m2 = r.p[2] | r.dim;
+    const float t2 = __builtin_fmaf(ffrom(m2), r.c[2], r.b[2]);
+    uint32_t m1, m0, t1, t0;
+    asm volatile("v_cmp_ge_f32_e32 vcc, %[t2], %[tm]\n\t"
+                 "v_or_b32_e32 %[m1], %[dim], %[p1]\n\t"
+                 "v_fma_f32 %[t1], %[m1], %[c1], %[b1]\n\t"
+                 "v_cndmask_b32_e32 %[p2], %[p2], %[m2], vcc\n\t"
+                 "v_cndmask_b32_e64 %[idx], 0, 1, vcc\n\t"
+                 "v_cmp_ge_f32_e32 vcc, %[t1], %[tm]\n\t"
+                 "v_or_b32_e32 %[m0], %[dim], %[p0]\n\t"
+                 "v_fma_f32 %[t0], %[m0], %[c0], %[b0]\n\t"
+                 "v_cndmask_b32_e32 %[p1], %[p1], %[m1], vcc\n\t"
+                 "v_addc_co_u32_e32 %[idx], vcc, %[idx], %[idx], vcc\n\t"
+                 "v_cmp_ge_f32_e32 vcc, %[t0], %[tm]\n\t"
+                 "v_subrev_u32 %[sp], %[n4s], %[sp]\n\t"
+                 "s_nop 0\n\t"
+                 "v_cndmask_b32_e32 %[p0], %[p0], %[m0], vcc\n\t"
+                 "v_addc_co_u32_e32 %[idx], vcc, %[idx], %[idx], vcc"
+                 : [p2] "+v"(r.p[2]), [p1] "+v"(r.p[1]), [p0] "+v"(r.p[0]), [sp] "+v"(r.sp), [idx] "=&v"(nidx), [m1] "=&v"(m1),
+                   [m0] "=&v"(m0), [t1] "=&v"(t1), [t0] "=&v"(t0)
+                 : [t2] "v"(t2), [tm] "v"(tm), [m2] "v"(m2), [dim] "v"(r.dim), [c1] "v"(r.c[1]), [b1] "v"(r.b[1]),
+                   [c0] "v"(r.c[0]), [b0] "v"(r.b[0]), [n4s] "s"(-4 * (int)stride)
+                 : "vcc");
     r.idx = nidx;
 }
 
@@ -536,7 +538,9 @@ template <int kPacked, bool kCount, bool kAsm = false, bool kIdxPlane = false>
 __device__ __forceinline__ void ray_iterate(Ray &r, const DevPool &P, uint32_t stride)
 {
     if (kPacked) {
-        if (in_mode(r, kStepping)) ray_phase_step<kPacked, kIdxPlane>(r, stride);
+        // mode is already behind a barrier (ray_push_descend, and before it below),
+        // so no second one here: that one cost an s_nop before this compare
+        if (r.mode == kStepping) ray_phase_step<kPacked, kIdxPlane>(r, stride);
         // no activity test: a miss leaves the lane kStepping, a HIT ends in this
         // phase; every lane takes the PUSH test (ray_push_descend)
         asm volatile("" : "+v"(r.mode));
