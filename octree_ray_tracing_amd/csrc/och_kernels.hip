@@ -136,7 +136,7 @@ __device__ __forceinline__ lds_byte *stack_idx(uint32_t a) { return (lds_byte *)
 // This lane's stack column (the LDS byte address of its slot 0).  The word
 // plane starts at wb with wb / 4 >= the dynamic area's start (the idx plane
 // stays clear of static LDS) and wb / 4 + e <= wb (it stays below the word
-// plane): e = (depth + 1) * blockDim slots.  stack_lds_bytes sizes the area.
+// plane): e = (depth + 1) * blockDim slots.  stack_bytes sizes the area.
 __device__ __forceinline__ uint32_t stack_column(const uint32_t *lds, uint32_t depth)
 {
     const uint32_t base = (uint32_t)(uintptr_t)(const lds_word *)lds;
@@ -1067,6 +1067,10 @@ __device__ __forceinline__ uint32_t xcd_block(uint32_t b, uint32_t nb, uint32_t 
 // most expensive workgroups of the planning frame first, so the frame does not
 // end on a few late grazing tiles); cost: optional per-block duration in
 // shader clocks (the planning launch).  Placement only: results are the same.
+// The traversal kernels are capped at 80 SGPRs: above 80 a SIMD admits 7 waves, not 8
+// (MI355X_MICROARCH.md, residency; the compiler's occupancy note says 8 there), and 8
+// give +5 % sustained.  tools/isa_check.py check 4 holds every
+// traversal kernel to 8 waves per SIMD.
 template <class Src, class Sink, int kPacked, bool kCount>
 __global__ __attribute__((amdgpu_num_sgpr(80))) void k_trace_grid(DevPool P, Src S, Sink K, uint32_t xcd_group, const uint32_t *__restrict__ order,
                              uint32_t *__restrict__ cost, uint64_t *stamps, uint32_t stamp_cap)
