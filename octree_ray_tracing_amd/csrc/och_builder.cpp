@@ -379,6 +379,7 @@ bool build_bricks_gpu(const Terrain &tr, NodeStore &ns, int threads, const std::
 {
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return false;
+    (void)hipGetLastError();        // a stale error of an earlier HIP call (another library's) is not this build's
     const size_t n_work = work.size();
     const size_t B = 4096;                        // bricks per batch: 64 MiB of codes
     int32_t *d_heights = nullptr;
@@ -748,6 +749,7 @@ int build_dag_gpu(const Terrain &tr, uint32_t cap, const std::vector<uint32_t> &
 {
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return OCH_E_NODEV;
+    (void)hipGetLastError();        // a stale error of an earlier HIP call (another library's) is not this build's
     const size_t n_work = work.size();
     const size_t B = 8192;                                    // bricks per batch
     const size_t cols = (size_t)tr.dim * tr.dim, grid_cells = (size_t)G * G * G;

@@ -233,6 +233,40 @@ def test_idx_plane_and_rebuild_waves(ort, O, gpu_device):
     pool.close()
 
 
+def test_stale_hip_error_is_not_a_launch_failure(ort, O, gpu_device):
+    """A launch reports hipGetLastError(), which also returns an error an earlier
+    HIP call of the thread left behind (another library's: RCCL's communicator
+    init, say).  The library clears it before each launch, so a failed HIP call
+    made by someone else does not fail the next render or trace."""
+    import ctypes
+    import torch
+    tree = ort.build_terrain(6)
+    pool = ort.HOctree(tree.nodes, tree.root, 6, device=0)
+    pool.set_stream(torch.cuda.current_stream())
+    # every HIP runtime loaded in this process (torch's, and the one the library
+    # resolved, if another): set the thread's last error in each
+    paths = sorted({line.split()[-1] for line in open("/proc/self/maps") if "libamdhip64" in line})
+    hips = [ctypes.CDLL(x) for x in paths]
+    assert hips
+    for h in hips:
+        h.hipSetDevice.argtypes = [ctypes.c_int]
+
+    def spoil():
+        for h in hips:
+            assert h.hipSetDevice(1 << 20) != 0          # an invalid ordinal: the thread's last error is set
+    cam = ort.camera((1.5, 1.5, 1.5), 0.3, -0.3, 1.25, 64, 36)
+    want = pool.render(cam)
+    for _ in range(2):
+        spoil()
+        assert np.array_equal(pool.render(cam), want)
+    o = np.tile(ORIGIN, (256, 1))
+    d = np.random.default_rng(3).uniform(-1, 1, (256, 3)).astype(np.float32)
+    ref = gpu_trace_dev(pool, o, d)
+    spoil()
+    assert_same(gpu_trace_dev(pool, o, d), ref)
+    pool.close()
+
+
 @pytest.mark.parametrize("W,H,pitch", [(1920, 1080, 0.0), (1920, 1080, -0.6), (641, 359, 0.4), (64, 36, -1.2)])
 def test_raygen_bit_exact(ort, O, gpu_device, W, H, pitch):
     import torch
