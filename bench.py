@@ -729,8 +729,9 @@ def main():
                          "+ och_deal_chunks), by count (rank 0 at --display-weight), or round-robin")
     ap.add_argument("--display-weight", type=float, default=None,
                     help="N > 1 with --shade display: rank 0's share of the row chunks relative to the other ranks "
-                         "(it also shades the whole frame); default ort.display_weight(N, exchange): 0.9 / 0.7 / "
-                         "0.5 at N = 2 / 4 / 8 with the gather, from tools/proxy_rank.py sweeps (DESIGN.md §5)")
+                         "(it also shades the whole frame); default ort.display_weight(N, exchange): 0.9 / 0.8 / "
+                         "0.5 at N = 2 / 4 / 8 with the all-gather, 0.9 / 0.7 / 0.5 with the gather, from "
+                         "tools/proxy_rank.py sweeps (DESIGN.md §5)")
     ap.add_argument("--no-direct", action="store_true",
                     help="N = 1: render codes and shade them in a second pass, as ranks do at N > 1, instead of "
                          "the fused launch writing the RGBA8 frames directly")

@@ -389,7 +389,10 @@ def deal_chunks(costs, n_shards: int, weights=None) -> np.ndarray:
 # per world size and exchange, from tools/proxy_rank.py sweeps of every shard
 # (profiles/r04/r04e/, r04f/): with the gather to rank 0 the
 # other ranks receive nothing, so the display rank takes a smaller share.
-DISPLAY_WEIGHTS = {"gather": {2: 0.9, 4: 0.7, 8: 0.5}, "all_gather": {2: 0.9, 4: 0.8, 8: 0.6}}
+# rank 0's deal weight by exchange and world size (tools/proxy_rank.py sweeps,
+# DESIGN.md §5); N = 8 all-gather 0.5 since round 5's faster kernel made the
+# display rank's whole-frame shade a larger part of its step (profiles/r05/r05al/)
+DISPLAY_WEIGHTS = {"gather": {2: 0.9, 4: 0.7, 8: 0.5}, "all_gather": {2: 0.9, 4: 0.8, 8: 0.5}}
 
 
 def display_weight(world: int, exchange: str = "all_gather") -> float:

@@ -146,14 +146,14 @@ def test_gloo_world2_dealt_exchange(ort):
 def test_gloo_world8_bench_deal_exchange(ort):
     """The deal the driver's 8-GPU run uses (configs[3]: 2160 rows in 8-row
     chunks, dealt by count with the display rank at display_weight(8) =
-    0.6, the all-gather's weight, as bench.py does over RCCL), broadcast from rank 0 and
+    0.5, the all-gather's weight, as bench.py does over RCCL), broadcast from rank 0 and
     exchanged by 8 gloo ranks: the padded slices all-gather into the whole
     frame on every rank."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     H, W, chunk, world = 2160, 4, 8, 8
     n_chunks = -(-H // chunk)
-    assert ort.display_weight(world, "gather") == 0.5 and ort.display_weight(world) == 0.6
+    assert ort.display_weight(world, "gather") == 0.5 and ort.display_weight(world) == 0.5
     deal = ort.deal_chunks(np.ones(n_chunks, np.float32), world, [ort.display_weight(world)] + [1.0] * (world - 1))
     counts = np.bincount(deal, minlength=world)
     assert counts[0] < counts[1:].min()                           # the display rank renders fewer rows
