@@ -1195,9 +1195,9 @@ def main():
         trace_parts = False
         in_window = True
         drain()
-        if world > 1:
+        if world > 1:                      # the ranks' barrier, then this rank's synchronize again
             dist.barrier()
-        drain()
+            drain()
         in_window = False
         t1 = time.perf_counter()
         if marked and a.host_stamps:
