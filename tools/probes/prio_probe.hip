@@ -68,13 +68,13 @@ int main()
             CK(hipEventElapsedTime(&tab, a0, b1));
             printf("rep %d %-20s A %.1f us  B %.1f us  B ends %.1f us after A starts\n", rep, arm.name,
                    ta * 1e3, tb * 1e3, tab * 1e3);
-            hipEventDestroy(a0);
-            hipEventDestroy(a1);
-            hipEventDestroy(b0);
-            hipEventDestroy(b1);
-            hipStreamDestroy(sa);
-            hipStreamDestroy(sb);
+            (void)hipEventDestroy(a0);
+            (void)hipEventDestroy(a1);
+            (void)hipEventDestroy(b0);
+            (void)hipEventDestroy(b1);
+            (void)hipStreamDestroy(sa);
+            (void)hipStreamDestroy(sb);
         }
-    hipFree(out);
+    (void)hipFree(out);
     return 0;
 }
