@@ -134,6 +134,91 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+METRIC = "Mrays/sec primary traversal (depth-12 SVO-DAG, raygen+trace+shade per frame)"
+
+
+class Watchdog:
+    """A deadline on every stage of a run, so a hang ends the run at once and
+    says where.  A collective whose peer never comes (a rank that died, or never
+    issued its side) blocks its stream and the host waiting on it; torch's own
+    timeout does not cover the library's RCCL communicator or the spin-waits on
+    the frame streams.  The stage names what this rank is doing; when its
+    deadline passes, a thread of this process aborts the library's
+    communicator(s) (ncclCommAbort, och_comm_abort), prints one JSON line
+    naming the stage (rank 0 on stdout, the others on stderr) and ends the
+    process with status 3 -- never by exec.  The launcher then stops the other
+    ranks.  enter(stage, seconds) starts a stage; done() disarms."""
+
+    EXIT = 3
+
+    def __init__(self, rank: int, world: int, poll_s: float = 0.25, exit_fn=None, out=None):
+        self.rank, self.world = rank, world
+        self.stage, self.deadline, self.limit = "start", None, None
+        self.aborts = []
+        self.poll_s = poll_s
+        self._exit = exit_fn or os._exit
+        self._out = out
+        self._lock = threading.Lock()
+        self._t0 = time.monotonic()
+        threading.Thread(target=self._run, name="bench-watchdog", daemon=True).start()
+
+    def enter(self, stage: str, seconds: float):
+        with self._lock:
+            self.stage, self.limit = stage, float(seconds)
+            self.deadline = time.monotonic() + float(seconds)
+
+    def done(self):
+        with self._lock:
+            self.deadline = None
+
+    def on_expiry(self, fn):
+        """fn() runs (on the watchdog's thread, bounded) before the exit."""
+        self.aborts.append(fn)
+
+    def _run(self):
+        while True:
+            time.sleep(self.poll_s)
+            with self._lock:
+                late = self.deadline is not None and time.monotonic() > self.deadline
+                stage, limit = self.stage, self.limit
+            if late:
+                self._expire(stage, limit)
+                return
+
+    def _expire(self, stage, limit):
+        aborted = []
+
+        def abort(fn):
+            fn()
+            aborted.append(fn)
+        for fn in self.aborts:              # each abort on its own thread: a hung abort cannot hold the exit
+            t = threading.Thread(target=abort, args=(fn,), daemon=True)
+            t.start()
+            t.join(timeout=10.0)
+        line = {"metric": METRIC, "value": None, "unit": "Mrays/s", "n_gpus": self.world,
+                "error": f"stage '{stage}' passed its {limit:g} s deadline on rank {self.rank}",
+                "stage": stage, "rank": self.rank, "deadline_s": limit,
+                "elapsed_s": round(time.monotonic() - self._t0, 1), "communicators_aborted": len(aborted)}
+        out = self._out or (sys.stdout if self.rank == 0 else sys.stderr)
+        try:
+            print(json.dumps(line), file=out, flush=True)
+            if out is not sys.stderr:
+                log(f"bench watchdog: {line['error']}")
+        finally:
+            self._exit(self.EXIT)
+
+
+# Deadlines per stage (seconds).  The driver gives a whole bench run 600 s;
+# every stage of a healthy run takes a small part of its deadline (the
+# slowest, the N > 1 parity check on the CPU, about 30 s), so only a hang
+# reaches one.
+DEADLINES = {"init": 120, "pool": 120, "comm": 120, "setup": 120, "exchange check": 60, "window": 60,
+             "scaling base": 120, "cpu leg": 300, "other configs": 180, "teardown": 60}
+# torch.distributed's timeout: rendezvous, and every torch collective (a rank
+# waits in one at most through another rank's "pool" or "scaling base" stage).
+PG_TIMEOUT_S = 150
+
+
 def kernel_source_digest() -> str:
     """Identity of the kernel code a PMC profile was taken of."""
     h = hashlib.sha256()
@@ -220,8 +305,10 @@ def cpu_leg(nodes, root, depth, width, height, frames, bounce_frames, time_it: b
     from oracle import oracle as O
     import octree_ray_tracing_amd as ort
 
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or len(os.sched_getaffinity(0))
-    threads = max(1, min(threads, 64))
+    allowed = len(os.sched_getaffinity(0))
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or allowed
+    threads = max(1, min(threads, allowed, 64))
+    hw_threads = os.cpu_count() or allowed
     pool = O.OraclePool(nodes, root, depth, 1)
     rcp = O.Rcp(None)
     pal = ort.VoxelData().get_colours()
@@ -278,9 +365,12 @@ def cpu_leg(nodes, root, depth, width, height, frames, bounce_frames, time_it: b
     except Exception:
         cpu = "unknown"
     n2 = width * height * len(PITCHES)
+    share = (f"{threads} of {hw_threads} hardware threads ({cpu}; this process's CPU affinity allows {allowed}, "
+             f"OMP_NUM_THREADS={os.environ.get('OMP_NUM_THREADS', 'unset')})")
     base = {"value": rays_done / t_total / 1e6, "unit": "Mrays/s", "cores": threads, "kind": "port",
+            "cores_note": share, "hardware_threads": hw_threads, "affinity_threads": allowed, "cpu_model": cpu,
             "sample": f"{n} traversals of full {width}x{height} camera frames (pitch 0 / -0.6 alternating, "
-                      f"rays generated untimed), depth {depth}, {threads} threads on {cpu}, {t_total:.1f}s",
+                      f"rays generated untimed), depth {depth}, {share}, {t_total:.1f}s",
             "value_1core": n2 / t1 / 1e6,
             "sample_1core": f"the two views' traversal once on 1 thread, {t1:.1f}s",
             "value_frame_path": n2 / tf / 1e6,
@@ -444,7 +534,11 @@ def group_bench(a):
     from octree_ray_tracing_amd.frame import FrameGroup
 
     n = a.gpus
-    inflight, _ = pipeline_defaults(n, a.inflight, a.hw_queues)
+    inflight, hw_queues = pipeline_defaults(n, a.inflight, a.hw_queues)
+    if hw_queues is not None and os.environ.get("GPU_MAX_HW_QUEUES") != str(hw_queues):
+        raise SystemExit("--launch group: GPU_MAX_HW_QUEUES must be set before HIP starts (main does)")
+    wd = Watchdog(0, n)
+    wd.enter("setup", DEADLINES["setup"])
     W, H = frame_size(n, a.width, a.height, a.scaling)
     torch.cuda.set_device(0)
     tree = ort.build_terrain(a.depth, use_gpu=True)
@@ -458,11 +552,14 @@ def group_bench(a):
         g.plan(cams, a.row_chunk)
 
         def window(steps):
+            wd.enter("window", DEADLINES["window"])
             g.synchronize()
             t0 = time.perf_counter()
             g.render_steps(cams, steps, inflight, a.row_chunk)
             g.synchronize()
-            return time.perf_counter() - t0
+            el_ = time.perf_counter() - t0
+            wd.enter("setup", DEADLINES["setup"])
+            return el_
 
         window(max(a.warmup, 1))
         el = window(a.steps)
@@ -477,13 +574,14 @@ def group_bench(a):
     finally:
         g.close()
     parity = None
+    wd.enter("cpu leg", DEADLINES["cpu leg"])
     if not a.no_parity:
         _, parity = cpu_leg(tree.nodes, tree.root, a.depth, W, H, frames[0], None, time_it=False, budget_s=0)
         parity["devices_equal_rank0"] = all(np.array_equal(f, frames[0]) for f in frames)
         if not parity["devices_equal_rank0"]:
             parity["mismatches"] += 1
     line = {
-        "metric": "Mrays/sec primary traversal (depth-12 SVO-DAG, raygen+trace+shade per frame)",
+        "metric": METRIC,
         "value": round(rays * a.steps / el / 1e6, 2), "unit": "Mrays/s", "n_gpus": n, "steps": a.steps,
         "warmup": a.warmup, "ms_per_step": round(el / a.steps * 1e3, 4), "higher_is_better": True,
         "scaling": "strong", "vs_baseline": None, "dtype": "f32",
@@ -493,11 +591,13 @@ def group_bench(a):
                    "launch": "one process, one issuing thread per device (och_frame_group_render_steps)",
                    "exchange": "RCCL all-gather (ncclCommInitAll communicators), every device shades the frame",
                    "row_deal": "och_frame_group_plan: chunks dealt by their cost in one timed render",
-                   "frames_in_flight": inflight, "width": W, "height": H, "depth": a.depth,
+                   "frames_in_flight": inflight, "hw_queues": int(os.environ.get("GPU_MAX_HW_QUEUES", "4")),
+                   "width": W, "height": H, "depth": a.depth,
                    "dag_nodes": int(tree.n_nodes), "parallelism": f"rows{n}"},
         "sustained": sustained, "parity": parity, "roofline": None, "cpu_baseline": None,
     }
     print(json.dumps(line), flush=True)
+    wd.done()
     if parity is not None and parity["mismatches"]:
         raise SystemExit("group frames differ from the oracle")
 
@@ -620,29 +720,68 @@ def check_exchange(frame, world: int, rank: int, receives: bool):
     return int(bad.item())
 
 
-def agreed_comm(make, world: int, dev, log=print):
-    """The library's communicator, or None on every rank if any rank failed to
-    create it (`make` raised): the ranks agree over torch.distributed (MIN of an
-    ok flag), and a rank that did create one closes it, so all of them fall back
-    to torch.distributed's all-gather together instead of one rank waiting in a
-    collective the others never join."""
+def agreed_comm(world: int, rank: int, dev, unique_id, available, create, log=print, id_bytes: int = 128):
+    """The library's RCCL communicator, or None on every rank.  The ranks agree
+    before each step that could leave one of them in a collective the others
+    never join:
+      1. rank 0 makes the id; whether it could travels in the same broadcast;
+      2. every rank says whether it can join at all (RCCL loadable): MIN all-reduce;
+      3. every rank joins (ncclCommInitRank returns once all of them have joined;
+         a rank that fails inside it leaves its peers there -- the watchdog's
+         'comm' deadline ends that);
+      4. MIN all-reduce of the join's outcome: if any rank failed, the ranks
+         that joined close theirs, and all fall back to torch.distributed's
+         all-gather together.
+    unique_id() -> bytes; available() -> bool; create(uid) -> communicator
+    (each may raise)."""
     import torch
     import torch.distributed as dist
 
-    comm, ok = None, 1
-    try:
-        comm = make()
-    except Exception as e:                         # OchError, or RCCL missing on the box
-        log(f"bench: the library's RCCL communicator failed on this rank ({e}); "
+    def fell_back(what, e):
+        log(f"bench: the library's RCCL communicator: {what} failed on this rank ({e}); "
             "falling back to torch.distributed all_gather_into_tensor")
-        ok = 0
-    if world > 1:
-        flag = torch.tensor([ok], dtype=torch.int32, device=dev)
+
+    def agree(ok):
+        if world == 1:
+            return ok
+        flag = torch.tensor([int(ok)], dtype=torch.int32, device=dev)
         coll(dist.all_reduce, flag, op=dist.ReduceOp.MIN)
-        ok = int(flag.item())
-    if not ok and comm is not None:
-        comm.close()
-        comm = None
+        return int(flag.item())
+
+    uid, ok = b"", 1
+    if rank == 0:
+        try:
+            uid = unique_id()
+        except Exception as e:                     # OchError: RCCL missing, or no id
+            fell_back("ncclGetUniqueId", e)
+            ok = 0
+    if world > 1:                                  # step 1: the id and rank 0's flag, one broadcast
+        buf = torch.zeros(id_bytes + 1, dtype=torch.uint8, device=dev)
+        if rank == 0:
+            ok = int(ok and len(uid) == id_bytes)
+            buf[0] = ok
+            if ok:
+                buf[1:] = torch.frombuffer(bytearray(uid), dtype=torch.uint8)
+        coll(dist.broadcast, buf, 0)
+        h = buf.cpu()
+        ok, uid = int(h[0]), bytes(h[1:].numpy().tobytes())
+    if ok and rank != 0:                           # step 2
+        try:
+            ok = int(bool(available()))
+        except Exception as e:
+            fell_back("loading RCCL", e)
+            ok = 0
+    if not agree(ok):
+        return None
+    comm = None
+    try:                                           # step 3
+        comm = create(uid)
+    except Exception as e:
+        fell_back("ncclCommInitRank", e)
+    if not agree(comm is not None):                # step 4
+        if comm is not None:
+            comm.close()
+        return None
     return comm
 
 
@@ -754,9 +893,20 @@ def main():
                          "environment's (4 on the box), 8 at N >= 8")
     a = ap.parse_args()
 
-    # A plain `bench.py --gpus N` (no launcher) must measure N GPUs or fail:
-    # torch.cuda.device_count() does not initialise HIP on this image, so the
-    # child ranks can still be started from here.
+    # Frames in flight and hardware queues by world size (tools/proxy_rank.py,
+    # every shard, profiles/r03/proxy/r03z*): at N = 8 a rank's launches are half
+    # the size of N = 1's and end on the same ~0.2 ms grazing tiles, so more
+    # frames must overlap -- 6 frames on 8 hardware queues: job 192 -> 211 G rays/s
+    # over 20 steps, 215 -> 242 G sustained; at N = 1, 2, 4 the default 3 on 4
+    # queues is best.  Set before anything can start HIP (torch.cuda.device_count
+    # below does not on this image while amdsmi is importable, but may without it).
+    world_env = int(os.environ.get("WORLD_SIZE", "0")) or (a.gpus if a.launch == "group" else 1)
+    a.inflight, a.hw_queues = pipeline_defaults(world_env, a.inflight, a.hw_queues)
+    if a.hw_queues is not None:
+        os.environ["GPU_MAX_HW_QUEUES"] = str(a.hw_queues)
+
+    # A plain `bench.py --gpus N` (no launcher) must measure N GPUs or fail;
+    # the child ranks are started from here, never by exec.
     import torch
     launch = resolve_launch(a.gpus, os.environ, a.launch, torch.cuda.device_count())
     if launch == "procs":
@@ -764,23 +914,15 @@ def main():
     if launch == "group":
         return group_bench(a)
 
-    # Frames in flight and hardware queues by world size (tools/proxy_rank.py,
-    # every shard, profiles/r03/proxy/r03z*): at N = 8 a rank's launches are half
-    # the size of N = 1's and end on the same ~0.2 ms grazing tiles, so more
-    # frames must overlap -- 6 frames on 8 hardware queues: job 192 -> 211 G rays/s
-    # over 20 steps, 215 -> 242 G sustained; at N = 1, 2, 4 the default 3 on 4
-    # queues is best.
-    a.inflight, a.hw_queues = pipeline_defaults(int(os.environ.get("WORLD_SIZE", "1")), a.inflight, a.hw_queues)
-    if a.hw_queues is not None:
-        os.environ["GPU_MAX_HW_QUEUES"] = str(a.hw_queues)
-
-    import torch
+    import datetime
     import torch.distributed as dist
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     backend = os.environ.get("OCH_DIST_BACKEND", "nccl")
+    wd = Watchdog(rank, world)
+    wd.enter("init", DEADLINES["init"])
     if backend == "gloo":
         # Rehearsal of the N > 1 path on a box with fewer GPUs than ranks:
         # ranks share devices round-robin and collectives go through the host.
@@ -791,16 +933,22 @@ def main():
     if world > 1 or (a.sharded and a.exchange == "torch"):
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29517")
+        # torch's own deadline (rendezvous and its collectives), well under the
+        # driver's 600 s and past every stage deadline a rank can spend inside
+        # a torch collective, so the watchdog names the stage first
+        pg_timeout = datetime.timedelta(seconds=PG_TIMEOUT_S)
         if backend == "gloo":
-            dist.init_process_group("gloo", rank=rank, world_size=world)
+            dist.init_process_group("gloo", rank=rank, world_size=world, timeout=pg_timeout)
         else:
-            dist.init_process_group("nccl", device_id=dev, rank=rank, world_size=world)
+            dist.init_process_group("nccl", device_id=dev, rank=rank, world_size=world, timeout=pg_timeout)
 
     import octree_ray_tracing_amd as ort
     from octree_ray_tracing_amd.frame import RcclComm, ShardedFrame, ShardedSteps, slice_row_map
 
     W, H = frame_size(world, a.width, a.height, a.scaling)
+    wd.enter("pool", DEADLINES["pool"])
     nodes, root, tree_nodes, build_s = build_pool_nodes(a.depth, rank, world, dev)
+    wd.enter("setup", DEADLINES["setup"])
     pool = ort.HOctree(nodes, root, a.depth, device=local)
     pool.set_palette(ort.VoxelData().get_colours())
     for kv in a.opt:
@@ -817,8 +965,12 @@ def main():
     # on every rank.  The gloo rehearsal (several ranks per GPU) keeps torch's.
     comm = None
     if sharded and indexed and backend == "nccl" and a.exchange in ("rccl", "gather"):
-        comm = agreed_comm(RcclComm.from_process_group if dist.is_initialized() else (lambda: RcclComm.local(local)),
-                           world, dev, log)
+        wd.enter("comm", DEADLINES["comm"])
+        comm = agreed_comm(world, rank, dev, RcclComm.unique_id, RcclComm.available,
+                           lambda uid: RcclComm(uid, world, rank, local), log)
+        if comm is not None:
+            wd.on_expiry(comm.abort)
+        wd.enter("setup", DEADLINES["setup"])
     exch_mode = "gather" if (comm is not None and a.exchange == "gather") else "all_gather"
     if exch_mode == "gather" and a.shade != "display":
         raise SystemExit("--exchange gather needs --shade display")
@@ -962,6 +1114,34 @@ def main():
                          "per wave; per_view = one launch per view, two_views = both views' rays in one launch "
                          "(W x 2H, planned with och_gpu_plan_batch_tiled)")
         trace_only["tiled"] = tiled
+        # the reference-signature host entry over the reference's ray layout
+        # (och_gpu_trace_batch_image: host rays x + y * W, host records): both
+        # views' rays as one W x 2H image, as the two-view tiled launch above
+        # (whose plan it uses); kernel time from the launch's own events, the
+        # whole call (PCIe both ways) beside it.  Its records must equal the
+        # device path's.
+        host_rays = both.cpu().numpy().reshape(-1, 3)
+        want = (bd.cpu().numpy(), bv.cpu().numpy().view(np.uint32), bt.cpu().numpy().view(np.uint32))
+        img = pool.trace_batch(o_t.cpu().numpy(), host_rays, width=W)
+        kms_img, call_s = [], []
+        for _ in range(5):
+            t0 = time.perf_counter()
+            img = pool.trace_batch(o_t.cpu().numpy(), host_rays, width=W)
+            call_s.append(time.perf_counter() - t0)
+            kms_img.append(pool.last_kernel_ms())
+        same = (np.array_equal(img[0], want[0]) and np.array_equal(img[1], want[1])
+                and np.array_equal(img[2].view(np.uint32), want[2]))
+        k_img = float(np.median(kms_img))
+        trace_only["image"] = {"mrays_s": 2 * n_px / k_img / 1e3, "ms_per_launch": k_img, "rays_per_launch": 2 * n_px,
+                               "call_ms": round(float(np.median(call_s)) * 1e3, 3),
+                               "call_mrays_s": round(2 * n_px / float(np.median(call_s)) / 1e6, 1),
+                               "records_equal_tiled_dev": bool(same),
+                               "path": "och_gpu_trace_batch_image: host rays in the reference's layout (x + y * W), "
+                                       f"both views as one {W}-wide image, traced as 8x8 tiles; ms_per_launch = the "
+                                       "kernel (dispatch-recorded events), call_ms = the whole call including the "
+                                       "host-device copies"}
+        if not same:
+            raise SystemExit("och_gpu_trace_batch_image records differ from och_gpu_trace_batch_tiled_dev's")
         # the arbitrary-order call with both views' rays in one launch: the same
         # launch size as the render's, so the per-ray comparison with it is not
         # set by one launch's latency floor (a lone launch ends on its grazing tiles)
@@ -1163,8 +1343,15 @@ def main():
             for k in range(n):
                 step(k, None, bounce)
 
-    def timed(n, bounce=False, ev=None, marked=False):
+    def timed(n, bounce=False, ev=None, marked=False, stage="window"):
         """n steps between barrier + synchronize; max over ranks of the wall time."""
+        wd.enter(stage, DEADLINES["window"])
+        try:
+            return timed_(n, bounce, ev, marked)
+        finally:
+            wd.enter("setup", DEADLINES["setup"])
+
+    def timed_(n, bounce, ev, marked):
         if marked:
             mark()
         drain()
@@ -1236,8 +1423,10 @@ def main():
             drain()
 
         def checked(label):
+            wd.enter("exchange check", DEADLINES["exchange check"])
             one_frame()
             bad = check_exchange(sfs[0], world, rank, exch_mode != "gather" or rank == 0)
+            wd.enter("setup", DEADLINES["setup"])
             return {"exchange": label, "frames": 1, "slices": world, "mismatches": bad}
         exchange_check = checked(exchange_label())
         if exchange_check["mismatches"] and comm is not None:
@@ -1267,11 +1456,12 @@ def main():
         trace_only["vs_lone_render_per_ray"] = {
             "untiled_per_view": round(trace_only["ms_per_frame"] / n_px / lone, 3),
             "untiled_two_views": round(trace_only["two_views"]["ms_per_launch"] / (2 * n_px) / lone, 3),
-            "tiled_two_views": round(trace_only["tiled"]["two_views"]["ms_per_launch"] / (2 * n_px) / lone, 3)}
+            "tiled_two_views": round(trace_only["tiled"]["two_views"]["ms_per_launch"] / (2 * n_px) / lone, 3),
+            "image_two_views": round(trace_only["image"]["ms_per_launch"] / (2 * n_px) / lone, 3)}
     # warmup, then the timed steps
     warm(a.warmup, events=not a.no_step_events)
     ev = None if a.no_step_events else []
-    elapsed = timed(a.steps, ev=ev, marked=True)
+    elapsed = timed(a.steps, ev=ev, marked=True, stage="window (headline)")
     ev = ev or []
     per_rank_ms = [round(t / a.steps * 1e3, 4) for t in rank_s[-1]]
     last = (a.steps - 1) % len(sfs)
@@ -1298,7 +1488,7 @@ def main():
     sustained = None
     if a.sustain > 0:
         n_s = max(a.steps, int(math.ceil(a.sustain / (elapsed / a.steps))))
-        runs = [timed(n_s) for _ in range(3)]
+        runs = [timed(n_s, stage="window (sustained)") for _ in range(3)]
         vals = [W * H * len(cams) * n_s / r / 1e6 for r in runs]
         sustained = {"value": round(statistics.median(vals), 2), "unit": "Mrays/s", "steps_per_run": n_s,
                      "runs_s": [round(r, 4) for r in runs], "values": [round(v, 2) for v in vals]}
@@ -1310,14 +1500,16 @@ def main():
     exchange_gather = None
     if world > 1 and sharded_steps is not None and exch_mode == "all_gather" and a.shade == "display":
         arm_steps = {False: ShardedSteps(sfs, streams, comm, cams, exchange="gather")}
+        wd.enter("exchange check (gather)", DEADLINES["exchange check"])
         prepare_sharded(1, False, None)()
         drain()
         bad = check_exchange(sfs[0], world, rank, rank == 0)
+        wd.enter("setup", DEADLINES["setup"])
         exchange_gather = {"exchange": "RCCL gather to rank 0 (ncclSend / ncclRecv) on the library's communicator",
                            "check_mismatches": bad}
         if not bad:
             prepare_sharded(a.warmup, False, None)()
-            el_g = timed(a.steps)
+            el_g = timed(a.steps, stage="window (gather)")
             exchange_gather.update({"value": round(total_rays / el_g / 1e6, 2),
                                     "ms_per_step": round(el_g / a.steps * 1e3, 4),
                                     "per_rank_ms_per_step": [round(t / a.steps * 1e3, 4) for t in rank_s[-1]]})
@@ -1337,7 +1529,7 @@ def main():
         if pool.get_option("tile_order") >= 2:
             pool.plan_views(cams, a.row_chunk, rank, world)       # the plan is per cull setting
         warm(a.warmup, events=False)
-        el_off = timed(a.steps)
+        el_off = timed(a.steps, stage="window (cull off)")
         cull_off = {"value": round(total_rays / el_off / 1e6, 2), "ms_per_step": round(el_off / a.steps * 1e3, 4),
                     "note": "same warmup and window, OCH_OPT_CULL = 0: every ray walks from the root"}
         pool.set_option("cull", c_prev)
@@ -1411,7 +1603,7 @@ def main():
             els, kms_ = [], []
             for _ in range(3):
                 bev = []
-                els.append(timed(n, bounce=True, ev=bev))
+                els.append(timed(n, bounce=True, ev=bev, stage="window (config 5)"))
                 kms_.append(float(np.mean([x.elapsed_time(y) for x, y in bev])))
             return statistics.median(els), statistics.median(kms_)
         # the pool's compaction mode (OCH_OPT_BOUNCE_COMPACT, default or --opt)
@@ -1537,6 +1729,7 @@ def main():
     # of one size: the driver's N = 1 line is configs[2]'s 1920x1080 frame.
     scaling_base = None
     if world > 1 and not a.no_scaling_base:
+        wd.enter("scaling base", DEADLINES["scaling base"])
         drain()
         dist.barrier()
         if rank == 0:
@@ -1550,14 +1743,25 @@ def main():
     # resident rays, next to the CPU oracle on the same rays.
     others = None
     if world == 1 and not a.no_other_configs:
+        wd.enter("other configs", DEADLINES["other configs"])
         others = other_configs(a, dev, stream)
 
     cpu, parity = None, None
+    # the other ranks go on to the teardown while rank 0 checks parity
+    wd.enter("cpu leg" if rank == 0 else "teardown",
+             DEADLINES["cpu leg"] + (0 if rank == 0 else DEADLINES["teardown"]))
     if rank == 0 and not a.no_parity:
         cpu, parity = cpu_leg(nodes, root, a.depth, W, H, frames_host, bounce_host,
                               time_it=world == 1 and not a.no_cpu_baseline, budget_s=a.cpu_budget,
                               moving=moving_frames)
 
+    # a HIP error some other call left pending, cleared by a launch (och_discarded_error):
+    # reported once, with the entry that found it
+    from octree_ray_tracing_amd._lib import discarded_error
+    discarded = discarded_error(reset=True)
+    if discarded is not None:
+        log(f"bench rank {rank}: {discarded['count']} pending HIP error(s) cleared before launches; "
+            f"the first: {discarded['what']}")
     if rank == 0:
         if world == 1:
             workload = "configs[2]: 4096^3 depth-12 och_h_octree DAG, 1920x1080 primary rays, 1 MI355X" + (
@@ -1571,7 +1775,7 @@ def main():
             else:
                 workload = f"depth-{a.depth} DAG, {W}x{H} frame row-sharded over {world} MI355X with {how}"
         line = {
-            "metric": "Mrays/sec primary traversal (depth-12 SVO-DAG, raygen+trace+shade per frame)",
+            "metric": METRIC,
             "value": round(value, 2),
             "unit": "Mrays/s",
             "n_gpus": world,
@@ -1630,16 +1834,19 @@ def main():
             **({"extra_windows": extra, "extra_windows_no_events": extra_noev} if extra else {}),
             **({"host_stamps_ns": stamps} if stamps else {}),
             "trace_batch": trace_only,
+            **({"discarded_hip_error": discarded} if discarded else {}),
             "bounce": bounce,
             "other_configs": others,
         }
         print(json.dumps(line), flush=True)
+        wd.enter("teardown", DEADLINES["teardown"])
     if comm is not None:
         torch.cuda.synchronize()
         comm.close()
     pool.close()
     if dist.is_initialized():
         dist.destroy_process_group()
+    wd.done()
 
 
 if __name__ == "__main__":

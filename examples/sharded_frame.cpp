@@ -155,6 +155,13 @@ int main(int argc, char **argv)
         std::fprintf(stderr, "rank %d: %s\n", rank, e.what());
         rc = 1;
     }
+    // A HIP error some earlier call left pending (RCCL's init, say) is cleared
+    // by the next launch and kept: say so once, with where it was found.
+    int stale = 0, n_stale = 0;
+    char where[320] = "";
+    if (och_discarded_error(&stale, &n_stale, where, sizeof where, 1) == OCH_OK && n_stale)
+        std::fprintf(stderr, "rank %d: %d pending HIP error(s) cleared before launches; the first: %s\n", rank,
+                     n_stale, where);
     for (void *p : owned) (void)hipFree(p);
     for (hipStream_t s : streams) (void)hipStreamDestroy(s);
     if (hp.nodes) och_host_pool_free(&hp);

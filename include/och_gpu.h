@@ -96,6 +96,15 @@ typedef struct och_pool_info {
 /* ------------------------------------------------------------ runtime */
 OCH_API int och_abi_version(void);
 OCH_API const char *och_last_error(void);      /* thread-local message of the last failure */
+/* Every kernel launch first clears its thread's pending HIP error: one left by
+ * an earlier HIP call of the thread (another library's, e.g. RCCL's
+ * communicator init) would otherwise be reported as the launch's own.  The
+ * error is kept, not dropped: the first one cleared since the last reset, in
+ * any thread -- its hipError_t in *hip_error (0 = none), the number cleared in
+ * *count, and into what (what_cap bytes, may be NULL) its name and the C-ABI
+ * entry and launcher that found it.  reset != 0 clears the record after
+ * reading.  Any argument may be NULL. */
+OCH_API int och_discarded_error(int *hip_error, int *count, char *what, size_t what_cap, int reset);
 OCH_API int och_device_count(int *count);       /* visible gfx950 devices */
 /* HIP indices of the visible gfx950 devices, in HIP order: up to capacity of
  * them into devices[], their total into *count. */
@@ -232,6 +241,15 @@ OCH_API int och_gpu_trace_batch_tiled_dev(och_gpu_pool *pool, const float *origi
                                           const float *dirs, uint32_t n, uint32_t width,
                                           int32_t *hit_direction, uint32_t *hit_voxel, float *hit_time,
                                           uint32_t *push_count);
+/* och_gpu_trace_batch for a camera's rays in the reference's layout, a
+ * row-major image `width` rays wide (x + y * W, ORT/test_och_h_octree.cpp:135):
+ * host buffers, synchronous, traced as och_gpu_trace_batch_tiled_dev traces
+ * them (8x8 tiles per wave; the plan of och_gpu_plan_batch_tiled when one
+ * exists for this geometry).  Records in the caller's order, bit-identical to
+ * och_gpu_trace_batch. */
+OCH_API int och_gpu_trace_batch_image(och_gpu_pool *pool, const float *origin, int origin_stride,
+                                      const float *dirs, uint32_t n, uint32_t width,
+                                      int32_t *hit_direction, uint32_t *hit_voxel, float *hit_time);
 /* Plan the launch order of tiled batches of n rays `width` wide (block size
  * included in the key): one timed trace of these rays, then
  * costliest tiles first.  Synchronous; a plan stays valid while the rays
@@ -400,6 +418,14 @@ typedef struct och_comm och_comm;
 OCH_API int och_comm_unique_id(uint8_t *id);
 OCH_API int och_comm_create(const uint8_t *id, int n_ranks, int rank, int device, och_comm **out);
 OCH_API int och_comm_destroy(och_comm *comm);
+/* OCH_OK when RCCL can be loaded (no communicator made): lets every rank agree
+ * that all can join before any of them blocks in och_comm_create. */
+OCH_API int och_comm_available(void);
+/* ncclCommAbort, callable from another thread (a watchdog): a collective whose
+ * peer never comes stops blocking its stream.  The handle stays valid for
+ * och_comm_destroy; later calls on it fail.  Aborting one rank does not
+ * unblock the others: each rank's caller aborts its own. */
+OCH_API int och_comm_abort(och_comm *comm);
 OCH_API int och_comm_info(const och_comm *comm, int *n_ranks, int *rank, int *device);
 /* recv = [n_ranks][bytes]: every rank's `bytes` (ncclAllGather), enqueued on stream. */
 OCH_API int och_comm_all_gather(och_comm *comm, const void *send, void *recv, size_t bytes, void *stream);

@@ -73,16 +73,24 @@ public:
         sse_trace(o.x, o.y, o.z, d.x, d.y, d.z, hit_direction, hit_voxel, hit_time);
     }
 
-    // Many rays at once (the per-pixel loop's calls, batched).
+    // Many rays at once (the per-pixel loop's calls, batched).  width > 0: the
+    // rays are a camera's, a row-major image that many rays wide (x + y * W,
+    // ORT/test_och_h_octree.cpp:135), traced 8x8 tiles per wave
+    // (och_gpu_trace_batch_image); same records either way.
     void trace_batch(float3 origin, const std::vector<float3> &dirs, std::vector<direction> &dir_out,
-                     std::vector<uint32_t> &voxel_out, std::vector<float> &t_out) const
+                     std::vector<uint32_t> &voxel_out, std::vector<float> &t_out, uint32_t width = 0) const
     {
         const uint32_t n = static_cast<uint32_t>(dirs.size());
         std::vector<int32_t> d(n);
         voxel_out.resize(n);
         t_out.resize(n);
-        check(och_gpu_trace_batch(pool_, &origin.x, 0, &dirs[0].x, n, d.data(), voxel_out.data(), t_out.data()),
-              "och_gpu_trace_batch");
+        if (width)
+            check(och_gpu_trace_batch_image(pool_, &origin.x, 0, &dirs[0].x, n, width, d.data(), voxel_out.data(),
+                                            t_out.data()),
+                  "och_gpu_trace_batch_image");
+        else
+            check(och_gpu_trace_batch(pool_, &origin.x, 0, &dirs[0].x, n, d.data(), voxel_out.data(), t_out.data()),
+                  "och_gpu_trace_batch");
         dir_out.resize(n);
         for (uint32_t i = 0; i < n; ++i) dir_out[i] = static_cast<direction>(d[i]);
     }

@@ -61,6 +61,7 @@ _u32, _i32, _f32 = C.c_uint32, C.c_int32, C.c_float
 PROTOTYPES = {
     "och_abi_version": (C.c_int, []),
     "och_last_error": (C.c_char_p, []),
+    "och_discarded_error": (C.c_int, [C.POINTER(C.c_int), C.POINTER(C.c_int), C.c_char_p, C.c_size_t, C.c_int]),
     "och_device_count": (C.c_int, [C.POINTER(C.c_int)]),
     "och_device_list": (C.c_int, [_P, C.c_int, C.POINTER(C.c_int)]),
     "och_host_rcp_lut": (C.c_int, [_P, C.POINTER(C.c_int)]),
@@ -83,6 +84,7 @@ PROTOTYPES = {
     "och_gpu_trace": (C.c_int, [_P] + [_f32] * 6 + [C.POINTER(_i32), C.POINTER(_u32), C.POINTER(_f32)]),
     "och_gpu_trace_batch": (C.c_int, [_P, _P, C.c_int, _P, _u32, _P, _P, _P]),
     "och_gpu_trace_batch_dev": (C.c_int, [_P, _P, C.c_int, _P, _u32, _P, _P, _P, _P]),
+    "och_gpu_trace_batch_image": (C.c_int, [_P, _P, C.c_int, _P, _u32, _u32, _P, _P, _P]),
     "och_gpu_trace_batch_tiled_dev": (C.c_int, [_P, _P, C.c_int, _P, _u32, _u32, _P, _P, _P, _P]),
     "och_gpu_plan_batch_tiled": (C.c_int, [_P, _P, C.c_int, _P, _u32, _u32]),
     "och_gpu_trace_bounce_batch_dev": (C.c_int, [_P, _P, C.c_int, _P, _u32, _P, _P, _P, _P, _P, _P, _P]),
@@ -130,6 +132,8 @@ PROTOTYPES = {
     "och_comm_unique_id": (C.c_int, [_P]),
     "och_comm_create": (C.c_int, [_P, C.c_int, C.c_int, C.c_int, C.POINTER(_P)]),
     "och_comm_destroy": (C.c_int, [_P]),
+    "och_comm_available": (C.c_int, []),
+    "och_comm_abort": (C.c_int, [_P]),
     "och_comm_info": (C.c_int, [_P, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int)]),
     "och_comm_all_gather": (C.c_int, [_P, _P, _P, C.c_size_t, _P]),
     "och_comm_gather": (C.c_int, [_P, _P, _P, C.c_size_t, C.c_int, _P]),
@@ -182,6 +186,17 @@ def call(name: str, *args):
         msg = lib.och_last_error()
         raise OchError(r, name, msg.decode() if msg else "")
     return r
+
+
+def discarded_error(reset: bool = False) -> dict | None:
+    """The first pending HIP error a kernel launch found and cleared since the
+    last reset (och_discarded_error), or None: {"hip_error", "count", "what"}."""
+    code, count = C.c_int(), C.c_int()
+    what = C.create_string_buffer(512)
+    call("och_discarded_error", C.byref(code), C.byref(count), what, len(what), int(bool(reset)))
+    if not count.value:
+        return None
+    return {"hip_error": code.value, "count": count.value, "what": what.value.decode(errors="replace")}
 
 
 def exported_symbols() -> list[str]:

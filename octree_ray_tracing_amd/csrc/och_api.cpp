@@ -22,6 +22,23 @@ constexpr uint32_t kIdLimit = 1u << 24;   // packed ids are 24 bits
 
 thread_local std::string g_error;
 
+thread_local const char *t_entry = nullptr;     // outermost C-ABI entry of this thread
+
+// The first pending HIP error a launcher cleared since the last reset, process
+// wide (the frame group issues from one thread per device), and how many.
+struct Discarded {
+    std::mutex m;
+    int code = 0;
+    int count = 0;
+    std::string what;
+};
+
+Discarded &discarded()
+{
+    static Discarded d;
+    return d;
+}
+
 int fail(int status, const char *fmt, ...)
 {
     char buf[512];
@@ -504,6 +521,20 @@ OCH_API int och_abi_version(void) { return OCH_GPU_ABI_VERSION; }
 
 OCH_API const char *och_last_error(void) { return g_error.c_str(); }
 
+OCH_API int och_discarded_error(int *hip_error, int *count, char *what, size_t what_cap, int reset)
+{
+    auto &d = discarded();
+    std::lock_guard<std::mutex> lk(d.m);
+    if (hip_error) *hip_error = d.code;
+    if (count) *count = d.count;
+    if (what && what_cap) snprintf(what, what_cap, "%s", d.what.c_str());
+    if (reset) {
+        d.code = d.count = 0;
+        d.what.clear();
+    }
+    return OCH_OK;
+}
+
 OCH_API int och_device_list(int *devices, int capacity, int *count)
 {
     if (!count || (capacity > 0 && !devices)) return fail(OCH_E_INVALID, "NULL argument");
@@ -646,6 +677,7 @@ OCH_API int och_gpu_pool_info(const och_gpu_pool *p, och_pool_info *info)
 
 OCH_API int och_gpu_pool_update(och_gpu_pool *p, uint32_t first, uint32_t count, const uint32_t *nodes, uint32_t root)
 {
+    OCH_ENTRY();
     if (!p || (count && !nodes)) return fail(OCH_E_INVALID, "pool/nodes is NULL");
     if (p->torn) return fail(OCH_E_INVALID, "pool left half written by a failed och_editor_flush: flush the editor again");
     const uint32_t n_user = p->n_nodes - (uint32_t)p->index_base;
@@ -681,6 +713,31 @@ OCH_API int och_gpu_pool_update(och_gpu_pool *p, uint32_t first, uint32_t count,
 }  // extern "C"
 
 int och::report(int status, const char *msg) { return fail(status, "%s", msg); }
+
+// ------------------------------------------------------------ discarded errors
+
+
+och::EntryScope::EntryScope(const char *name) : prev(t_entry)
+{
+    if (!t_entry) t_entry = name;
+}
+
+och::EntryScope::~EntryScope() { t_entry = prev; }
+
+void och::clear_pending_error(const char *launcher)
+{
+    const hipError_t e = hipGetLastError();
+    if (e == hipSuccess) return;
+    Discarded &d = discarded();
+    std::lock_guard<std::mutex> lk(d.m);
+    if (d.count++ == 0) {
+        char buf[320];
+        snprintf(buf, sizeof buf, "%s (%d) pending at %s, cleared by %s", hipGetErrorName(e), (int)e,
+                 t_entry ? t_entry : "an internal call", launcher);
+        d.code = (int)e;
+        d.what = buf;
+    }
+}
 
 uint64_t och::pool_serial(const och_gpu_pool *p) { return p ? p->serial : 0; }
 void *och::pool_stream(const och_gpu_pool *p) { return p ? static_cast<void *>(p->stream()) : nullptr; }
@@ -1017,6 +1074,7 @@ OCH_API int och_gpu_trace_batch_dev(och_gpu_pool *p, const float *origin, int or
                                     uint32_t n, int32_t *hit_dir, uint32_t *hit_voxel, float *hit_time,
                                     uint32_t *push_count)
 {
+    OCH_ENTRY();
     if (!p || (n && (!origin || !dirs || !hit_dir || !hit_voxel || !hit_time)))
         return fail(OCH_E_INVALID, "NULL argument");
     if (origin_stride != 0 && origin_stride != 3) return fail(OCH_E_INVALID, "origin_stride must be 0 or 3");
@@ -1035,6 +1093,7 @@ OCH_API int och_gpu_trace_bounce_batch_dev(och_gpu_pool *p, const float *origin,
                                            int32_t *bounce_dir, uint32_t *bounce_voxel, float *bounce_time,
                                            uint32_t *push_count)
 {
+    OCH_ENTRY();
     if (!p || (n && (!origin || !dirs || !hit_dir || !hit_voxel || !hit_time || !bounce_dir || !bounce_voxel ||
                      !bounce_time)))
         return fail(OCH_E_INVALID, "NULL argument");
@@ -1077,6 +1136,7 @@ OCH_API int och_gpu_trace_batch_tiled_dev(och_gpu_pool *p, const float *origin, 
                                           uint32_t n, uint32_t width, int32_t *hit_dir, uint32_t *hit_voxel,
                                           float *hit_time, uint32_t *push_count)
 {
+    OCH_ENTRY();
     if (int st = tiled_args(p, origin, origin_stride, dirs, n, width)) return st;
     if (n && (!hit_dir || !hit_voxel || !hit_time)) return fail(OCH_E_INVALID, "NULL argument");
     DeviceGuard g(p->device);
@@ -1099,6 +1159,7 @@ OCH_API int och_gpu_trace_batch_tiled_dev(och_gpu_pool *p, const float *origin, 
 OCH_API int och_gpu_plan_batch_tiled(och_gpu_pool *p, const float *origin, int origin_stride, const float *dirs,
                                      uint32_t n, uint32_t width)
 {
+    OCH_ENTRY();
     if (int st = tiled_args(p, origin, origin_stride, dirs, n, width)) return st;
     if (n == 0) return OCH_OK;
     DeviceGuard g(p->device);
@@ -1139,8 +1200,13 @@ OCH_API int och_gpu_plan_batch_tiled(och_gpu_pool *p, const float *origin, int o
     return OCH_OK;
 }
 
-OCH_API int och_gpu_trace_batch(och_gpu_pool *p, const float *origin, int origin_stride, const float *dirs,
-                                uint32_t n, int32_t *hit_dir, uint32_t *hit_voxel, float *hit_time)
+namespace {
+
+// Host rays in, host records out, synchronous: the rays staged in the pool's
+// scratch, traced by the array kernel (width 0) or as a `width`-wide image of
+// 8x8 tiles (och_gpu_trace_batch_tiled_dev), the records copied back.
+int host_batch(och_gpu_pool *p, const float *origin, int origin_stride, const float *dirs, uint32_t n, uint32_t width,
+               int32_t *hit_dir, uint32_t *hit_voxel, float *hit_time)
 {
     if (!p || (n && (!origin || !dirs || !hit_dir || !hit_voxel || !hit_time)))
         return fail(OCH_E_INVALID, "NULL argument");
@@ -1162,7 +1228,8 @@ OCH_API int och_gpu_trace_batch(och_gpu_pool *p, const float *origin, int origin
     hipStream_t s = p->stream();
     OCH_HIP(hipMemcpyAsync(d_orig, origin, n_orig * 4, hipMemcpyHostToDevice, s));
     OCH_HIP(hipMemcpyAsync(d_dirs, dirs, (size_t)n * 12, hipMemcpyHostToDevice, s));
-    st = och_gpu_trace_batch_dev(p, d_orig, origin_stride, d_dirs, n, d_dir, d_vox, d_t, nullptr);
+    st = width ? och_gpu_trace_batch_tiled_dev(p, d_orig, origin_stride, d_dirs, n, width, d_dir, d_vox, d_t, nullptr)
+               : och_gpu_trace_batch_dev(p, d_orig, origin_stride, d_dirs, n, d_dir, d_vox, d_t, nullptr);
     if (st != OCH_OK) return st;
     OCH_HIP(hipMemcpyAsync(hit_dir, d_dir, (size_t)n * 4, hipMemcpyDeviceToHost, s));
     OCH_HIP(hipMemcpyAsync(hit_voxel, d_vox, (size_t)n * 4, hipMemcpyDeviceToHost, s));
@@ -1171,9 +1238,28 @@ OCH_API int och_gpu_trace_batch(och_gpu_pool *p, const float *origin, int origin
     return OCH_OK;
 }
 
+}  // namespace
+
+OCH_API int och_gpu_trace_batch(och_gpu_pool *p, const float *origin, int origin_stride, const float *dirs,
+                                uint32_t n, int32_t *hit_dir, uint32_t *hit_voxel, float *hit_time)
+{
+    OCH_ENTRY();
+    return host_batch(p, origin, origin_stride, dirs, n, 0, hit_dir, hit_voxel, hit_time);
+}
+
+OCH_API int och_gpu_trace_batch_image(och_gpu_pool *p, const float *origin, int origin_stride, const float *dirs,
+                                      uint32_t n, uint32_t width, int32_t *hit_dir, uint32_t *hit_voxel,
+                                      float *hit_time)
+{
+    OCH_ENTRY();
+    if (width == 0) return fail(OCH_E_INVALID, "width must be positive");
+    return host_batch(p, origin, origin_stride, dirs, n, width, hit_dir, hit_voxel, hit_time);
+}
+
 OCH_API int och_gpu_trace(och_gpu_pool *p, float ox, float oy, float oz, float dx, float dy, float dz,
                           int32_t *hit_direction, uint32_t *hit_voxel, float *hit_time)
 {
+    OCH_ENTRY();
     if (!hit_direction || !hit_voxel || !hit_time) return fail(OCH_E_INVALID, "NULL output");
     const float o[3] = {ox, oy, oz}, d[3] = {dx, dy, dz};
     return och_gpu_trace_batch(p, o, 0, d, 1, hit_direction, hit_voxel, hit_time);
@@ -1210,6 +1296,7 @@ OCH_API int och_camera_setup(float px, float py, float pz, float yaw, float pitc
 
 OCH_API int och_gpu_raygen_dev(och_gpu_pool *p, const och_camera *cam, float *dirs)
 {
+    OCH_ENTRY();
     if (!p || !cam || !dirs) return fail(OCH_E_INVALID, "NULL argument");
     DeviceGuard g(p->device);
     OCH_HIP(och::launch_raygen(*cam, dirs, p->stream()));
@@ -1317,6 +1404,7 @@ void plan_shape(std::vector<uint32_t> &order, int mode)
 OCH_API int och_gpu_plan_views(och_gpu_pool *p, const och_camera *cams, int n_views, int row_chunk, int shard,
                                int n_shards)
 {
+    OCH_ENTRY();
     if (!p || !cams) return fail(OCH_E_INVALID, "NULL argument");
     if (n_views < 1 || n_views > OCH_MAX_VIEWS || row_chunk <= 0 || n_shards <= 0 || shard < 0 || shard >= n_shards)
         return fail(OCH_E_INVALID, "bad plan arguments");
@@ -1491,6 +1579,7 @@ OCH_API int och_gpu_slice_rows(const och_gpu_pool *p, int height, int row_chunk,
 
 OCH_API int och_gpu_chunk_costs(och_gpu_pool *p, const och_camera *cams, int n_views, int row_chunk, float *costs)
 {
+    OCH_ENTRY();
     if (!p || !cams || !costs || row_chunk <= 0) return fail(OCH_E_INVALID, "bad chunk-cost arguments");
     if (n_views < 1 || n_views > OCH_MAX_VIEWS) return fail(OCH_E_INVALID, "n_views %d outside 1..%d", n_views, OCH_MAX_VIEWS);
     for (int v = 0; v < n_views; ++v)
@@ -1587,12 +1676,14 @@ OCH_API int och_deal_chunks(const float *costs, int n_chunks, int n_shards, cons
 OCH_API int och_gpu_render_views_dev(och_gpu_pool *p, const och_camera *cams, int n_views, uint32_t *rgba_slices,
                                      int row_chunk, int shard, int n_shards)
 {
+    OCH_ENTRY();
     return render_views(p, cams, n_views, rgba_slices, row_chunk, shard, n_shards, false);
 }
 
 OCH_API int och_gpu_render_bounce_views_dev(och_gpu_pool *p, const och_camera *cams, int n_views, uint32_t *rgba_slices,
                                             int row_chunk, int shard, int n_shards)
 {
+    OCH_ENTRY();
     return render_views(p, cams, n_views, rgba_slices, row_chunk, shard, n_shards, true);
 }
 
@@ -1600,6 +1691,7 @@ OCH_API int och_gpu_render_steps_dev(och_gpu_pool *p, const och_camera *cams, in
                                      void *const *streams, uint32_t *const *frames, int n_buffers,
                                      void *const *start_events, void *const *stop_events, int row_chunk, int bounce)
 {
+    OCH_ENTRY();
     if (!p || !cams || !streams || !frames) return fail(OCH_E_INVALID, "NULL argument");
     if (n_steps < 0 || n_buffers < 1) return fail(OCH_E_INVALID, "n_steps %d / n_buffers %d", n_steps, n_buffers);
     if ((start_events == nullptr) != (stop_events == nullptr))
@@ -1634,6 +1726,7 @@ OCH_API int och_gpu_render_sharded_steps_dev(och_gpu_pool *p, och_comm *comm, co
                                              void *const *start_events, void *const *stop_events, int row_chunk,
                                              int bounce, int exchange)
 {
+    OCH_ENTRY();
     if (!p || !comm || !cams || !streams || !slices) return fail(OCH_E_INVALID, "NULL argument");
     if (n_steps < 0 || n_buffers < 1) return fail(OCH_E_INVALID, "n_steps %d / n_buffers %d", n_steps, n_buffers);
     if (n_views < 1 || n_views > OCH_MAX_VIEWS || row_chunk <= 0) return fail(OCH_E_INVALID, "bad views / row_chunk");
@@ -1691,8 +1784,12 @@ OCH_API int och_gpu_render_sharded_steps_dev(och_gpu_pool *p, och_comm *comm, co
     p->next_ev_start = p->next_ev_stop = nullptr;
     p->ext_stream = prev;
     p->use_ext = had_ext;
-    if (st != OCH_OK && (issued || n_ranks > 1)) {
-        // the peers' collectives of this window can no longer all complete
+    if (st != OCH_OK && issued) {
+        // The peers' collectives of this window can no longer all complete.
+        // Aborting here does not unblock the peers: their callers must abort
+        // theirs (bench.py's watchdog, or the process exiting).  A failure
+        // before this rank queued any collective leaves the communicator as
+        // it was (every rank failing alike keeps a consistent one).
         const std::string msg = och_last_error();
         och::comm_abort(comm);
         return fail(st, "%s (communicator aborted: the window stopped part way)", msg.c_str());
@@ -1703,6 +1800,7 @@ OCH_API int och_gpu_render_sharded_steps_dev(och_gpu_pool *p, och_comm *comm, co
 OCH_API int och_gpu_render_codes_views_dev(och_gpu_pool *p, const och_camera *cams, int n_views, uint8_t *code_slices,
                                            int row_chunk, int shard, int n_shards, int bounce)
 {
+    OCH_ENTRY();
     if (!code_slices) return fail(OCH_E_INVALID, "NULL argument");
     return render_views(p, cams, n_views, nullptr, row_chunk, shard, n_shards, bounce != 0, code_slices);
 }
@@ -1710,6 +1808,7 @@ OCH_API int och_gpu_render_codes_views_dev(och_gpu_pool *p, const och_camera *ca
 OCH_API int och_gpu_shade_unshard_views_dev(och_gpu_pool *p, const uint8_t *gathered, uint32_t *frames, int width,
                                             int height, int row_chunk, int n_shards, int n_views)
 {
+    OCH_ENTRY();
     if (!p || !gathered || !frames || width <= 0 || height <= 0 || row_chunk <= 0 || n_shards <= 0 || n_views < 1)
         return fail(OCH_E_INVALID, "bad unshard arguments");
     if (!p->d_code_table)
@@ -1724,6 +1823,7 @@ OCH_API int och_gpu_shade_unshard_views_dev(och_gpu_pool *p, const uint8_t *gath
 OCH_API int och_gpu_render_dev(och_gpu_pool *p, const och_camera *cam, uint32_t *rgba_slice, int row_chunk, int shard,
                                int n_shards)
 {
+    OCH_ENTRY();
     if (!cam) return fail(OCH_E_INVALID, "NULL camera");
     return och_gpu_render_views_dev(p, cam, 1, rgba_slice, row_chunk, shard, n_shards);
 }
@@ -1731,6 +1831,7 @@ OCH_API int och_gpu_render_dev(och_gpu_pool *p, const och_camera *cam, uint32_t 
 OCH_API int och_gpu_unshard_views_dev(och_gpu_pool *p, const uint32_t *gathered, uint32_t *frames, int width,
                                       int height, int row_chunk, int n_shards, int n_views)
 {
+    OCH_ENTRY();
     if (!p || !gathered || !frames || width <= 0 || height <= 0 || row_chunk <= 0 || n_shards <= 0 || n_views < 1)
         return fail(OCH_E_INVALID, "bad unshard arguments");
     DeviceGuard g(p->device);
@@ -1743,11 +1844,13 @@ OCH_API int och_gpu_unshard_views_dev(och_gpu_pool *p, const uint32_t *gathered,
 OCH_API int och_gpu_unshard_dev(och_gpu_pool *p, const uint32_t *gathered, uint32_t *frame, int width, int height,
                                 int row_chunk, int n_shards)
 {
+    OCH_ENTRY();
     return och_gpu_unshard_views_dev(p, gathered, frame, width, height, row_chunk, n_shards, 1);
 }
 
 OCH_API int och_gpu_render(och_gpu_pool *p, const och_camera *cam, uint32_t *rgba)
 {
+    OCH_ENTRY();
     if (!p || !cam || !rgba) return fail(OCH_E_INVALID, "NULL argument");
     DeviceGuard g(p->device);
     const size_t bytes = (size_t)cam->width * cam->height * 4;

@@ -200,6 +200,23 @@ OCH_API int och_comm_create(const uint8_t *id, int n_ranks, int rank, int device
     return OCH_OK;
 }
 
+OCH_API int och_comm_available(void)
+{
+    const och::Rccl &R = och::rccl();
+    return R.ok ? OCH_OK : comm_fail(OCH_E_NODEV, R.error);
+}
+
+// For a watchdog on another thread: a collective that never completes (a peer
+// that died or never issued its side) keeps its stream, and the host waiting
+// on it, blocked; ncclCommAbort makes RCCL stop waiting.  The handle stays
+// valid for och_comm_destroy; every later call on it fails.
+OCH_API int och_comm_abort(och_comm *c)
+{
+    if (!c) return comm_fail(OCH_E_INVALID, "NULL communicator");
+    och::comm_abort(c);
+    return OCH_OK;
+}
+
 OCH_API int och_comm_destroy(och_comm *c)
 {
     if (!c) return OCH_OK;

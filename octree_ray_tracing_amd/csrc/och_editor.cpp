@@ -458,6 +458,7 @@ OCH_API int och_editor_nodes(const och_editor *e, const uint32_t **nodes, uint32
 
 OCH_API int och_editor_flush(och_editor *e, och_gpu_pool *pool)
 {
+    OCH_ENTRY();
     if (!e || !pool) return OCH_E_INVALID;
     och_pool_info pi;
     int st = och_gpu_pool_info(pool, &pi);

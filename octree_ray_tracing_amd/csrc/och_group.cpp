@@ -447,6 +447,7 @@ OCH_API int och_frame_group_set_option(och_frame_group *g, int option, int value
 
 OCH_API int och_frame_group_plan(och_frame_group *g, const och_camera *cams, int n_views, int row_chunk)
 {
+    OCH_ENTRY();
     if (!g || !cams || row_chunk < 1 || n_views < 1) return group_fail(OCH_E_INVALID, "bad plan arguments");
     if (g->broken) return group_fail(OCH_E_HIP, "frame group unusable after a failed frame (communicators aborted)");
     if (int st = sync_all(g)) return st;     // frames in flight may read the deal and the plans
@@ -478,12 +479,14 @@ OCH_API int och_frame_group_plan(och_frame_group *g, const och_camera *cams, int
 
 OCH_API int och_frame_group_render(och_frame_group *g, const och_camera *cams, int n_views, int row_chunk, int bounce)
 {
+    OCH_ENTRY();
     return render_steps(g, cams, n_views, 1, 1, row_chunk, bounce);
 }
 
 OCH_API int och_frame_group_render_steps(och_frame_group *g, const och_camera *cams, int n_views, int n_steps,
                                          int n_buffers, int row_chunk, int bounce)
 {
+    OCH_ENTRY();
     return render_steps(g, cams, n_views, n_steps, n_buffers, row_chunk, bounce);
 }
 

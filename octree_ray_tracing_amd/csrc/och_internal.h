@@ -77,6 +77,22 @@ bool occupied_box(const uint32_t *nodes, uint32_t n_nodes, uint32_t root, int de
 // report: record `msg` as och_last_error's text and return status.
 int report(int status, const char *msg);
 
+// Launch hygiene (och_kernels.hip): a launcher clears the thread's pending HIP
+// error before it launches, because hipGetLastError() after the launch also
+// returns an error that an earlier HIP call of the thread left behind (another
+// library's -- RCCL's communicator init, say) and would fail a correct launch.
+// What it clears is kept, not dropped: the first such error since the last
+// reset, the C-ABI entry the thread was in (EntryScope) and the launcher, read
+// by och_discarded_error.
+void clear_pending_error(const char *launcher);
+// The outermost C-ABI entry of this thread, by name, while it runs (OCH_ENTRY).
+struct EntryScope {
+    const char *prev;
+    explicit EntryScope(const char *name);
+    ~EntryScope();
+};
+#define OCH_ENTRY() const och::EntryScope och_entry_scope_(__func__)
+
 int pool_drain(och_gpu_pool *pool);
 int pool_write_slots(och_gpu_pool *pool, uint32_t first, uint32_t count, const uint32_t *raw,
                      const uint32_t *packed, bool full);

@@ -32,14 +32,15 @@
 // Every launch here clears the thread's last HIP error first and reports
 // hipGetLastError() after it: that call also returns an error left behind by
 // any earlier HIP call of the thread (another library's -- RCCL's communicator
-// init, say), which is not this launch's.
+// init, say), which is not this launch's.  The cleared error is kept for
+// och_discarded_error (clear_pending_error, och_api.cpp).
 // A traversal launch, timed by the dispatch itself when the schedule carries
 // events (Schedule::ev_start / ev_stop, OCH_OPT_TIMING): hipExtLaunchKernel
 // takes the kernel's own start and end times, with no packets of its own
 // between two launches of a stream.
 #define OCH_LAUNCH_TIMED(sc, kernel, grid, block, lds, stream, ...)                                                   \
     do {                                                                                                             \
-        (void)hipGetLastError();                                                                                     \
+        clear_pending_error(__func__);                                                                               \
         if ((sc).ev_start || (sc).ev_stop)                                                                           \
             hipExtLaunchKernelGGL(kernel, grid, block, (uint32_t)(lds), stream, (sc).ev_start, (sc).ev_stop, 0u,     \
                                   __VA_ARGS__);                                                                      \
@@ -1453,7 +1454,7 @@ hipError_t launch_trace_batch_tiled(const DevPool &p, const float *origin, int o
 hipError_t launch_raygen(const och_camera &cam, float *dirs, hipStream_t stream)
 {
     const dim3 grid((cam.width + 15) / 16, (cam.height + 15) / 16);
-    (void)hipGetLastError();
+    clear_pending_error(__func__);
     hipLaunchKernelGGL(k_raygen, grid, dim3(256), 0, stream, cam, dirs);
     return hipGetLastError();
 }
@@ -1491,13 +1492,13 @@ hipError_t launch_shade_unshard(const uint8_t *gathered, uint32_t *frames, const
     const bool vec4 = width % 4 == 0 && ((uintptr_t)gathered & 3u) == 0 && ((uintptr_t)frames & 15u) == 0;
     if (vec4) {
         const dim3 grid((width / 4 + 255) / 256, height, n_views);
-        (void)hipGetLastError();
+        clear_pending_error(__func__);
         hipLaunchKernelGGL(k_shade_unshard4, grid, dim3(256), 0, stream, gathered, frames, table, width, height,
                            row_chunk, n_shards, slice_rows, n_views, owner);
         return hipGetLastError();
     }
     const dim3 grid((width + 255) / 256, height, n_views);
-    (void)hipGetLastError();
+    clear_pending_error(__func__);
     hipLaunchKernelGGL(k_shade_unshard, grid, dim3(256), 0, stream, gathered, frames, table, width, height, row_chunk,
                        n_shards, slice_rows, n_views, owner);
     return hipGetLastError();
@@ -1524,7 +1525,7 @@ hipError_t launch_scatter_slots(const uint32_t *ids, const uint32_t *raw, const 
                                 uint32_t *d_raw, uint32_t *d_packed, hipStream_t stream)
 {
     if (count == 0) return hipSuccess;
-    (void)hipGetLastError();
+    clear_pending_error(__func__);
     hipLaunchKernelGGL(k_scatter_slots, dim3((count * 8u + 255u) / 256u), dim3(256), 0, stream, ids, raw, packed, count,
                        d_raw, d_packed);
     return hipGetLastError();
@@ -1534,7 +1535,7 @@ hipError_t launch_unshard(const uint32_t *gathered, uint32_t *frames, int width,
                           int n_shards, int slice_rows, int n_views, const int32_t *owner, hipStream_t stream)
 {
     const dim3 grid((width + 255) / 256, height, n_views);
-    (void)hipGetLastError();
+    clear_pending_error(__func__);
     hipLaunchKernelGGL(k_unshard, grid, dim3(256), 0, stream, gathered, frames, width, height, row_chunk, n_shards,
                        slice_rows, n_views, owner);
     return hipGetLastError();

@@ -118,6 +118,22 @@ class RcclComm:
              C.c_void_p(recv.data_ptr() if recv is not None else 0), send.numel() * send.element_size(), int(root),
              C.c_void_p(stream.cuda_stream))
 
+    @staticmethod
+    def available() -> bool:
+        """RCCL can be loaded here (och_comm_available; no communicator made)."""
+        try:
+            call("och_comm_available")
+            return True
+        except Exception:
+            return False
+
+    def abort(self):
+        """ncclCommAbort (och_comm_abort), safe from another thread: this rank's
+        collectives stop waiting for peers that never come.  close() still frees
+        the handle."""
+        if getattr(self, "_h", None) and self._h.value:
+            call("och_comm_abort", self._h)
+
     def close(self):
         if getattr(self, "_h", None) and self._h.value:
             call("och_comm_destroy", self._h)

@@ -211,15 +211,21 @@ class GpuPool:
              C.byref(d), C.byref(v), C.byref(t))
         return Direction(d.value), v.value, t.value
 
-    def trace_batch(self, origins, dirs):
-        """Host arrays in, host arrays out (synchronous).  origins (3,) or (n,3)."""
+    def trace_batch(self, origins, dirs, width: int | None = None):
+        """Host arrays in, host arrays out (synchronous).  origins (3,) or (n,3).
+        width: the rays are a row-major image that many rays wide (a camera's
+        rays, x + y * W): traced 8x8 tiles per wave (och_gpu_trace_batch_image)."""
         dirs = np.ascontiguousarray(dirs, np.float32).reshape(-1, 3)
         origins = np.ascontiguousarray(origins, np.float32)
         stride = 0 if origins.size == 3 else 3
         n = dirs.shape[0]
         hd, hv, ht = np.empty(n, np.int32), np.empty(n, np.uint32), np.empty(n, np.float32)
-        call("och_gpu_trace_batch", self._h, _np_ptr(origins), stride, _np_ptr(dirs), n,
-             _np_ptr(hd), _np_ptr(hv), _np_ptr(ht))
+        if width:
+            call("och_gpu_trace_batch_image", self._h, _np_ptr(origins), stride, _np_ptr(dirs), n, int(width),
+                 _np_ptr(hd), _np_ptr(hv), _np_ptr(ht))
+        else:
+            call("och_gpu_trace_batch", self._h, _np_ptr(origins), stride, _np_ptr(dirs), n,
+                 _np_ptr(hd), _np_ptr(hv), _np_ptr(ht))
         return hd, hv, ht
 
     def trace_batch_dev(self, origins, dirs, hit_dir, hit_voxel, hit_time, push=None, n=None):

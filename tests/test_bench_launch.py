@@ -112,35 +112,132 @@ class _FakeComm:
         _FakeComm.closed = True
 
 
-def _comm_worker(rank, world, port, fail_rank, q):
+def _comm_worker(rank, world, port, fail, q):
+    """fail = (step, rank): which agreement step fails on which rank."""
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
+    step, bad_rank = fail
+    calls = []
 
-    def make():
-        if rank == fail_rank:
+    def unique_id():
+        calls.append("id")
+        if step == "id" and rank == bad_rank:
+            raise RuntimeError("ncclGetUniqueId failed (test)")
+        return bytes(range(128))
+
+    def available():
+        calls.append("available")
+        return not (step == "available" and rank == bad_rank)
+
+    def create(uid):
+        calls.append("create")
+        assert uid == bytes(range(128))               # rank 0's id reached every rank
+        if step == "create" and rank == bad_rank:
             raise RuntimeError("ncclCommInitRank failed (test)")
         return _FakeComm()
-    comm = bench.agreed_comm(make, world, torch.device("cpu"), log=lambda *a: None)
-    q.put((rank, comm is not None, _FakeComm.closed))
+    comm = bench.agreed_comm(world, rank, torch.device("cpu"), unique_id, available, create, log=lambda *a: None)
+    q.put((rank, comm is not None, _FakeComm.closed, tuple(calls)))
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("fail_rank", [-1, 1])
-def test_agreed_comm_gloo_world2(fail_rank):
-    """The library communicator is used only if every rank made one: when rank 1
-    fails, rank 0 closes its own and both fall back together."""
+@pytest.mark.parametrize("fail", [("none", -1), ("id", 0), ("available", 1), ("create", 1), ("create", 0)])
+def test_agreed_comm_gloo_world2(fail):
+    """The library communicator is used only if every rank made one, and no
+    rank enters a collective step the others skip: rank 0's failed id travels
+    with the id broadcast (no rank calls ncclCommInitRank), a rank that cannot
+    load RCCL is known before anyone joins, and a failed join makes the ranks
+    that joined close theirs -- all fall back together."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    port = 33700 + os.getpid() % 1000 + 5 * (fail_rank + 1)
-    procs = [ctx.Process(target=_comm_worker, args=(r, 2, port, fail_rank, q)) for r in range(2)]
+    port = 33700 + os.getpid() % 1000 + 11 * ["none", "id", "available", "create"].index(fail[0]) + fail[1] + 1
+    procs = [ctx.Process(target=_comm_worker, args=(r, 2, port, fail, q)) for r in range(2)]
     for p in procs:
         p.start()
-    got = dict((r, (has, closed)) for r, has, closed in (q.get(timeout=120) for _ in range(2)))
+    got = {r: (has, closed, calls) for r, has, closed, calls in (q.get(timeout=120) for _ in range(2))}
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    if fail_rank < 0:
-        assert got == {0: (True, False), 1: (True, False)}
+    step, bad = fail
+    if step == "none":
+        assert got == {0: (True, False, ("id", "create")), 1: (True, False, ("available", "create"))}
+    elif step in ("id", "available"):
+        # nobody joins: no rank is left inside ncclCommInitRank
+        assert all(not has and "create" not in calls for has, _, calls in got.values())
     else:
-        assert got == {0: (False, True), 1: (False, False)}
+        good = 1 - bad
+        assert got[bad][:2] == (False, False) and got[good][:2] == (False, True)
+
+
+def test_watchdog_in_process():
+    """A stage past its deadline: the abort hooks run, one JSON line names the
+    stage, the exit status is 3; a stage ended in time never fires."""
+    import io
+    import json
+    import threading
+    out, exited, aborted = io.StringIO(), [], []
+    done = threading.Event()
+
+    def fake_exit(code):
+        exited.append(code)
+        done.set()
+    wd = bench.Watchdog(0, 8, poll_s=0.02, exit_fn=fake_exit, out=out)
+    wd.on_expiry(lambda: aborted.append(1))
+    wd.enter("window (headline)", 0.1)
+    assert done.wait(10)
+    line = json.loads(out.getvalue().strip().splitlines()[-1])
+    assert exited == [3] and aborted == [1]
+    assert line["stage"] == "window (headline)" and line["value"] is None and line["n_gpus"] == 8
+    assert line["communicators_aborted"] == 1 and "deadline" in line["error"]
+    wd2 = bench.Watchdog(1, 2, poll_s=0.02, exit_fn=fake_exit, out=io.StringIO())
+    wd2.enter("setup", 0.2)
+    wd2.done()
+    import time
+    time.sleep(0.5)
+    assert exited == [3]
+
+
+_WITHHOLD = r"""
+import os, sys, time, datetime
+from types import SimpleNamespace
+sys.path.insert(0, {root!r})
+import torch, torch.distributed as dist
+import bench
+rank = int(sys.argv[1])
+dist.init_process_group("gloo", rank=rank, world_size=2, init_method="tcp://127.0.0.1:{port}",
+                        timeout=datetime.timedelta(seconds=120))
+wd = bench.Watchdog(rank, 2, poll_s=0.05)
+wd.enter("exchange check", {deadline} if rank == 0 else 120)
+sl = torch.zeros((2, 4, 8), dtype=torch.uint8)
+frame = SimpleNamespace(slice=sl, gathered=torch.stack([sl, sl]))
+if rank == 1:
+    time.sleep(60)                      # withholds its side of the collective
+bad = bench.check_exchange(frame, 2, rank, True)
+print("returned", bad, flush=True)
+"""
+
+
+def test_watchdog_names_stage_when_a_rank_withholds_gloo_world2():
+    """Two gloo ranks: rank 1 never joins the exchange check's collective.
+    Rank 0 exits with status 3 within its deadline and prints one JSON line
+    naming the stage, instead of waiting out torch's timeout (or the driver's)."""
+    import json
+    import time
+    port = 35100 + os.getpid() % 1000
+    code = _WITHHOLD.format(root=str(ROOT), port=port, deadline=4)
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r1 = subprocess.Popen([sys.executable, "-c", code, "1"], env=env, stdout=subprocess.PIPE,
+                          stderr=subprocess.PIPE, text=True)
+    try:
+        t0 = time.monotonic()
+        r0 = subprocess.run([sys.executable, "-c", code, "0"], env=env, capture_output=True, text=True, timeout=100)
+        took = time.monotonic() - t0
+    finally:
+        r1.kill()
+        r1.communicate()
+    assert r0.returncode == bench.Watchdog.EXIT, r0.stderr[-2000:]
+    assert "returned" not in r0.stdout
+    line = json.loads(r0.stdout.strip().splitlines()[-1])
+    assert line["stage"] == "exchange check" and line["rank"] == 0 and line["value"] is None
+    assert "exchange check" in r0.stderr
+    assert took < 60                                    # the deadline (4 s) plus start-up, not torch's 120 s

@@ -252,18 +252,39 @@ def test_stale_hip_error_is_not_a_launch_failure(ort, O, gpu_device):
         h.hipSetDevice.argtypes = [ctypes.c_int]
 
     def spoil():
-        for h in hips:
-            assert h.hipSetDevice(1 << 20) != 0          # an invalid ordinal: the thread's last error is set
+        codes = {h.hipSetDevice(1 << 20) for h in hips}  # an invalid ordinal: the thread's last error is set
+        assert 0 not in codes
+        return codes
+    from octree_ray_tracing_amd._lib import discarded_error
     cam = ort.camera((1.5, 1.5, 1.5), 0.3, -0.3, 1.25, 64, 36)
     want = pool.render(cam)
-    for _ in range(2):
-        spoil()
+    discarded_error(reset=True)
+    assert discarded_error() is None
+    for k in range(2):
+        codes = spoil()
         assert np.array_equal(pool.render(cam), want)
+        # the cleared error is kept as evidence: its code, the C-ABI entry that found it
+        got = discarded_error()
+        assert got is not None and got["hip_error"] in codes and got["count"] == k + 1
+        assert "och_gpu_render" in got["what"] and "launch" in got["what"]
     o = np.tile(ORIGIN, (256, 1))
     d = np.random.default_rng(3).uniform(-1, 1, (256, 3)).astype(np.float32)
     ref = gpu_trace_dev(pool, o, d)
+    dev = torch.device("cuda", 0)
+    o_t = torch.from_numpy(np.ascontiguousarray(o, np.float32).reshape(-1)).to(dev)
+    d_t = torch.from_numpy(d.reshape(-1)).to(dev)
+    out = [torch.empty(256, dtype=t, device=dev) for t in (torch.int32, torch.int32, torch.float32)]
+    torch.cuda.synchronize()
+    discarded_error(reset=True)
     spoil()
-    assert_same(gpu_trace_dev(pool, o, d), ref)
+    pool.trace_batch_dev(o_t, d_t, *out, n=256)          # the launch right after the failed call
+    torch.cuda.synchronize()
+    assert np.array_equal(out[0].cpu().numpy(), ref["dir"])
+    assert np.array_equal(out[1].cpu().numpy().view(np.uint32), ref["voxel"])
+    assert np.array_equal(out[2].cpu().numpy().view(np.uint32), ref["t"].view(np.uint32))
+    got = discarded_error(reset=True)
+    assert got is not None and "och_gpu_trace_batch_dev" in got["what"]
+    assert discarded_error() is None
     pool.close()
 
 

@@ -99,3 +99,31 @@ def test_tiled_planned_order(ort, O, gpu_device):
         assert_same(tiled_dev(pool, ORIGIN, rays, width, want_push=False), ref, push=False)
         assert_same(gpu_trace_dev(pool, ORIGIN, rays), ref)
     pool.close()
+
+
+def test_trace_batch_image_host_entry(ort, O, gpu_device):
+    """och_gpu_trace_batch_image: host rays in the reference's camera layout
+    (x + y * W, ORT/test_och_h_octree.cpp:135), host records out, traced as
+    8x8 tiles -- the oracle's records, and och_gpu_trace_batch's, bit for bit;
+    per-ray origins and a width that does not divide the batch too."""
+    tree = ort.build_terrain(10, use_gpu=True)
+    pool = ort.HOctree(tree.nodes, tree.root, 10, device=0)
+    ref_pool = O.OraclePool(tree.nodes, tree.root, 10, 1)
+    for pitch in (0.0, -0.6):
+        rays = O.raygen(0.3, pitch, 1.25, 1920, 1080)
+        ref = O.trace_batch(ref_pool, O.Rcp(None), ORIGIN, rays, nthreads=16)
+        for width in (1920, 333):
+            hd, hv, ht = pool.trace_batch(ORIGIN, rays, width=width)
+            assert_same({"dir": hd, "voxel": hv, "t": ht.view(np.uint32)}, ref, push=False)
+        hd, hv, ht = pool.trace_batch(ORIGIN, rays)
+        assert_same({"dir": hd, "voxel": hv, "t": ht.view(np.uint32)}, ref, push=False)
+    rng = np.random.default_rng(5)
+    o = rng.uniform(1.01, 1.99, (5001, 3)).astype(np.float32)
+    d = rng.uniform(-1, 1, (5001, 3)).astype(np.float32)
+    ref = O.trace_batch(ref_pool, O.Rcp(None), o, d, nthreads=16)
+    hd, hv, ht = pool.trace_batch(o, d, width=70)
+    assert_same({"dir": hd, "voxel": hv, "t": ht.view(np.uint32)}, ref, push=False)
+    from octree_ray_tracing_amd._lib import call
+    with pytest.raises(ort.OchError, match="width"):            # width 0 is refused, not traced untiled
+        call("och_gpu_trace_batch_image", pool._h, None, 0, None, 1, 0, None, None, None)
+    pool.close()

@@ -1,0 +1,231 @@
+/* split_model.c -- checks and prices splitting one ray's walk over S lanes.
+ *
+ * Design tool only (not product, not a checker): its own restatement of the
+ * walk (ORT/och_h_octree.h:292-447) with the host's RCPPS, on a raw 1-based
+ * pool.
+ *
+ * The decomposition.  Call the cells of level L (size 2^-L) the walk tests at
+ * a PUSH and finds present its "segments", numbered 0, 1, 2, ... in walk
+ * order.  What the walk does at levels <= L does not depend on what it does
+ * inside a segment: it enters a present level-L cell, walks below it, and
+ * POPs back to level L with the position bits, child index and child size it
+ * had before the PUSH (a POP clears exactly the bits the descent set), and
+ * its next STEP at level L computes the same t values -- the same state a
+ * walk that found the cell empty reaches by STEPping at once.  So a lane that
+ * treats every segment but its own (ordinal % S == s) as empty walks the same
+ * levels <= L, enters its own segments in the same state as the full walk,
+ * and finds the same hit there if the hit lies there.  The ray's record is
+ * then the hit of the lowest segment ordinal any lane found, or the MISS.
+ * This tool checks that claim ray by ray against the full walk, and prices
+ * the split with the lockstep model (a wave costs its longest lane's PUSH
+ * tests, one per iteration of the render loop).
+ *
+ * Build: gcc -O2 -msse2 -o /tmp/split_model tools/split_model.c -lm -lpthread
+ * Input: raw uint32 nodes[n][8] of a 1-based h_octree pool, root 1, e.g.
+ *   ort.build_terrain(12).nodes.astype(np.uint32).tofile("d12_nodes.bin")
+ * Usage: split_model nodes.bin depth pitch L S [threads] */
+#include <immintrin.h>
+#include <math.h>
+#include <pthread.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+static inline uint32_t f2u(float f) { uint32_t u; memcpy(&u, &f, 4); return u; }
+static inline float u2f(uint32_t u) { float f; memcpy(&f, &u, 4); return f; }
+
+static const uint32_t *N;
+static int DEPTH, LEVEL, SEGS;
+
+typedef struct { int32_t dir; uint32_t voxel, t; int ord; int push; } Rec;
+
+/* seg < 0: the full walk; else only segments with ordinal % SEGS == seg are
+ * entered.  ord: the hit's segment ordinal (-1: MISS). */
+static void walk(const float *o, const float *d, int seg, Rec *out)
+{
+    float c[3], b[3];
+    uint32_t p[3], stack[32];
+    int inv = 0, idx = 0, sp = 0, level = 1, axis = 8, ord = 0, push = 0;
+    for (int a = 0; a < 3; ++a) {
+        const int pos = 0.0F < d[a];
+        inv |= pos << a;
+        const float refl = fabsf((pos ? 3.0F : 0.0F) - o[a]);
+        c[a] = _mm_cvtss_f32(_mm_rcp_ss(_mm_set_ss(u2f(f2u(d[a]) | 0x80000000u))));
+        b[a] = u2f(f2u(c[a] * refl) ^ 0x80000000u);
+        p[a] = f2u(refl) & 0x3FC00000u;
+        if (p[a] == 0x3FC00000u) idx |= 1 << a;
+    }
+    uint32_t dim = 1u << 22, node = 1, t_min = 0;
+    int cur_ord = -1;                       /* the segment the walk is inside (level > LEVEL) */
+    enum { PUSH, STEP, POP } st = PUSH;
+    for (;;) {
+        if (st == PUSH) {
+            ++push;
+            const uint32_t ch = N[(size_t)(node - 1) * 8 + ((idx ^ inv) & 7)];
+            if (!ch) { st = STEP; continue; }
+            if (level == LEVEL) {           /* a present level-L cell: segment ord */
+                const int k = ord++;
+                if (seg >= 0 && k % SEGS != seg) { st = STEP; continue; }
+                cur_ord = k;
+            }
+            if (level++ == DEPTH) {
+                out->dir = (axis >> 1) + 3 * ((inv & axis) == 0);
+                out->voxel = ch;
+                out->t = t_min;
+                out->ord = cur_ord;
+                out->push = push;
+                return;
+            }
+            stack[sp++] = node;
+            node = ch;
+            dim >>= 1;
+            idx = 0;
+            for (int a = 0; a < 3; ++a)
+                if (fmaf(u2f(p[a] | dim), c[a], b[a]) >= u2f(t_min)) { idx |= 1 << a; p[a] |= dim; }
+        } else if (st == STEP) {
+            uint32_t t[3];
+            for (int a = 0; a < 3; ++a) t[a] = f2u(fmaf(u2f(p[a]), c[a], b[a]));
+            const int a = (t[0] <= t[1] && t[0] <= t[2]) ? 0 : (t[1] < t[0] && t[1] <= t[2]) ? 1 : 2;
+            axis = 1 << a;
+            t_min = t[a];
+            if (!(idx & axis)) { st = POP; continue; }
+            p[a] &= ~dim;
+            idx ^= axis;
+            st = PUSH;
+        } else {
+            if (--level == 0) {
+                out->dir = 6; out->voxel = 0; out->t = 0x7F800000u; out->ord = -1; out->push = push;
+                return;
+            }
+            node = stack[--sp];
+            for (int a = 0; a < 3; ++a) p[a] &= ~dim;
+            dim <<= 1;
+            idx = 0;
+            for (int a = 0; a < 3; ++a)
+                if (u2f(dim) == u2f(p[a] & dim)) idx |= 1 << a;
+            st = STEP;
+        }
+    }
+}
+
+static void camera(float yaw, float pitch, int W, int H, int col, int row, float *d)
+{
+    const float aspect = (float)W / (float)H, fov = 1.25F;
+    const float f = 1.0F / tanf(fov / 2);
+    const float sb = sinf(yaw), cb = cosf(yaw), sc = sinf(pitch), cc = cosf(pitch);
+    const float m[9] = {cb, sb * sc, sb * cc, 0, cc, -sc, -sb, cb * sc, cb * cc};
+    const float u = aspect * ((2.0F / W) * col - 1.0F), v = (2.0F / H) * row - 1.0F;
+    const float ru = u * m[0] + v * m[1] + f * m[2];
+    const float rv = u * m[3] + v * m[4] + f * m[5];
+    const float rw = u * m[6] + v * m[7] + f * m[8];
+    const float rm = 1.0F / sqrtf(ru * ru + rv * rv + rw * rw);
+    d[0] = rw * rm; d[1] = ru * rm; d[2] = -rv * rm;
+}
+
+enum { W = 1920, H = 1080, TX = W / 8, TY = H / 8 };
+static float PITCH;
+static int *FULL, *SPLIT;        /* per tile: longest lane, full walk / split (max over its S x 64 lane tasks) */
+static long *SPLIT_WORK;         /* per tile: sum over the S waves of their longest lane */
+static long BAD, RAYS;
+static int NEXT;
+static pthread_mutex_t MU = PTHREAD_MUTEX_INITIALIZER;
+
+static void *worker(void *arg)
+{
+    (void)arg;
+    const float o[3] = {1.5F, 1.5F, 1.5F};
+    Rec seg[64];
+    for (;;) {
+        const int tile = __atomic_fetch_add(&NEXT, 1, __ATOMIC_RELAXED);
+        if (tile >= TX * TY) return NULL;
+        const int tx = tile % TX, ty = tile / TX;
+        int full_max = 0, split_max = 0;
+        int wave_max[64] = {0};                 /* S waves of 64 / S rays x S segments */
+        long bad = 0;
+        for (int l = 0; l < 64; ++l) {
+            float d[3];
+            camera(0.3F, PITCH, W, H, tx * 8 + l % 8, ty * 8 + l / 8, d);
+            Rec full;
+            walk(o, d, -1, &full);
+            if (full.push > full_max) full_max = full.push;
+            int best = -1;
+            for (int s = 0; s < SEGS; ++s) {
+                walk(o, d, s, &seg[s]);
+                if (seg[s].push > split_max) split_max = seg[s].push;
+                const int w = l / (64 / SEGS);
+                if (seg[s].push > wave_max[w]) wave_max[w] = seg[s].push;
+                if (seg[s].ord >= 0 && (best < 0 || seg[s].ord < seg[best].ord)) best = s;
+            }
+            const Rec m = best < 0 ? (Rec){6, 0, 0x7F800000u, -1, 0} : seg[best];
+            if (m.dir != full.dir || m.voxel != full.voxel || m.t != full.t) ++bad;
+        }
+        long work = 0;
+        for (int w = 0; w < SEGS; ++w) work += wave_max[w];
+        FULL[tile] = full_max;
+        SPLIT[tile] = split_max;
+        SPLIT_WORK[tile] = work;
+        pthread_mutex_lock(&MU);
+        BAD += bad;
+        RAYS += 64;
+        pthread_mutex_unlock(&MU);
+    }
+}
+
+static int cmp_desc(const void *a, const void *b) { return *(const int *)b - *(const int *)a; }
+
+int main(int argc, char **argv)
+{
+    if (argc < 6) { fprintf(stderr, "usage: split_model nodes.bin depth pitch L S [threads]\n"); return 2; }
+    FILE *fp = fopen(argv[1], "rb");
+    if (!fp) return 1;
+    fseek(fp, 0, SEEK_END);
+    const long sz = ftell(fp);
+    fseek(fp, 0, SEEK_SET);
+    uint32_t *buf = malloc(sz);
+    if (fread(buf, 1, sz, fp) != (size_t)sz) return 1;
+    fclose(fp);
+    N = buf;
+    DEPTH = atoi(argv[2]);
+    PITCH = (float)atof(argv[3]);
+    LEVEL = atoi(argv[4]);
+    SEGS = atoi(argv[5]);
+    const int threads = argc > 6 ? atoi(argv[6]) : 8;
+    if (LEVEL < 1 || LEVEL >= DEPTH || SEGS < 1 || 64 % SEGS) { fprintf(stderr, "need 1 <= L < depth, S | 64\n"); return 2; }
+    FULL = calloc(TX * TY, sizeof *FULL);
+    SPLIT = calloc(TX * TY, sizeof *SPLIT);
+    SPLIT_WORK = calloc(TX * TY, sizeof *SPLIT_WORK);
+    pthread_t th[256];
+    for (int k = 0; k < threads; ++k) pthread_create(&th[k], NULL, worker, NULL);
+    for (int k = 0; k < threads; ++k) pthread_join(th[k], NULL);
+    int *sorted = malloc(sizeof(int) * TX * TY);
+    memcpy(sorted, FULL, sizeof(int) * TX * TY);
+    qsort(sorted, TX * TY, sizeof(int), cmp_desc);
+    printf("{\"pitch\": %g, \"L\": %d, \"S\": %d, \"rays\": %ld, \"records_differ\": %ld, "
+           "\"longest_tile_full\": %d, \"tile_full_p99.9\": %d, \"tile_full_p99\": %d, \"tile_full_p90\": %d,",
+           PITCH, LEVEL, SEGS, RAYS, BAD, sorted[0], sorted[TX * TY / 1000], sorted[TX * TY / 100], sorted[TX * TY / 10]);
+    /* split the tiles whose longest lane exceeds T: the critical path becomes the
+     * longest lane of what is left (unsplit tiles' longest lane, split tiles'
+     * longest segment lane); the work, the sum of the waves' longest lanes */
+    printf(" \"by_threshold\": [");
+    const int Ts[] = {400, 300, 250, 200, 150, 100};
+    for (size_t k = 0; k < sizeof Ts / sizeof Ts[0]; ++k) {
+        long base = 0, work = 0;
+        int crit = 0, n = 0;
+        for (int t = 0; t < TX * TY; ++t) {
+            base += FULL[t];
+            if (FULL[t] > Ts[k]) {
+                ++n;
+                work += SPLIT_WORK[t];
+                if (SPLIT[t] > crit) crit = SPLIT[t];
+            } else {
+                work += FULL[t];
+                if (FULL[t] > crit) crit = FULL[t];
+            }
+        }
+        printf("%s{\"T\": %d, \"tiles_split\": %d, \"critical_path\": %d, \"work_vs_unsplit\": %.4f}", k ? ", " : "",
+               Ts[k], n, crit, (double)work / base);
+    }
+    printf("]}\n");
+    return BAD != 0;
+}
