@@ -183,9 +183,18 @@ typedef enum och_option {
                                   1 (default) = recorded by the kernel's own dispatch (hipExtLaunchKernel: no
                                   packets between two launches of a stream); 2 = hipEventRecord before and
                                   after the launch; 0 = not timed */
-    OCH_OPT_PLAN = 11          /* shape of och_gpu_plan_views' launch order (set before planning): 0 =
+    OCH_OPT_PLAN = 11,         /* shape of och_gpu_plan_views' launch order (set before planning): 0 =
                                   costliest first; P in 1..99 = the costliest P % first, the rest in natural
                                   order (default 10); 100 = costliest and cheapest alternating */
+    OCH_OPT_SPLIT = 14,        /* heavy-tile split (set before och_gpu_plan_views; renders with OCH_OPT_TILE_ORDER
+                                  2, block 64, packed layout): the planned tiles whose cost reaches this % of the
+                                  costliest one's walk each ray over OCH_OPT_SPLIT_SEGS lanes, a lane entering
+                                  only every S-th present cell of level OCH_OPT_SPLIT_LEVEL along the ray, the
+                                  lowest one's hit kept -- the same records, a lone
+                                  frame no longer waiting on its few longest rays.  0 = off */
+    OCH_OPT_SPLIT_SEGS = 15,   /* lanes per ray of a split tile: 2, 4 (default), 8 or 16 */
+    OCH_OPT_SPLIT_LEVEL = 16,  /* the level whose cells are the split's segments (default 6) */
+    OCH_OPT_SPLIT_TILES = 17   /* read only: tiles split by the current plan */
 } och_option;
 OCH_API int och_gpu_set_option(och_gpu_pool *pool, int option, int value);
 OCH_API int och_gpu_get_option(const och_gpu_pool *pool, int option, int *value);

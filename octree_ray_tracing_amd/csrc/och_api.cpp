@@ -173,6 +173,9 @@ struct och_gpu_pool {
     int opt_cull = 1;
     int opt_timing = 1;                        // OCH_OPT_TIMING
     int opt_plan = 10;                         // OCH_OPT_PLAN (shape of och_gpu_plan_views' order)
+    int opt_split = 0;                         // OCH_OPT_SPLIT: heavy-tile threshold, % of the costliest tile (0 off)
+    int opt_split_segs = 4;                    // OCH_OPT_SPLIT_SEGS: lanes per heavy tile's ray (2, 4, 8, 16)
+    int opt_split_level = 6;                   // OCH_OPT_SPLIT_LEVEL: the level whose cells are the segments
     hipEvent_t next_ev_start = nullptr;        // och_gpu_set_launch_events: the next launch's events
     hipEvent_t next_ev_stop = nullptr;
     // bounding box of the pool's voxels (voxel units, [lo, hi)), for the cull
@@ -192,6 +195,12 @@ struct och_gpu_pool {
     uint32_t order_blocks[3] = {0, 0, 0};     // allocated entries
     uint32_t plan_blocks[3] = {0, 0, 0};      // entries of the current plan (its launch's grid)
     int64_t plan_key[3][9] = {};
+    // the primary plan's split form (OCH_OPT_SPLIT, plan_split): the heavy tiles'
+    // parts first, then the plan's other workgroups; valid with plan_key[0] while
+    // split_params matches the options it was made with
+    uint32_t *d_order_split = nullptr;
+    uint32_t split_alloc = 0, split_n = 0, split_extra = 0, split_tiles = 0;
+    int split_params[3] = {0, 0, 0};          // threshold, segments, level
     // row deal (och_gpu_set_row_deal): for frames of deal_h rows in chunks of
     // deal_chunk over deal_n shards, chunk g belongs to a chosen shard instead
     // of g % n; slices hold deal_max chunks (the largest shard's, the rest padded)
@@ -216,6 +225,8 @@ struct och_gpu_pool {
         sc.order = nullptr;
         sc.order_n = 0;
         sc.cost = nullptr;
+        sc.split = 0;
+        sc.split_extra = 0;
         sc.ev_start = nullptr;
         sc.ev_stop = nullptr;
         return sc;
@@ -650,6 +661,7 @@ OCH_API int och_gpu_pool_destroy(och_gpu_pool *p)
     if (p->d_stage) (void)hipFree(p->d_stage);
     for (uint32_t *o : p->d_order)
         if (o) (void)hipFree(o);
+    if (p->d_order_split) (void)hipFree(p->d_order_split);
     for (uint32_t *o : p->d_order_xcd)
         if (o) (void)hipFree(o);
     if (p->d_chunk_map) (void)hipFree(p->d_chunk_map);
@@ -960,6 +972,20 @@ OCH_API int och_gpu_set_option(och_gpu_pool *p, int option, int value)
         if (value < 0 || value > 100) return fail(OCH_E_INVALID, "plan shape must be 0..100");
         p->opt_plan = value;
         return OCH_OK;
+    case OCH_OPT_SPLIT:
+        if (value < 0 || value > 100) return fail(OCH_E_INVALID, "split threshold must be 0..100 (%% of the costliest tile)");
+        p->opt_split = value;
+        return OCH_OK;
+    case OCH_OPT_SPLIT_SEGS:
+        if (value != 2 && value != 4 && value != 8 && value != 16) return fail(OCH_E_INVALID, "split segments must be 2, 4, 8 or 16");
+        p->opt_split_segs = value;
+        return OCH_OK;
+    case OCH_OPT_SPLIT_LEVEL:
+        if (value < 1 || value > 21) return fail(OCH_E_INVALID, "split level must be 1..21");
+        p->opt_split_level = value;
+        return OCH_OK;
+    case OCH_OPT_SPLIT_TILES:
+        return fail(OCH_E_INVALID, "OCH_OPT_SPLIT_TILES is read-only");
     case 0: case 2: case 3: case 7: case 9: case 12: case 13:
         return retired_option(option);
     default:
@@ -978,6 +1004,10 @@ OCH_API int och_gpu_get_option(const och_gpu_pool *p, int option, int *value)
     case OCH_OPT_CULL: *value = p->opt_cull; return OCH_OK;
     case OCH_OPT_TIMING: *value = p->opt_timing; return OCH_OK;
     case OCH_OPT_PLAN: *value = p->opt_plan; return OCH_OK;
+    case OCH_OPT_SPLIT: *value = p->opt_split; return OCH_OK;
+    case OCH_OPT_SPLIT_SEGS: *value = p->opt_split_segs; return OCH_OK;
+    case OCH_OPT_SPLIT_LEVEL: *value = p->opt_split_level; return OCH_OK;
+    case OCH_OPT_SPLIT_TILES: *value = (int)p->split_tiles; return OCH_OK;
     case 0: case 2: case 3: case 7: case 9: case 12: case 13:
         return retired_option(option);
     default: return fail(OCH_E_INVALID, "unknown option %d", option);
@@ -1352,6 +1382,14 @@ int render_views(och_gpu_pool *p, const och_camera *cams, int n_views, uint32_t 
         if (std::memcmp(key, p->plan_key[which], sizeof key) == 0) {
             sc.order = p->opt_tile_order == 3 ? p->d_order_xcd[which] : p->d_order[which];
             sc.order_n = p->plan_blocks[which];
+            // the plan's split form, while the options it was made with hold
+            if (!bounce && p->opt_tile_order == 2 && p->split_n && p->dev().packed && p->opt_split == p->split_params[0] &&
+                p->opt_split_segs == p->split_params[1] && p->opt_split_level == p->split_params[2]) {
+                sc.order = p->d_order_split;
+                sc.order_n = p->split_n;
+                sc.split_extra = p->split_extra;
+                sc.split = (uint32_t)__builtin_ctz((unsigned)p->opt_split_segs) | ((uint32_t)p->opt_split_level << 8);
+            }
         }
     }
     if (code_slices)
@@ -1397,6 +1435,50 @@ void plan_shape(std::vector<uint32_t> &order, int mode)
             if (!taken[b]) out.push_back(b);
     }
     order.swap(out);
+}
+
+// The split form of a primary plan (OCH_OPT_SPLIT): the tiles
+// whose planning cost reaches opt_split % of the costliest one go first, each
+// as opt_split_segs parts (1 << 31 | part << 24 | tile: one wave walks 64 / S
+// of its rays, every ray over S lanes), then the plan's other workgroups in
+// its order.  Block 64 only (workgroup = tile), packed layout, tiles < 2^24,
+// and a split level above the leaves; otherwise no split plan.
+int plan_split(och_gpu_pool *p, const std::vector<uint32_t> &by_cost, const std::vector<uint32_t> &order,
+               const std::vector<uint32_t> &c)
+{
+    p->split_n = p->split_extra = p->split_tiles = 0;
+    p->split_params[0] = p->split_params[1] = p->split_params[2] = 0;
+    const uint32_t n = (uint32_t)order.size();
+    const int S = p->opt_split_segs;
+    if (p->opt_split <= 0 || p->opt_block != 64 || !p->dev().packed || p->opt_split_level >= p->depth || n == 0 ||
+        n >= (1u << 24))
+        return OCH_OK;
+    const double thr = (double)c[by_cost[0]] * p->opt_split / 100.0;
+    std::vector<uint8_t> heavy(n, 0);
+    std::vector<uint32_t> split;
+    const uint32_t cap = std::max(1u, n / 16);                  // a bound on the extra waves
+    for (uint32_t k = 0; k < n && k < cap && (double)c[by_cost[k]] >= thr; ++k) {
+        heavy[by_cost[k]] = 1;
+        for (int part = 0; part < S; ++part) split.push_back(0x80000000u | ((uint32_t)part << 24) | by_cost[k]);
+    }
+    const uint32_t n_heavy = (uint32_t)split.size() / (uint32_t)S;
+    for (uint32_t b : order)
+        if (!heavy[b]) split.push_back(b);
+    if (p->split_alloc < split.size()) {
+        if (p->d_order_split) OCH_HIP(hipFree(p->d_order_split));
+        p->d_order_split = nullptr;
+        p->split_alloc = 0;
+        OCH_HIP(hipMalloc(&p->d_order_split, split.size() * 4));
+        p->split_alloc = (uint32_t)split.size();
+    }
+    OCH_HIP(hipMemcpy(p->d_order_split, split.data(), split.size() * 4, hipMemcpyHostToDevice));
+    p->split_n = (uint32_t)split.size();
+    p->split_extra = n_heavy * (uint32_t)(S - 1);
+    p->split_tiles = n_heavy;
+    p->split_params[0] = p->opt_split;
+    p->split_params[1] = S;
+    p->split_params[2] = p->opt_split_level;
+    return OCH_OK;
 }
 
 }  // namespace
@@ -1453,6 +1535,7 @@ OCH_API int och_gpu_plan_views(och_gpu_pool *p, const och_camera *cams, int n_vi
         std::vector<uint32_t> order(n_blocks);
         for (uint32_t i = 0; i < n_blocks; ++i) order[i] = i;
         std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return c[a] > c[b]; });
+        const std::vector<uint32_t> by_cost = order;
         plan_shape(order, p->opt_plan);
         // Grouped per XCD (OCH_OPT_TILE_ORDER = 3): workgroup slot i runs on XCD
         // i % 8, so deal 64x64-pixel supertiles over the XCDs (each XCD's L2 then
@@ -1492,6 +1575,8 @@ OCH_API int och_gpu_plan_views(och_gpu_pool *p, const och_camera *cams, int n_vi
         }
         OCH_HIP(hipMemcpy(p->d_order[which], order.data(), (size_t)n_blocks * 4, hipMemcpyHostToDevice));
         OCH_HIP(hipMemcpy(p->d_order_xcd[which], grouped.data(), (size_t)n_blocks * 4, hipMemcpyHostToDevice));
+        if (which == 0)
+            if (int ss = plan_split(p, by_cost, order, c)) return ss;
         const int64_t key[9] = {W, H, n_views, row_chunk, shard, n_shards, p->opt_block,
                                 which ? p->opt_bounce_compact : 0, dealt ? (int64_t)p->deal_serial : 0};
         std::memcpy(p->plan_key[which], key, sizeof key);

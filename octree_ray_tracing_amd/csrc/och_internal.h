@@ -156,6 +156,12 @@ struct Schedule {
     const uint32_t *order;  // optional workgroup permutation (och_gpu_plan_views)
     uint32_t order_n;       // entries in *order: a launch whose grid differs runs in natural order
     uint32_t *cost;         // optional per-workgroup duration output (the planning launch)
+    // A split plan (OCH_OPT_SPLIT; camera renders, packed layout, block 64):
+    // order then lists the grid's workgroups with each heavy tile replaced by
+    // its parts (1 << 31 | part << 24 | tile), order_n = grid + split_extra.
+    // split = log2(segments) | split level << 8, 0 = none.
+    uint32_t split;
+    uint32_t split_extra;
     hipEvent_t ev_start;    // optional: recorded by the traversal kernel's own dispatch (hipExtLaunchKernel)
     hipEvent_t ev_stop;
 };

@@ -110,6 +110,11 @@ struct Ray {
     uint32_t mode;        // see below
     uint32_t push;
     bool inside;          // wave-uniform: every ray of the wave starts inside the root (ray_trace)
+    // Split walks only (kSplit, k_trace_grid's heavy tiles): the PUSH test of a
+    // present cell of child size split_dim is segment `ord` of the walk, which
+    // this lane enters only when ord & split_mask == split_seg; hit_ord: the
+    // last segment it entered (the segment of its HIT).
+    uint32_t split_dim, split_mask, split_seg, ord, hit_ord;
 };
 
 // Ray phase.  Packed layout (one merged PUSH + descend phase): kStepping (0)
@@ -184,7 +189,7 @@ __device__ __forceinline__ void ray_push_raw(Ray &r, const DevPool &P)
     r.child = (P.nodes - 24)[8u * r.cur + c24];
 }
 
-template <bool kCount, bool kAsm, bool kIdxPlane>
+template <bool kCount, bool kAsm, bool kIdxPlane, bool kSplit = false>
 __device__ __forceinline__ void ray_push_descend(Ray &r, const DevPool &P, uint32_t stride);
 
 // Occupied-box cull (OCH_OPT_CULL; DESIGN.md §4b has the proof).  With
@@ -474,7 +479,7 @@ __device__ __forceinline__ void wait_cur(Ray &r)
 // cur -- the node of the next PUSH, or the voxel id of a HIT -- and the child
 // cell chosen.  The next PUSH takes the word after the other lanes' STEP phase
 // has hidden the load.
-template <bool kCount, bool kAsm, bool kIdxPlane>
+template <bool kCount, bool kAsm, bool kIdxPlane, bool kSplit>
 __device__ __forceinline__ void ray_push_descend(Ray &r, const DevPool &P, uint32_t stride)
 {
     wait_cur<kAsm>(r);
@@ -485,7 +490,19 @@ __device__ __forceinline__ void ray_push_descend(Ray &r, const DevPool &P, uint3
     // (profiles/r05/r05r/).
     if (kCount) r.push += r.mode != kStepping;
     const uint32_t c24 = r.idx ^ r.inv;                                     // 24 + child index
-    const uint32_t present = __builtin_amdgcn_ubfe(r.cur, c24, 1u);
+    uint32_t present = __builtin_amdgcn_ubfe(r.cur, c24, 1u);
+    if (kSplit) {
+        // A present cell of the split level due to PUSH is segment ord of the
+        // walk; another lane's segment counts as empty here (the walk above
+        // the split level does not depend on what happens inside a segment,
+        // DESIGN.md §4e).
+        if (r.mode != kStepping && present && r.dim == r.split_dim) {
+            const bool mine = (r.ord & r.split_mask) == r.split_seg;
+            r.hit_ord = mine ? r.ord : r.hit_ord;
+            present = mine ? 1u : 0u;
+            ++r.ord;
+        }
+    }
     r.mode = min(r.mode, present);          // kStepping (0), or 1: "PUSH due" after the descent
     const bool go = r.mode != kStepping;    // compared before the barrier: no copy of mode
     asm volatile("" : "+v"(r.mode));
@@ -540,7 +557,7 @@ __device__ __forceinline__ void ray_push_descend(Ray &r, const DevPool &P, uint3
     r.idx = nidx;
 }
 
-template <int kPacked, bool kCount, bool kAsm = false, bool kIdxPlane = false>
+template <int kPacked, bool kCount, bool kAsm = false, bool kIdxPlane = false, bool kSplit = false>
 __device__ __forceinline__ void ray_iterate(Ray &r, const DevPool &P, uint32_t stride)
 {
     if (kPacked) {
@@ -550,7 +567,7 @@ __device__ __forceinline__ void ray_iterate(Ray &r, const DevPool &P, uint32_t s
         // no activity test: a miss leaves the lane kStepping, a HIT ends in this
         // phase; every lane takes the PUSH test (ray_push_descend)
         asm volatile("" : "+v"(r.mode));
-        ray_push_descend<kCount, kAsm, kIdxPlane>(r, P, stride);
+        ray_push_descend<kCount, kAsm, kIdxPlane, kSplit>(r, P, stride);
         return;
     }
     if (in_mode(r, kPending)) ray_phase_descend_raw(r, stride);
@@ -563,11 +580,11 @@ __device__ __forceinline__ void ray_iterate(Ray &r, const DevPool &P, uint32_t s
 // (A lane mask of active lanes cleared by the MISS and HIT compares instead
 // of the activity test -- two VALU per iteration -- measured 5 % slower: it
 // added a compare to the descent and SALU to every block, profiles/r05/r05e/.)
-template <int kPacked, bool kCount, bool kAsm, bool kIdxPlane>
+template <int kPacked, bool kCount, bool kAsm, bool kIdxPlane, bool kSplit = false>
 __device__ __forceinline__ void ray_walk(Ray &r, const DevPool &P, uint32_t stride)
 {
     if (kPacked)
-        ray_push_descend<kCount, kAsm, kIdxPlane>(r, P, stride);
+        ray_push_descend<kCount, kAsm, kIdxPlane, kSplit>(r, P, stride);
     else
         ray_push_raw<kCount>(r, P);
     // the activity test's two constants in VGPRs: as SGPRs the compiler re-loads
@@ -576,22 +593,22 @@ __device__ __forceinline__ void ray_walk(Ray &r, const DevPool &P, uint32_t stri
     uint32_t lo = P.dim_lo, span = P.dim_span;
     asm volatile("" : "+v"(lo), "+v"(span));
     if (r.dim - lo <= span) do {
-        ray_iterate<kPacked, kCount, kAsm, kIdxPlane>(r, P, stride);
+        ray_iterate<kPacked, kCount, kAsm, kIdxPlane, kSplit>(r, P, stride);
     } while (r.dim - lo <= span);
 }
 
 // Setup, then the walk.  The branch on inside (wave-uniform) comes
 // before the root PUSH issues its asm load, so no copy of cur is made at a
 // join while a load is in flight (tools/isa_check.py).
-template <int kPacked, bool kCount, bool kCull = false, bool kAsm = false>
+template <int kPacked, bool kCount, bool kCull = false, bool kAsm = false, bool kSplit = false>
 __device__ __forceinline__ void ray_trace(Ray &r, const DevPool &P, const float *o, const float *d, uint32_t stack,
                                           uint32_t stride, bool exact = true)
 {
     if (!ray_setup<kCount, kCull>(r, P, o, d, stack, stride, exact)) return;
     if (kPacked && r.inside)
-        ray_walk<kPacked, kCount, kAsm, true>(r, P, stride);
+        ray_walk<kPacked, kCount, kAsm, true, kSplit>(r, P, stride);
     else
-        ray_walk<kPacked, kCount, kAsm, false>(r, P, stride);
+        ray_walk<kPacked, kCount, kAsm, false, kSplit>(r, P, stride);
 }
 
 // The hit record of a finished ray (:346-355 hit, :423-431 miss).  The packed
@@ -639,6 +656,7 @@ __device__ __forceinline__ void bounce_ray(const float *o, const float *d, const
 // Rays from arrays: shared (stride 0) or per-ray (stride 3) origin, AoS float3 dirs.
 struct ArraySource {
     static constexpr bool kProvenMiss = false;    // no camera_proven_miss before setup
+    static constexpr bool kSplittable = false;    // split plans come from och_gpu_plan_views (camera rays)
     const float *origin;
     const float *dirs;
     int origin_stride;
@@ -801,6 +819,7 @@ struct FastDiv {
 // of a wave runs on the scalar unit.
 struct TiledArraySource {
     static constexpr bool kProvenMiss = false;
+    static constexpr bool kSplittable = false;
     const float *origin;
     const float *dirs;
     int origin_stride;
@@ -838,6 +857,7 @@ struct TiledArraySource {
 // output token is view * slice_pixels + slice pixel.
 struct CameraSource {
     static constexpr bool kProvenMiss = true;     // get_wave_culled runs camera_proven_miss when P.cam_cull
+    static constexpr bool kSplittable = true;     // heavy tiles split over lanes (kSplit launches)
     och_camera cam[kMaxViews];
     CameraView view[kMaxViews];
     int32_t n_views, row_chunk, shard, n_shards, slice_rows, width, height, order;
@@ -1077,14 +1097,72 @@ __device__ __forceinline__ uint32_t xcd_block(uint32_t b, uint32_t nb, uint32_t 
 // (MI355X_MICROARCH.md, residency; the compiler's occupancy note says 8 there), and 8
 // give +5 % sustained.  tools/isa_check.py check 4 holds every
 // traversal kernel to 8 waves per SIMD.
-template <class Src, class Sink, int kPacked, bool kCount>
+// A heavy tile's rays, each walked by S lanes (kSplit launches, OCH_OPT_SPLIT;
+// DESIGN.md §4e).  Workgroup = one wave = 64 / S rays of the tile (part
+// `part` of its S parts) x S segment lanes: lane = seg * (64 / S) + ray.  A
+// lane walks the whole ray above the split level but enters only the present
+// split-level cells (segments) whose ordinal is its seg modulo S; the ray's
+// record is the HIT of the lowest segment ordinal any of its lanes found, or
+// the MISS -- the full walk's record, bit for bit, because the walk above the
+// split level does not depend on what it does inside a segment.  The lanes
+// of a ray agree through lane swizzles; segment 0's lane stores the record.
+template <class Src, class Sink, int kPacked>
+__device__ __forceinline__ void split_tile(const DevPool &P, const Src &S, const Sink &K, uint32_t ent, uint32_t split,
+                                           uint32_t *lds_stack)
+{
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t log2s = split & 0xFFu, level = (split >> 8) & 0xFFu;
+    const uint32_t per = 64u >> log2s;                                      // rays per wave
+    const uint32_t tile = ent & 0xFFFFFFu, part = (ent >> 24) & 0x7Fu;
+    const uint32_t ray = lane & (per - 1u), seg = lane >> (6u - log2s);
+    const uint32_t pix = part * per + ray;                                  // pixel of the 8x8 tile
+    float o[3], d[3];
+    uint32_t out = 0, key = ~0u;
+    bool miss = false;
+    Hit h{OCH_EXIT, 0u, P.miss_bits, 0u};
+    const bool valid = tile * 64u + pix < S.count() &&
+                       S.get_wave_culled(tile * 64u, pix, P, P.cull != 0, o, d, out, miss);
+    if (valid && !miss) {
+        Ray r;
+        r.split_dim = 1u << (23u - level);
+        r.split_mask = (1u << log2s) - 1u;
+        r.split_seg = seg;
+        r.ord = 0;
+        r.hit_ord = ~0u;
+        ray_trace<kPacked, false, true, kAsmLoad, true>(r, P, o, d, stack_column(lds_stack, P.depth), blockDim.x,
+                                                       !(Src::kProvenMiss && P.cam_cull));
+        h = ray_result<kPacked, kAsmLoad>(r, P);
+        key = r.dim > (1u << 22) ? ~0u : r.hit_ord;                         // a MISS loses to any HIT
+    }
+    // the ray's lanes are ray + k * per: keep the lowest segment's HIT
+    for (uint32_t off = per; off < 64u; off <<= 1) {
+        const uint32_t k2 = (uint32_t)__shfl_xor((int)key, (int)off);
+        const int32_t d2 = __shfl_xor(h.dir, (int)off);
+        const uint32_t v2 = (uint32_t)__shfl_xor((int)h.voxel, (int)off);
+        const uint32_t t2 = (uint32_t)__shfl_xor((int)h.t, (int)off);
+        if (k2 < key) {
+            key = k2;
+            h.dir = d2;
+            h.voxel = v2;
+            h.t = t2;
+        }
+    }
+    if (valid && seg == 0) K.put(out, h);
+}
+
+template <class Src, class Sink, int kPacked, bool kCount, bool kSplit>
 __global__ __attribute__((amdgpu_num_sgpr(80))) void k_trace_grid(DevPool P, Src S, Sink K, uint32_t xcd_group, const uint32_t *__restrict__ order,
-                             uint32_t *__restrict__ cost, uint64_t *stamps, uint32_t stamp_cap)
+                             uint32_t *__restrict__ cost, uint64_t *stamps, uint32_t stamp_cap, uint32_t split)
 {
     extern __shared__ uint32_t lds_stack[];
     const uint64_t t0 = stamps ? realtime() : 0;
     const uint64_t c0 = cost ? __builtin_amdgcn_s_memtime() : 0;
-    const uint32_t blk = order ? order[blockIdx.x] : xcd_block(blockIdx.x, gridDim.x, xcd_group);
+    uint32_t blk = order ? order[blockIdx.x] : xcd_block(blockIdx.x, gridDim.x, xcd_group);
+    if (kSplit && (blk >> 31)) {                    // a part of a heavy tile (wave-uniform)
+        split_tile<Src, Sink, kPacked>(P, S, K, blk, split, lds_stack);
+        if (stamps) stamp(stamps, stamp_cap, t0, 64);
+        return;
+    }
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave_base = blk * blockDim.x + (threadIdx.x & ~63u);
     float o[3], d[3];
@@ -1332,10 +1410,19 @@ hipError_t launch_as(const DevPool &p, const Src &s, const Sink &k, uint32_t n, 
     const size_t lds = stack_bytes(p.depth, block);
     const uint32_t xcd_group = supertile_rays >= (uint32_t)block ? supertile_rays / (uint32_t)block : 0u;
     const uint32_t grid = (n + (uint32_t)block - 1) / (uint32_t)block;
+    if constexpr (Src::kSplittable && kPacked && !kCount) {
+        // a split plan (och_api.cpp plan_split): this grid's workgroups, the
+        // heavy ones replaced by their parts; one wave per workgroup
+        if (sc.split && sc.order && block == 64 && sc.order_n == grid + sc.split_extra) {
+            OCH_LAUNCH_TIMED(sc, (k_trace_grid<Src, Sink, kPacked, kCount, true>), dim3(sc.order_n), dim3(block), lds,
+                             stream, p, s, k, 0u, sc.order, sc.cost, sc.stamps, sc.stamp_cap, sc.split);
+            return hipGetLastError();
+        }
+    }
     // a plan is a permutation of exactly this grid's workgroups; any other
     // (stale or for another block size) would index past it
-    OCH_LAUNCH_TIMED(sc, (k_trace_grid<Src, Sink, kPacked, kCount>), dim3(grid), dim3(block), lds, stream, p, s, k,
-                     xcd_group, sc.order_n == grid ? sc.order : nullptr, sc.cost, sc.stamps, sc.stamp_cap);
+    OCH_LAUNCH_TIMED(sc, (k_trace_grid<Src, Sink, kPacked, kCount, false>), dim3(grid), dim3(block), lds, stream, p, s,
+                     k, xcd_group, sc.order_n == grid ? sc.order : nullptr, sc.cost, sc.stamps, sc.stamp_cap, 0u);
     return hipGetLastError();
 }
 
@@ -1409,9 +1496,11 @@ hipError_t occupancy_blocks_per_cu(int kind, int block, int depth, int *blocks)
     const size_t lds = stack_bytes(depth, block);
     switch (kind) {
     case 0:
-        return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, k_trace_grid<CameraSource, FrameSink, 1, false>, block, lds);
+        return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, k_trace_grid<CameraSource, FrameSink, 1, false, false>,
+                                                            block, lds);
     case 2:
-        return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, k_trace_grid<ArraySource, HitSink<false>, 1, false>,
+        return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks,
+                                                            k_trace_grid<ArraySource, HitSink<false>, 1, false, false>,
                                                             block, lds);
     default:
         return hipErrorInvalidValue;

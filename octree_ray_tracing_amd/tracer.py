@@ -168,7 +168,9 @@ class GpuPool:
         call("och_gpu_pool_update", self._h, int(first), nodes.shape[0], _np_ptr(nodes), int(root))
 
     # och_option (include/och_gpu.h); ids 0, 2, 3, 7, 9, 12, 13 were retired arms
-    OPTIONS = {"block": 1, "layout": 4, "tile_order": 5, "bounce_compact": 6, "cull": 8, "timing": 10, "plan": 11}
+    OPTIONS = {"block": 1, "layout": 4, "tile_order": 5, "bounce_compact": 6, "cull": 8, "timing": 10, "plan": 11,
+               "split": 14, "split_segs": 15, "split_level": 16}
+    READ_ONLY = {"split_tiles": 17}
 
     def set_option(self, name: str, value: int):
         """Launch options (och_gpu_set_option): block, layout, tile_order, bounce_compact, cull
@@ -177,7 +179,7 @@ class GpuPool:
 
     def get_option(self, name: str) -> int:
         v = C.c_int()
-        call("och_gpu_get_option", self._h, self.OPTIONS[name], C.byref(v))
+        call("och_gpu_get_option", self._h, self.OPTIONS.get(name) or self.READ_ONLY[name], C.byref(v))
         return v.value
 
     def set_stamp_buffer(self, stamps, capacity_waves: int):

@@ -23,7 +23,9 @@
  * Build: gcc -O2 -msse2 -o /tmp/split_model tools/split_model.c -lm -lpthread
  * Input: raw uint32 nodes[n][8] of a 1-based h_octree pool, root 1, e.g.
  *   ort.build_terrain(12).nodes.astype(np.uint32).tofile("d12_nodes.bin")
- * Usage: split_model nodes.bin depth pitch L S [threads] */
+ * Usage: split_model nodes.bin depth pitch L S [threads [early]]
+ *   early 1: a lane stops at the first segment past the ray's hit (ideal: as if
+ *   the lane that finds the hit told the others at once). */
 #include <immintrin.h>
 #include <math.h>
 #include <pthread.h>
@@ -36,13 +38,13 @@ static inline uint32_t f2u(float f) { uint32_t u; memcpy(&u, &f, 4); return u; }
 static inline float u2f(uint32_t u) { float f; memcpy(&f, &u, 4); return f; }
 
 static const uint32_t *N;
-static int DEPTH, LEVEL, SEGS;
+static int DEPTH, LEVEL, SEGS, EARLY;
 
 typedef struct { int32_t dir; uint32_t voxel, t; int ord; int push; } Rec;
 
 /* seg < 0: the full walk; else only segments with ordinal % SEGS == seg are
  * entered.  ord: the hit's segment ordinal (-1: MISS). */
-static void walk(const float *o, const float *d, int seg, Rec *out)
+static void walk(const float *o, const float *d, int seg, int stop_ord, Rec *out)
 {
     float c[3], b[3];
     uint32_t p[3], stack[32];
@@ -66,6 +68,10 @@ static void walk(const float *o, const float *d, int seg, Rec *out)
             if (!ch) { st = STEP; continue; }
             if (level == LEVEL) {           /* a present level-L cell: segment ord */
                 const int k = ord++;
+                if (stop_ord >= 0 && k > stop_ord) {    /* past the ray's first hit: no later segment can win */
+                    out->dir = 6; out->voxel = 0; out->t = 0x7F800000u; out->ord = -1; out->push = push;
+                    return;
+                }
                 if (seg >= 0 && k % SEGS != seg) { st = STEP; continue; }
                 cur_ord = k;
             }
@@ -147,11 +153,11 @@ static void *worker(void *arg)
             float d[3];
             camera(0.3F, PITCH, W, H, tx * 8 + l % 8, ty * 8 + l / 8, d);
             Rec full;
-            walk(o, d, -1, &full);
+            walk(o, d, -1, -1, &full);
             if (full.push > full_max) full_max = full.push;
             int best = -1;
             for (int s = 0; s < SEGS; ++s) {
-                walk(o, d, s, &seg[s]);
+                walk(o, d, s, EARLY ? full.ord : -1, &seg[s]);
                 if (seg[s].push > split_max) split_max = seg[s].push;
                 const int w = l / (64 / SEGS);
                 if (seg[s].push > wave_max[w]) wave_max[w] = seg[s].push;
@@ -191,6 +197,7 @@ int main(int argc, char **argv)
     LEVEL = atoi(argv[4]);
     SEGS = atoi(argv[5]);
     const int threads = argc > 6 ? atoi(argv[6]) : 8;
+    EARLY = argc > 7 ? atoi(argv[7]) : 0;
     if (LEVEL < 1 || LEVEL >= DEPTH || SEGS < 1 || 64 % SEGS) { fprintf(stderr, "need 1 <= L < depth, S | 64\n"); return 2; }
     FULL = calloc(TX * TY, sizeof *FULL);
     SPLIT = calloc(TX * TY, sizeof *SPLIT);
@@ -201,9 +208,9 @@ int main(int argc, char **argv)
     int *sorted = malloc(sizeof(int) * TX * TY);
     memcpy(sorted, FULL, sizeof(int) * TX * TY);
     qsort(sorted, TX * TY, sizeof(int), cmp_desc);
-    printf("{\"pitch\": %g, \"L\": %d, \"S\": %d, \"rays\": %ld, \"records_differ\": %ld, "
+    printf("{\"early\": %d, \"pitch\": %g, \"L\": %d, \"S\": %d, \"rays\": %ld, \"records_differ\": %ld, "
            "\"longest_tile_full\": %d, \"tile_full_p99.9\": %d, \"tile_full_p99\": %d, \"tile_full_p90\": %d,",
-           PITCH, LEVEL, SEGS, RAYS, BAD, sorted[0], sorted[TX * TY / 1000], sorted[TX * TY / 100], sorted[TX * TY / 10]);
+           EARLY, PITCH, LEVEL, SEGS, RAYS, BAD, sorted[0], sorted[TX * TY / 1000], sorted[TX * TY / 100], sorted[TX * TY / 10]);
     /* split the tiles whose longest lane exceeds T: the critical path becomes the
      * longest lane of what is left (unsplit tiles' longest lane, split tiles'
      * longest segment lane); the work, the sum of the waves' longest lanes */
