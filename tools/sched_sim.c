@@ -13,7 +13,8 @@
  * Input: raw uint32 nodes[n][8] (1-based h_octree pool), e.g. written by
  *   ort.build_terrain(12).nodes.astype(np.uint32).tofile("d12_nodes.bin")
  * Usage: sched_sim nodes.bin depth pitch [tile_stride [schedule [threshold]]]
- *        sched_sim nodes.bin depth pitch tile_stride 4 [K [move_cost [waves_per_block <= 4]]] */
+ * (Schedule 4, in-block wave merging, went with the retired merge arm:
+ * profiles/r05/retired/tools/sched_sim_merge.diff.) */
 #include <immintrin.h>
 #include <math.h>
 #include <stdint.h>
@@ -330,77 +331,6 @@ static void wave_chain(Ray *R, int n, Stats *S)
     S->waves += 1;
 }
 
-/* schedule 4: wave merging inside a block of NB waves (NB tiles).  Every
- * MERGE_K iterations the block's unfinished rays are packed in order into the
- * fewest waves (finished lanes dropped), as a block-level ballot + LDS
- * exchange of ray state would do; each packing charges MOVE_COST VALU to every
- * wave that remains.  Per iteration each wave pays the merged loop's blocks
- * (as wave_merged) when any of its lanes needs them.  MERGE_K = 0: no merging
- * (the same as schedule 2 for the block's waves). */
-static int MERGE_K = 16, MOVE_COST = 40, NB = 4;
-
-static void block_merged(Ray **rays, int n, Stats *S)
-{
-    Ray *slot[256];
-    int len = n;
-    for (int i = 0; i < n; ++i) slot[i] = rays[i];
-    for (int it = 0;; ++it) {
-        if (MERGE_K && it && it % MERGE_K == 0) {
-            int m = 0;
-            for (int i = 0; i < len; ++i)
-                if (active(slot[i])) slot[m++] = slot[i];
-            if (m < len) S->valu += MOVE_COST * ((m + 63) / 64);
-            len = m;
-        }
-        int any_block = 0;
-        for (int w = 0; w * 64 < len; ++w) {
-            Ray **R = slot + w * 64;
-            const int nw = len - w * 64 < 64 ? len - w * 64 : 64;
-            int any = 0;
-            for (int i = 0; i < nw; ++i) any |= active(R[i]);
-            if (!any) continue;
-            any_block = 1;
-            S->iters += 1;
-            S->valu += M_LOOP + M_AENTRY;
-            int ns = 0, nadv = 0, npop = 0;
-            for (int i = 0; i < nw; ++i) {
-                Ray *r = R[i];
-                if (!active(r) || !r->stepping) continue;
-                ++ns; ++r->iters;
-                const int k = step_one(r);
-                if (k == 1) ++nadv;
-                else ++npop;
-            }
-            if (ns) S->valu += M_STEP;
-            if (nadv) S->valu += M_ADV;
-            if (npop) S->valu += M_POP;
-            int nb = 0, npres = 0;
-            for (int i = 0; i < nw; ++i) {
-                Ray *r = R[i];
-                if (!active(r) || r->stepping) continue;
-                ++nb; ++r->push;
-                const uint32_t ch = N[(size_t)(r->cur - 1) * 8 + ((r->idx ^ r->inv) & 7)];
-                if (!ch) { r->stepping = 1; continue; }
-                ++npres;
-                if (r->level == DEPTH) { r->level = DEPTH + 1; continue; }
-                r->stack[r->sp++] = r->cur; ++r->level; r->cur = ch; r->dim >>= 1;
-                uint32_t ni = 0;
-                for (int a = 0; a < 3; ++a) {
-                    const uint32_t mid = r->p[a] | r->dim;
-                    const int up = fmaf(u2f(mid), r->c[a], r->b[a]) >= u2f(r->t_min);
-                    ni |= up << a; if (up) r->p[a] = mid;
-                }
-                r->idx = ni;
-            }
-            if (nb) S->valu += M_BENTRY;
-            if (npres) S->valu += M_DESC;
-        }
-        if (!any_block) break;
-    }
-    for (int i = 0; i < n; ++i) S->rays_it += rays[i]->iters;
-    S->waves += n / 64.0;
-}
-
 static void camera(float yaw, float pitch, int W, int H, int col, int row, float *d)
 {
     /* tree_camera::update_position (ORT/test_och_h_octree.cpp:87-138), float math */
@@ -429,46 +359,13 @@ int main(int argc, char **argv)
     const int stride = argc > 4 ? atoi(argv[4]) : 1;
     SCHED = argc > 5 ? atoi(argv[5]) : 0;
     THRESH = argc > 6 ? atoi(argv[6]) : 0;
-    if (SCHED == 4) {   /* sched_sim nodes depth pitch stride 4 MERGE_K MOVE_COST NB */
-        MERGE_K = argc > 6 ? atoi(argv[6]) : 16;
-        MOVE_COST = argc > 7 ? atoi(argv[7]) : 40;
-        NB = argc > 8 ? atoi(argv[8]) : 4;
-    }
     const int W = 1920, H = 1080;
     const float o[3] = {1.5F, 1.5F, 1.5F};
     Stats S = {0};
     Ray R[64];
-    static Ray BR[256];
-    Ray *BP[256];
-    int tile = 0, in_block = 0;
+    int tile = 0;
     for (int ty = 0; ty < H / 8; ++ty)
         for (int tx = 0; tx < W / 8; ++tx, ++tile) {
-            if (SCHED == 4) {   /* NB consecutive tiles of a row form one block; every stride-th block */
-                if ((tile / NB) % stride) continue;
-                for (int l = 0; l < 64; ++l) {
-                    float d[3];
-                    camera(0.3F, pitch, W, H, tx * 8 + l % 8, ty * 8 + l / 8, d);
-                    Ray *r = &BR[in_block * 64 + l];
-                    ray_setup(r, o, d);
-                    const uint32_t ch = N[(size_t)(r->cur - 1) * 8 + ((r->idx ^ r->inv) & 7)];
-                    ++r->push;
-                    if (!ch) { r->stepping = 1; continue; }
-                    r->stack[r->sp++] = r->cur; ++r->level; r->cur = ch; r->dim >>= 1;
-                    uint32_t ni = 0;
-                    for (int a = 0; a < 3; ++a) {
-                        const uint32_t mid = r->p[a] | r->dim;
-                        const int up = fmaf(u2f(mid), r->c[a], r->b[a]) >= u2f(r->t_min);
-                        ni |= up << a; if (up) r->p[a] = mid;
-                    }
-                    r->idx = ni;
-                }
-                if (++in_block == NB) {
-                    for (int i = 0; i < NB * 64; ++i) BP[i] = &BR[i];
-                    block_merged(BP, NB * 64, &S);
-                    in_block = 0;
-                }
-                continue;
-            }
             if (tile % stride) continue;
             for (int l = 0; l < 64; ++l) {
                 float d[3];

@@ -67,14 +67,14 @@ def main():
         if order == 2:
             pool.plan_views(cams, 8, 0, 1)
         for _ in range(3):
-            pool.render_views_dev(cams, frames)
+            pool.render_views_dev(cams, frames, 8)
         kms = []
         for _ in range(5):
-            pool.render_views_dev(cams, frames)
+            pool.render_views_dev(cams, frames, 8)
             kms.append(pool.last_kernel_ms())
         stamps.zero_()
         pool.set_stamp_buffer(stamps, cap)
-        pool.render_views_dev(cams, frames)
+        pool.render_views_dev(cams, frames, 8)
         ms = pool.last_kernel_ms()
         pool.set_stamp_buffer(None, 0)
         st = stamps.cpu().numpy().reshape(-1, 4)[: len(tile_max)].astype(np.int64)
