@@ -196,10 +196,11 @@ struct och_gpu_pool {
     uint32_t plan_blocks[3] = {0, 0, 0};      // entries of the current plan (its launch's grid)
     int64_t plan_key[3][9] = {};
     // the primary plan's split form (OCH_OPT_SPLIT, plan_split): the heavy tiles'
-    // parts first, then the plan's other workgroups; valid with plan_key[0] while
-    // split_params matches the options it was made with
-    uint32_t *d_order_split = nullptr;
-    uint32_t split_alloc = 0, split_n = 0, split_extra = 0, split_tiles = 0;
+    // split waves first, then the plan's other workgroups, and the waves' task
+    // rows; valid with plan_key[0] while split_params matches the options it was
+    // made with
+    uint32_t *d_order_split = nullptr, *d_split_tasks = nullptr;
+    uint32_t split_alloc = 0, task_alloc = 0, split_n = 0, split_extra = 0, split_tiles = 0;
     int split_params[3] = {0, 0, 0};          // threshold, segments, level
     // row deal (och_gpu_set_row_deal): for frames of deal_h rows in chunks of
     // deal_chunk over deal_n shards, chunk g belongs to a chosen shard instead
@@ -225,7 +226,8 @@ struct och_gpu_pool {
         sc.order = nullptr;
         sc.order_n = 0;
         sc.cost = nullptr;
-        sc.split = 0;
+        sc.split_tasks = nullptr;
+        sc.split_level = 0;
         sc.split_extra = 0;
         sc.ev_start = nullptr;
         sc.ev_stop = nullptr;
@@ -662,6 +664,7 @@ OCH_API int och_gpu_pool_destroy(och_gpu_pool *p)
     for (uint32_t *o : p->d_order)
         if (o) (void)hipFree(o);
     if (p->d_order_split) (void)hipFree(p->d_order_split);
+    if (p->d_split_tasks) (void)hipFree(p->d_split_tasks);
     for (uint32_t *o : p->d_order_xcd)
         if (o) (void)hipFree(o);
     if (p->d_chunk_map) (void)hipFree(p->d_chunk_map);
@@ -1388,7 +1391,8 @@ int render_views(och_gpu_pool *p, const och_camera *cams, int n_views, uint32_t 
                 sc.order = p->d_order_split;
                 sc.order_n = p->split_n;
                 sc.split_extra = p->split_extra;
-                sc.split = (uint32_t)__builtin_ctz((unsigned)p->opt_split_segs) | ((uint32_t)p->opt_split_level << 8);
+                sc.split_tasks = p->d_split_tasks;
+                sc.split_level = (uint32_t)p->opt_split_level;
             }
         }
     }
@@ -1437,44 +1441,104 @@ void plan_shape(std::vector<uint32_t> &order, int mode)
     order.swap(out);
 }
 
-// The split form of a primary plan (OCH_OPT_SPLIT): the tiles
-// whose planning cost reaches opt_split % of the costliest one go first, each
-// as opt_split_segs parts (1 << 31 | part << 24 | tile: one wave walks 64 / S
-// of its rays, every ray over S lanes), then the plan's other workgroups in
-// its order.  Block 64 only (workgroup = tile), packed layout, tiles < 2^24,
-// and a split level above the leaves; otherwise no split plan.
-int plan_split(och_gpu_pool *p, const std::vector<uint32_t> &by_cost, const std::vector<uint32_t> &order,
-               const std::vector<uint32_t> &c)
+// A split tile's rays longer than this % of its longest walk over
+// OCH_OPT_SPLIT_SEGS lanes; the others take one lane and walk whole
+// (tools/split_model.c: 30 % keeps the critical path of splitting every ray
+// and adds almost no work).
+constexpr int kSplitRayPct = 30;
+
+// The split form of a primary plan (OCH_OPT_SPLIT).  The tiles
+// whose planning cost reaches opt_split % of the costliest one's are split:
+// one counting render gives every pixel's walked PUSHes, a tile's rays longer
+// than kSplitRayPct % of its longest get opt_split_segs lanes each (segment
+// lanes), the others one, and its rays are packed, costliest first, into
+// waves of 64 lanes with every lane of a ray in one wave (their records merge
+// through that wave's LDS).  Rows of d_split_tasks: the tile, then 64 lane
+// tasks (pixel | seg << 6 | log2(S) << 10, ~0 idle).  The order: the split
+// waves (1 << 31 | row), then the plan's other workgroups in its order.
+// Block 64 only (workgroup = tile), packed layout, tiles < 2^24, and a split
+// level above the leaves; otherwise no split plan.
+int plan_split(och_gpu_pool *p, const och::DevFrame &f, const std::vector<uint32_t> &by_cost,
+               const std::vector<uint32_t> &order, const std::vector<uint32_t> &c)
 {
     p->split_n = p->split_extra = p->split_tiles = 0;
     p->split_params[0] = p->split_params[1] = p->split_params[2] = 0;
     const uint32_t n = (uint32_t)order.size();
-    const int S = p->opt_split_segs;
+    const int S = p->opt_split_segs, log2s = __builtin_ctz((unsigned)S);
     if (p->opt_split <= 0 || p->opt_block != 64 || !p->dev().packed || p->opt_split_level >= p->depth || n == 0 ||
         n >= (1u << 24))
         return OCH_OK;
     const double thr = (double)c[by_cost[0]] * p->opt_split / 100.0;
+    std::vector<uint32_t> heavy_tiles;
+    const uint32_t cap = std::max(1u, n / 16);                  // a bound on the planner's work
+    for (uint32_t k = 0; k < n && k < cap && (double)c[by_cost[k]] >= thr; ++k) heavy_tiles.push_back(by_cost[k]);
+    // every pixel's walked PUSHes (one counting render of the planned frame)
+    const int W = f.cams[0].width, rows = f.slice_rows;
+    const size_t px = (size_t)f.n_views * rows * W;
+    uint16_t *d_push = nullptr;
+    OCH_HIP(hipMalloc(&d_push, px * 2));
+    std::vector<uint16_t> push(px);
+    och::Schedule sc = p->schedule();
+    sc.tile_order = 0;
+    hipError_t e = och::launch_render_push(p->dev(), f, sc, d_push, p->stream());
+    if (e == hipSuccess) e = hipMemcpyAsync(push.data(), d_push, px * 2, hipMemcpyDeviceToHost, p->stream());
+    if (e == hipSuccess) e = hipStreamSynchronize(p->stream());
+    (void)hipFree(d_push);
+    if (e != hipSuccess) return fail(OCH_E_HIP, "split plan: counting render: %s", hipGetErrorString(e));
+    const uint32_t tiles_x = (uint32_t)(W + 7) / 8, per_view = tiles_x * (uint32_t)((rows + 7) / 8);
+    std::vector<uint32_t> rowsv, split;                         // task rows (65 words each), order
     std::vector<uint8_t> heavy(n, 0);
-    std::vector<uint32_t> split;
-    const uint32_t cap = std::max(1u, n / 16);                  // a bound on the extra waves
-    for (uint32_t k = 0; k < n && k < cap && (double)c[by_cost[k]] >= thr; ++k) {
-        heavy[by_cost[k]] = 1;
-        for (int part = 0; part < S; ++part) split.push_back(0x80000000u | ((uint32_t)part << 24) | by_cost[k]);
+    for (uint32_t t : heavy_tiles) {
+        heavy[t] = 1;
+        const uint32_t view = t / per_view, tt = t % per_view, ty = tt / tiles_x, tx = tt % tiles_x;
+        int cnt[64], mx = 0;
+        for (int l = 0; l < 64; ++l) {
+            const uint32_t col = tx * 8 + (uint32_t)(l % 8), srow = ty * 8 + (uint32_t)(l / 8);
+            cnt[l] = col < (uint32_t)W && srow < (uint32_t)rows ? push[((size_t)view * rows + srow) * W + col] : -1;
+            mx = std::max(mx, cnt[l]);
+        }
+        // rays costliest first (a long ray by its segments' share), first fit into waves
+        std::vector<std::pair<int, int>> rays;                  // (estimated lane cost, pixel)
+        for (int l = 0; l < 64; ++l)
+            if (cnt[l] >= 0) rays.push_back({cnt[l] * 100 > kSplitRayPct * mx ? cnt[l] / S : cnt[l], l});
+        std::stable_sort(rays.begin(), rays.end(), [](const auto &a, const auto &b) { return a.first > b.first; });
+        std::vector<std::vector<uint32_t>> waves;
+        for (const auto &r : rays) {
+            const int l = r.second;
+            const bool long_ray = cnt[l] * 100 > kSplitRayPct * mx;
+            const size_t lanes = long_ray ? (size_t)S : 1;
+            size_t w = 0;
+            while (w < waves.size() && waves[w].size() + lanes > 64) ++w;
+            if (w == waves.size()) waves.emplace_back();
+            for (size_t s_ = 0; s_ < lanes; ++s_)
+                waves[w].push_back((uint32_t)l | (uint32_t)s_ << 6 | (uint32_t)(long_ray ? log2s : 0) << 10);
+        }
+        for (auto &w : waves) {
+            split.push_back(0x80000000u | (uint32_t)(rowsv.size() / 65));
+            rowsv.push_back(t);
+            for (size_t l = 0; l < 64; ++l) rowsv.push_back(l < w.size() ? w[l] : ~0u);
+        }
     }
-    const uint32_t n_heavy = (uint32_t)split.size() / (uint32_t)S;
+    if (heavy_tiles.empty()) return OCH_OK;
+    const uint32_t n_waves = (uint32_t)split.size();
     for (uint32_t b : order)
         if (!heavy[b]) split.push_back(b);
-    if (p->split_alloc < split.size()) {
-        if (p->d_order_split) OCH_HIP(hipFree(p->d_order_split));
-        p->d_order_split = nullptr;
-        p->split_alloc = 0;
-        OCH_HIP(hipMalloc(&p->d_order_split, split.size() * 4));
-        p->split_alloc = (uint32_t)split.size();
-    }
-    OCH_HIP(hipMemcpy(p->d_order_split, split.data(), split.size() * 4, hipMemcpyHostToDevice));
+    auto upload = [&](uint32_t *&d, uint32_t &alloc, const std::vector<uint32_t> &v) -> hipError_t {
+        if (alloc < v.size()) {
+            if (d) (void)hipFree(d);
+            d = nullptr;
+            alloc = 0;
+            const hipError_t me = hipMalloc(&d, v.size() * 4);
+            if (me != hipSuccess) return me;
+            alloc = (uint32_t)v.size();
+        }
+        return hipMemcpy(d, v.data(), v.size() * 4, hipMemcpyHostToDevice);
+    };
+    OCH_HIP(upload(p->d_order_split, p->split_alloc, split));
+    OCH_HIP(upload(p->d_split_tasks, p->task_alloc, rowsv));
     p->split_n = (uint32_t)split.size();
-    p->split_extra = n_heavy * (uint32_t)(S - 1);
-    p->split_tiles = n_heavy;
+    p->split_extra = n_waves - (uint32_t)heavy_tiles.size();
+    p->split_tiles = (uint32_t)heavy_tiles.size();
     p->split_params[0] = p->opt_split;
     p->split_params[1] = S;
     p->split_params[2] = p->opt_split_level;
@@ -1576,7 +1640,7 @@ OCH_API int och_gpu_plan_views(och_gpu_pool *p, const och_camera *cams, int n_vi
         OCH_HIP(hipMemcpy(p->d_order[which], order.data(), (size_t)n_blocks * 4, hipMemcpyHostToDevice));
         OCH_HIP(hipMemcpy(p->d_order_xcd[which], grouped.data(), (size_t)n_blocks * 4, hipMemcpyHostToDevice));
         if (which == 0)
-            if (int ss = plan_split(p, by_cost, order, c)) return ss;
+            if (int ss = plan_split(p, f, by_cost, order, c)) return ss;
         const int64_t key[9] = {W, H, n_views, row_chunk, shard, n_shards, p->opt_block,
                                 which ? p->opt_bounce_compact : 0, dealt ? (int64_t)p->deal_serial : 0};
         std::memcpy(p->plan_key[which], key, sizeof key);

@@ -157,10 +157,12 @@ struct Schedule {
     uint32_t order_n;       // entries in *order: a launch whose grid differs runs in natural order
     uint32_t *cost;         // optional per-workgroup duration output (the planning launch)
     // A split plan (OCH_OPT_SPLIT; camera renders, packed layout, block 64):
-    // order then lists the grid's workgroups with each heavy tile replaced by
-    // its parts (1 << 31 | part << 24 | tile), order_n = grid + split_extra.
-    // split = log2(segments) | split level << 8, 0 = none.
-    uint32_t split;
+    // order lists the grid's workgroups with the heavy tiles replaced by split
+    // waves (1 << 31 | row of split_tasks), order_n = grid + split_extra;
+    // split_tasks rows: the tile, then 64 lane tasks (och_kernels.hip
+    // split_tile).  split_tasks = null: no split.
+    const uint32_t *split_tasks;
+    uint32_t split_level;
     uint32_t split_extra;
     hipEvent_t ev_start;    // optional: recorded by the traversal kernel's own dispatch (hipExtLaunchKernel)
     hipEvent_t ev_stop;
@@ -187,6 +189,9 @@ hipError_t launch_trace_bounce_batch(const DevPool &p, const float *origin, int 
 hipError_t launch_render_bounce(const DevPool &p, const DevFrame &f, const Schedule &sc, hipStream_t stream);
 hipError_t launch_raygen(const och_camera &cam, float *dirs, hipStream_t stream);
 hipError_t launch_render(const DevPool &p, const DevFrame &f, const Schedule &sc, hipStream_t stream);
+// The split planner's counting render: each pixel's walked PUSH count (16 bits)
+// into push, indexed as the frame's slices.
+hipError_t launch_render_push(const DevPool &p, const DevFrame &f, const Schedule &sc, uint16_t *push, hipStream_t stream);
 // Indexed-colour frames (OCH_CODE_*): render into f.codes, and turn gathered
 // code slices into RGBA8 frames through a 256-entry table.
 hipError_t launch_render_codes(const DevPool &p, const DevFrame &f, const Schedule &sc, bool bounce, hipStream_t stream);

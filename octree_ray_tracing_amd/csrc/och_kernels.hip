@@ -857,7 +857,7 @@ struct TiledArraySource {
 // output token is view * slice_pixels + slice pixel.
 struct CameraSource {
     static constexpr bool kProvenMiss = true;     // get_wave_culled runs camera_proven_miss when P.cam_cull
-    static constexpr bool kSplittable = true;     // heavy tiles split over lanes (kSplit launches)
+    static constexpr bool kSplittable = true;     // heavy tiles' long rays split over lanes (kSplit launches)
     och_camera cam[kMaxViews];
     CameraView view[kMaxViews];
     int32_t n_views, row_chunk, shard, n_shards, slice_rows, width, height, order;
@@ -949,6 +949,13 @@ struct HitSink {
         t[i] = h.t;
         if (kCount) push[i] = h.push;
     }
+};
+
+// Walked PUSH counts per pixel of a camera launch, saturated to 16 bits: the
+// split planner's per-ray costs (och_api.cpp plan_split).
+struct PushSink {
+    uint16_t *push;
+    __device__ __forceinline__ void put(uint32_t i, const Hit &h) const { push[i] = (uint16_t)min(h.push, 65535u); }
 };
 
 // trace_pixel's colour choice (ORT/test_och_h_octree.cpp:76-84) as olc::Pixel RGBA8.
@@ -1075,6 +1082,59 @@ __device__ __forceinline__ void stamp(uint64_t *stamps, uint32_t cap, uint64_t t
 
 // ---------------------------------------------------------------- kernels
 
+// A heavy tile's rays, the long ones walked by S lanes each (kSplit launches,
+// OCH_OPT_SPLIT).  The workgroup is one wave of lane tasks from
+// the plan's task table (och_api.cpp plan_split): word 0 the tile, then per
+// lane pixel | seg << 6 | log2(S) << 10, or ~0 for an idle lane.  A lane walks
+// its ray's whole walk above the split level but enters only the present
+// split-level cells (segments) whose ordinal is seg modulo S (S = 1: all, the
+// plain walk).  The ray's record is the HIT of the lowest segment ordinal any
+// of its lanes found, or the MISS -- the full walk's record, bit for bit,
+// because the walk above the split level does not depend on what it does
+// inside a segment.  The lanes agree through one LDS word per pixel (atomic
+// min of ordinal << 6 | lane); the winning lane stores its record, or, with no
+// HIT, the ray's segment-0 lane stores the MISS.
+template <class Src, class Sink, int kPacked>
+__device__ __forceinline__ void split_tile(const DevPool &P, const Src &S, const Sink &K, uint32_t ent,
+                                           const uint32_t *__restrict__ tasks, uint32_t level, uint32_t *lds_stack)
+{
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t *w = tasks + (size_t)(ent & 0x7FFFFFFFu) * 65u;
+    const uint32_t tile = __builtin_amdgcn_readfirstlane(w[0]);
+    const uint32_t task = w[1u + lane];
+    const uint32_t pix = task & 63u, seg = (task >> 6) & 15u, log2s = (task >> 10) & 7u;
+    const uint32_t stack = stack_column(lds_stack, P.depth);
+    float o[3], d[3];
+    uint32_t out = 0, key = ~0u;
+    bool miss = false;
+    Hit h{OCH_EXIT, 0u, P.miss_bits, 0u};
+    const bool valid = task != ~0u && tile * 64u + pix < S.count() &&
+                       S.get_wave_culled(tile * 64u, pix, P, P.cull != 0, o, d, out, miss);
+    if (valid && !miss) {
+        Ray r;
+        r.split_dim = 1u << (23u - level);
+        r.split_mask = (1u << log2s) - 1u;
+        r.split_seg = seg;
+        r.ord = 0;
+        r.hit_ord = ~0u;
+        ray_trace<kPacked, false, true, kAsmLoad, true>(r, P, o, d, stack, blockDim.x,
+                                                       !(Src::kProvenMiss && P.cam_cull));
+        h = ray_result<kPacked, kAsmLoad>(r, P);
+        key = r.dim > (1u << 22) ? ~0u : r.hit_ord;                         // a MISS loses to any HIT
+    }
+    // one word per pixel: slot 0 of lane `pixel`'s stack column (the walks are over)
+    const uint32_t best0 = (stack - (uint32_t)(uintptr_t)(const lds_word *)lds_stack) / 4u - threadIdx.x;
+    __syncthreads();
+    lds_stack[best0 + lane] = ~0u;
+    __syncthreads();
+    if (key != ~0u) atomicMin(&lds_stack[best0 + pix], (key << 6) | lane);   // ordinals < 2^26
+    __syncthreads();
+    if (valid) {
+        const uint32_t b = lds_stack[best0 + pix];
+        if (b == ~0u ? seg == 0u : (b & 63u) == lane) K.put(out, h);
+    }
+}
+
 // Workgroups are dealt round-robin over the 8 XCDs (blocks b, b + 8, ... share
 // one XCD and its L2).  Remap so each XCD receives runs of `group`
 // consecutive logical blocks -- one supertile of neighbouring rays, which walk
@@ -1097,69 +1157,19 @@ __device__ __forceinline__ uint32_t xcd_block(uint32_t b, uint32_t nb, uint32_t 
 // (MI355X_MICROARCH.md, residency; the compiler's occupancy note says 8 there), and 8
 // give +5 % sustained.  tools/isa_check.py check 4 holds every
 // traversal kernel to 8 waves per SIMD.
-// A heavy tile's rays, each walked by S lanes (kSplit launches, OCH_OPT_SPLIT;
-// DESIGN.md §4e).  Workgroup = one wave = 64 / S rays of the tile (part
-// `part` of its S parts) x S segment lanes: lane = seg * (64 / S) + ray.  A
-// lane walks the whole ray above the split level but enters only the present
-// split-level cells (segments) whose ordinal is its seg modulo S; the ray's
-// record is the HIT of the lowest segment ordinal any of its lanes found, or
-// the MISS -- the full walk's record, bit for bit, because the walk above the
-// split level does not depend on what it does inside a segment.  The lanes
-// of a ray agree through lane swizzles; segment 0's lane stores the record.
-template <class Src, class Sink, int kPacked>
-__device__ __forceinline__ void split_tile(const DevPool &P, const Src &S, const Sink &K, uint32_t ent, uint32_t split,
-                                           uint32_t *lds_stack)
-{
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t log2s = split & 0xFFu, level = (split >> 8) & 0xFFu;
-    const uint32_t per = 64u >> log2s;                                      // rays per wave
-    const uint32_t tile = ent & 0xFFFFFFu, part = (ent >> 24) & 0x7Fu;
-    const uint32_t ray = lane & (per - 1u), seg = lane >> (6u - log2s);
-    const uint32_t pix = part * per + ray;                                  // pixel of the 8x8 tile
-    float o[3], d[3];
-    uint32_t out = 0, key = ~0u;
-    bool miss = false;
-    Hit h{OCH_EXIT, 0u, P.miss_bits, 0u};
-    const bool valid = tile * 64u + pix < S.count() &&
-                       S.get_wave_culled(tile * 64u, pix, P, P.cull != 0, o, d, out, miss);
-    if (valid && !miss) {
-        Ray r;
-        r.split_dim = 1u << (23u - level);
-        r.split_mask = (1u << log2s) - 1u;
-        r.split_seg = seg;
-        r.ord = 0;
-        r.hit_ord = ~0u;
-        ray_trace<kPacked, false, true, kAsmLoad, true>(r, P, o, d, stack_column(lds_stack, P.depth), blockDim.x,
-                                                       !(Src::kProvenMiss && P.cam_cull));
-        h = ray_result<kPacked, kAsmLoad>(r, P);
-        key = r.dim > (1u << 22) ? ~0u : r.hit_ord;                         // a MISS loses to any HIT
-    }
-    // the ray's lanes are ray + k * per: keep the lowest segment's HIT
-    for (uint32_t off = per; off < 64u; off <<= 1) {
-        const uint32_t k2 = (uint32_t)__shfl_xor((int)key, (int)off);
-        const int32_t d2 = __shfl_xor(h.dir, (int)off);
-        const uint32_t v2 = (uint32_t)__shfl_xor((int)h.voxel, (int)off);
-        const uint32_t t2 = (uint32_t)__shfl_xor((int)h.t, (int)off);
-        if (k2 < key) {
-            key = k2;
-            h.dir = d2;
-            h.voxel = v2;
-            h.t = t2;
-        }
-    }
-    if (valid && seg == 0) K.put(out, h);
-}
-
+// kSplit: order entries with bit 31 set are split waves (split_tile): their
+// task table row, split_level the split's level.
 template <class Src, class Sink, int kPacked, bool kCount, bool kSplit>
 __global__ __attribute__((amdgpu_num_sgpr(80))) void k_trace_grid(DevPool P, Src S, Sink K, uint32_t xcd_group, const uint32_t *__restrict__ order,
-                             uint32_t *__restrict__ cost, uint64_t *stamps, uint32_t stamp_cap, uint32_t split)
+                             uint32_t *__restrict__ cost, uint64_t *stamps, uint32_t stamp_cap,
+                             const uint32_t *__restrict__ split_tasks, uint32_t split_level)
 {
     extern __shared__ uint32_t lds_stack[];
     const uint64_t t0 = stamps ? realtime() : 0;
     const uint64_t c0 = cost ? __builtin_amdgcn_s_memtime() : 0;
-    uint32_t blk = order ? order[blockIdx.x] : xcd_block(blockIdx.x, gridDim.x, xcd_group);
-    if (kSplit && (blk >> 31)) {                    // a part of a heavy tile (wave-uniform)
-        split_tile<Src, Sink, kPacked>(P, S, K, blk, split, lds_stack);
+    const uint32_t blk = order ? order[blockIdx.x] : xcd_block(blockIdx.x, gridDim.x, xcd_group);
+    if (kSplit && (blk >> 31)) {                    // a split wave (wave-uniform)
+        split_tile<Src, Sink, kPacked>(P, S, K, blk, split_tasks, split_level, lds_stack);
         if (stamps) stamp(stamps, stamp_cap, t0, 64);
         return;
     }
@@ -1413,16 +1423,18 @@ hipError_t launch_as(const DevPool &p, const Src &s, const Sink &k, uint32_t n, 
     if constexpr (Src::kSplittable && kPacked && !kCount) {
         // a split plan (och_api.cpp plan_split): this grid's workgroups, the
         // heavy ones replaced by their parts; one wave per workgroup
-        if (sc.split && sc.order && block == 64 && sc.order_n == grid + sc.split_extra) {
+        if (sc.split_tasks && sc.order && block == 64 && sc.order_n == grid + sc.split_extra) {
             OCH_LAUNCH_TIMED(sc, (k_trace_grid<Src, Sink, kPacked, kCount, true>), dim3(sc.order_n), dim3(block), lds,
-                             stream, p, s, k, 0u, sc.order, sc.cost, sc.stamps, sc.stamp_cap, sc.split);
+                             stream, p, s, k, 0u, sc.order, sc.cost, sc.stamps, sc.stamp_cap, sc.split_tasks,
+                             sc.split_level);
             return hipGetLastError();
         }
     }
     // a plan is a permutation of exactly this grid's workgroups; any other
     // (stale or for another block size) would index past it
     OCH_LAUNCH_TIMED(sc, (k_trace_grid<Src, Sink, kPacked, kCount, false>), dim3(grid), dim3(block), lds, stream, p, s,
-                     k, xcd_group, sc.order_n == grid ? sc.order : nullptr, sc.cost, sc.stamps, sc.stamp_cap, 0u);
+                     k, xcd_group, sc.order_n == grid ? sc.order : nullptr, sc.cost, sc.stamps, sc.stamp_cap, nullptr,
+                     0u);
     return hipGetLastError();
 }
 
@@ -1554,6 +1566,15 @@ hipError_t launch_render(const DevPool &p, const DevFrame &f, const Schedule &sc
     const CameraSource src = camera_source(p, f, sc);
     return launch<CameraSource, FrameSink, false>(p, src, FrameSink{f.out, f.palette, f.n_voxels}, src.count(), sc,
                                                   stream, sc.tile_order == 1 ? 64u * 64u : 0u);
+}
+
+hipError_t launch_render_push(const DevPool &p, const DevFrame &f, const Schedule &sc, uint16_t *push, hipStream_t stream)
+{
+    if (f.n_views < 1 || f.n_views > kMaxViews) return hipErrorInvalidValue;
+    DevPool q = p;
+    q.cull = 2;                                 // a counting launch culls only at 2: the PUSHes the render walks
+    const CameraSource src = camera_source(q, f, sc);
+    return launch<CameraSource, PushSink, true>(q, src, PushSink{push}, src.count(), sc, stream);
 }
 
 hipError_t launch_render_bounce(const DevPool &p, const DevFrame &f, const Schedule &sc, hipStream_t stream)

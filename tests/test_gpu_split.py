@@ -1,7 +1,7 @@
-"""Heavy-tile split (OCH_OPT_SPLIT): the planned costliest tiles
-walk each ray over S lanes, a lane entering only every S-th present cell of
-the split level along the ray, and the ray keeps the hit of the lowest such
-cell.  The records must be the full walk's (ORT/och_h_octree.h:292-447) bit
+"""Heavy-tile split (OCH_OPT_SPLIT): the planned costliest
+tiles walk their long rays over S lanes each, a lane entering only every S-th
+present cell of the split level along the ray, and the ray keeps the hit of
+the lowest such cell.  The records must be the full walk's (ORT/och_h_octree.h:292-447) bit
 for bit: frames against the oracle's at the bench's configs[2] instance, and
 against the unsplit launch for every segment count, split levels from the
 root's children to just above the leaves, a threshold that splits the most
@@ -67,15 +67,16 @@ def test_split_bench_instance_d12_against_oracle(ort, O, d12):
 @pytest.mark.parametrize("segs", [2, 4, 8, 16])
 @pytest.mark.parametrize("level", [1, 3, 6, 9])
 def test_split_levels_and_segments_d10(ort, d10, segs, level):
-    """Threshold 1 %: the plan splits as many tiles as it may (a sixteenth of
-    the grid), so most terrain tiles take the split walk; every level from the
-    root's children to just above the leaves, every segment count."""
+    """Threshold 1 %: the plan splits every tile that walks at all, up to a
+    sixteenth of the grid, so most terrain tiles take the split walk; every
+    level from the root's children to just above the leaves, every segment
+    count."""
     pool = ort.HOctree(d10.nodes, d10.root, 10, device=0)
     pool.set_palette(ort.VoxelData().get_colours())
     cams = [ort.camera(ORIGIN, 0.3, p, 1.25, 1024, 576) for p in PITCHES]
     want = frames_of(pool, cams)
     got = frames_of(pool, cams, {"split": 1, "split_segs": segs, "split_level": level})
-    assert pool.get_option("split_tiles") == (2 * 128 * 72) // 16
+    assert 100 < pool.get_option("split_tiles") <= (2 * 128 * 72) // 16
     assert np.array_equal(got, want)
     pool.close()
 

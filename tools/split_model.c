@@ -23,9 +23,11 @@
  * Build: gcc -O2 -msse2 -o /tmp/split_model tools/split_model.c -lm -lpthread
  * Input: raw uint32 nodes[n][8] of a 1-based h_octree pool, root 1, e.g.
  *   ort.build_terrain(12).nodes.astype(np.uint32).tofile("d12_nodes.bin")
- * Usage: split_model nodes.bin depth pitch L S [threads [early]]
+ * Usage: split_model nodes.bin depth pitch L S [threads [early [theta]]]
  *   early 1: a lane stops at the first segment past the ray's hit (ideal: as if
- *   the lane that finds the hit told the others at once). */
+ *   the lane that finds the hit told the others at once).
+ *   theta: the per-ray variant splits only the rays of a split tile longer than
+ *   theta % of its longest, the others walking whole on one lane (default 50). */
 #include <immintrin.h>
 #include <math.h>
 #include <pthread.h>
@@ -38,7 +40,7 @@ static inline uint32_t f2u(float f) { uint32_t u; memcpy(&u, &f, 4); return u; }
 static inline float u2f(uint32_t u) { float f; memcpy(&f, &u, 4); return f; }
 
 static const uint32_t *N;
-static int DEPTH, LEVEL, SEGS, EARLY;
+static int DEPTH, LEVEL, SEGS, EARLY, THETA;
 
 typedef struct { int32_t dir; uint32_t voxel, t; int ord; int push; } Rec;
 
@@ -133,6 +135,8 @@ enum { W = 1920, H = 1080, TX = W / 8, TY = H / 8 };
 static float PITCH;
 static int *FULL, *SPLIT;        /* per tile: longest lane, full walk / split (max over its S x 64 lane tasks) */
 static long *SPLIT_WORK;         /* per tile: sum over the S waves of their longest lane */
+static int *RSPLIT;              /* per tile, per-ray split: longest task */
+static long *RSPLIT_WORK;        /* per tile, per-ray split: waves' longest tasks summed (tasks packed longest first) */
 static long BAD, RAYS;
 static int NEXT;
 static pthread_mutex_t MU = PTHREAD_MUTEX_INITIALIZER;
@@ -142,6 +146,7 @@ static void *worker(void *arg)
     (void)arg;
     const float o[3] = {1.5F, 1.5F, 1.5F};
     Rec seg[64];
+    int full_push[64], seg_push[64][16];
     for (;;) {
         const int tile = __atomic_fetch_add(&NEXT, 1, __ATOMIC_RELAXED);
         if (tile >= TX * TY) return NULL;
@@ -154,10 +159,12 @@ static void *worker(void *arg)
             camera(0.3F, PITCH, W, H, tx * 8 + l % 8, ty * 8 + l / 8, d);
             Rec full;
             walk(o, d, -1, -1, &full);
+            full_push[l] = full.push;
             if (full.push > full_max) full_max = full.push;
             int best = -1;
             for (int s = 0; s < SEGS; ++s) {
                 walk(o, d, s, EARLY ? full.ord : -1, &seg[s]);
+                seg_push[l][s] = seg[s].push;
                 if (seg[s].push > split_max) split_max = seg[s].push;
                 const int w = l / (64 / SEGS);
                 if (seg[s].push > wave_max[w]) wave_max[w] = seg[s].push;
@@ -168,6 +175,23 @@ static void *worker(void *arg)
         }
         long work = 0;
         for (int w = 0; w < SEGS; ++w) work += wave_max[w];
+        /* per-ray split: rays longer than THETA % of the tile's longest take SEGS lanes */
+        {
+            int task[64 * 16], nt = 0, lmax = 0;
+            for (int l = 0; l < 64; ++l) {
+                if (full_push[l] * 100 > THETA * full_max) {
+                    for (int s = 0; s < SEGS; ++s) task[nt++] = seg_push[l][s];
+                } else
+                    task[nt++] = full_push[l];
+            }
+            /* longest first, 64 to a wave */
+            for (int i = 1; i < nt; ++i) { int v = task[i], j = i; while (j > 0 && task[j - 1] < v) { task[j] = task[j - 1]; --j; } task[j] = v; }
+            long rw = 0;
+            for (int i = 0; i < nt; i += 64) rw += task[i];
+            lmax = task[0];
+            RSPLIT[tile] = lmax;
+            RSPLIT_WORK[tile] = rw;
+        }
         FULL[tile] = full_max;
         SPLIT[tile] = split_max;
         SPLIT_WORK[tile] = work;
@@ -198,10 +222,13 @@ int main(int argc, char **argv)
     SEGS = atoi(argv[5]);
     const int threads = argc > 6 ? atoi(argv[6]) : 8;
     EARLY = argc > 7 ? atoi(argv[7]) : 0;
+    THETA = argc > 8 ? atoi(argv[8]) : 50;
     if (LEVEL < 1 || LEVEL >= DEPTH || SEGS < 1 || 64 % SEGS) { fprintf(stderr, "need 1 <= L < depth, S | 64\n"); return 2; }
     FULL = calloc(TX * TY, sizeof *FULL);
     SPLIT = calloc(TX * TY, sizeof *SPLIT);
     SPLIT_WORK = calloc(TX * TY, sizeof *SPLIT_WORK);
+    RSPLIT = calloc(TX * TY, sizeof *RSPLIT);
+    RSPLIT_WORK = calloc(TX * TY, sizeof *RSPLIT_WORK);
     pthread_t th[256];
     for (int k = 0; k < threads; ++k) pthread_create(&th[k], NULL, worker, NULL);
     for (int k = 0; k < threads; ++k) pthread_join(th[k], NULL);
@@ -230,8 +257,15 @@ int main(int argc, char **argv)
                 if (FULL[t] > crit) crit = FULL[t];
             }
         }
-        printf("%s{\"T\": %d, \"tiles_split\": %d, \"critical_path\": %d, \"work_vs_unsplit\": %.4f}", k ? ", " : "",
-               Ts[k], n, crit, (double)work / base);
+        long rwork = 0;
+        int rcrit = 0;
+        for (int t = 0; t < TX * TY; ++t) {
+            if (FULL[t] > Ts[k]) { rwork += RSPLIT_WORK[t]; if (RSPLIT[t] > rcrit) rcrit = RSPLIT[t]; }
+            else { rwork += FULL[t]; if (FULL[t] > rcrit) rcrit = FULL[t]; }
+        }
+        printf("%s{\"T\": %d, \"tiles_split\": %d, \"critical_path\": %d, \"work_vs_unsplit\": %.4f, "
+               "\"per_ray_critical_path\": %d, \"per_ray_work_vs_unsplit\": %.4f}", k ? ", " : "",
+               Ts[k], n, crit, (double)work / base, rcrit, (double)rwork / base);
     }
     printf("]}\n");
     return BAD != 0;
