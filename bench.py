@@ -549,6 +549,9 @@ def group_bench(a):
         for kv in a.opt:
             k, v = kv.split("=")
             g.set_option(k, int(v))
+        if not any(kv.startswith("split") for kv in a.opt):      # as the rank path: by world size
+            for k, v in ort.split_defaults(n).items():
+                g.set_option(k, v)
         g.plan(cams, a.row_chunk)
 
         def window(steps):
@@ -863,6 +866,8 @@ def main():
                     help="N > 1: every rank all-gathers the frame's codes; 'display' = only rank 0 (the display) "
                          "expands them to RGBA8 frames, 'all' = every rank does")
     ap.add_argument("--no-cull-off", action="store_true", help="skip the cull-off window (value_cull_off)")
+    ap.add_argument("--no-split-arm", action="store_true",
+                    help="N = 1: skip the heavy-tile split arm (lone launch, window and sustained with the split on)")
     ap.add_argument("--deal", choices=("cost", "count", "rr"), default="count",
                     help="N > 1: row chunks dealt by their cost in one timed render on rank 0 (och_gpu_chunk_costs "
                          "+ och_deal_chunks), by count (rank 0 at --display-weight), or round-robin")
@@ -1024,6 +1029,12 @@ def main():
     # frames identical), so no frame ends on a few late grazing tiles.
     if not any(kv.startswith("tile_order=") for kv in a.opt):
         pool.set_option("tile_order", 2)
+    # The heavy-tile split by world size (ort.split_defaults, DESIGN.md §4d:
+    # on where a rank's launches end on their tails), unless --opt sets it;
+    # set before planning, which makes the split plan.
+    if not any(kv.startswith("split") for kv in a.opt):
+        for k, v in ort.split_defaults(world).items():
+            pool.set_option(k, v)
     if world >= 8 and not any(kv.startswith("plan=") for kv in a.opt):
         # N = 8 (proxy, 6 frames on 8 queues, profiles/r03/ab/plan_n8/): costliest-first
         # 204-210 G over 20 steps against 200-202 G for the 10 % shape (sustained
@@ -1445,11 +1456,13 @@ def main():
             raise SystemExit(f"exchange check failed: {exchange_check}")
 
     # Frame latency: the render launch alone on an otherwise idle GPU.
-    lat = []
-    for k in range(max(a.warmup, 1) + 5):
-        step(0, lat if k >= max(a.warmup, 1) else None)
-        torch.cuda.synchronize()
-    latency_ms = float(np.median([x.elapsed_time(y) for x, y in lat]))
+    def lone_latency():
+        lat = []
+        for k in range(max(a.warmup, 1) + 5):
+            step(0, lat if k >= max(a.warmup, 1) else None)
+            torch.cuda.synchronize()
+        return float(np.median([x.elapsed_time(y) for x, y in lat]))
+    latency_ms = lone_latency()
     if trace_only is not None:
         # per ray against a lone render launch (both views, raygen + trace + shade)
         lone = latency_ms / (W * H * len(cams))
@@ -1535,6 +1548,38 @@ def main():
         pool.set_option("cull", c_prev)
         if pool.get_option("tile_order") >= 2:
             pool.plan_views(cams, a.row_chunk, rank, world)
+        pool.set_stream(stream)
+
+    # The heavy-tile split beside the headline at N = 1, where it
+    # is off by default: a lone frame no longer waits on its few longest rays,
+    # at a cost in throughput (the split waves walk the coarse levels once per
+    # lane).  Same cameras, the same window; its last frames must equal the
+    # headline's.
+    split_arm = None
+    if world == 1 and direct and not a.no_split_arm and pool.get_option("split") == 0:
+        sopts = ort.split_defaults(8)
+        for k, v in sopts.items():
+            pool.set_option(k, v)
+        pool.plan_views(cams, a.row_chunk, 0, 1)
+        lat_split = lone_latency()
+        warm(a.warmup, events=False)
+        el_s = timed(a.steps, stage="window (split)")
+        last_s = sfs[(a.steps - 1) % len(sfs)].frames.cpu().numpy()
+        sus_s = None
+        if sustained is not None:
+            sus_s = round(statistics.median([W * H * len(cams) * sustained["steps_per_run"] /
+                                             timed(sustained["steps_per_run"], stage="window (split sustained)") / 1e6
+                                             for _ in range(3)]), 2)
+        split_arm = {"options": sopts, "tiles_split": pool.get_option("split_tiles"),
+                     "kernel_ms_serial": round(lat_split, 4), "value": round(total_rays / el_s / 1e6, 2),
+                     "ms_per_step": round(el_s / a.steps * 1e3, 4), "sustained": sus_s,
+                     "frames_equal_headline": None if frames_host is None else bool(np.array_equal(last_s, frames_host)),
+                     "note": "heavy-tile split on (the N >= 8 default): the planned costliest tiles walk their long "
+                             "rays over 4 lanes each; kernel_ms_serial = a lone two-view launch"}
+        if split_arm["frames_equal_headline"] is False:
+            raise SystemExit("split frames differ from the headline's")
+        pool.set_option("split", 0)
+        pool.plan_views(cams, a.row_chunk, 0, 1)
         pool.set_stream(stream)
 
     # A moving camera (N = 1): the bench's cameras pan by dyaw per step, so no
@@ -1816,13 +1861,14 @@ def main():
                                   else "every rank shades them to RGBA8")),
                        "frames": ("rgba8 frames written by the fused launch (no exchange at N = 1)" if direct else
                                   "indexed-colour codes, shaded after the exchange" if indexed else "rgba8 slices"),
-                       "options": {k: pool.get_option(k) for k in pool.OPTIONS}},
+                       "options": {k: pool.get_option(k) for k in (*pool.OPTIONS, *pool.READ_ONLY)}},
             "roofline": roof,
             "cpu_baseline": cpu,
             "parity": parity,
             "sustained": sustained,
             "value_cull_off": None if cull_off is None else cull_off["value"],
             "cull_off": cull_off,
+            **({"split": split_arm} if split_arm else {}),
             **({"moving_camera": moving} if moving else {}),
             "walked_rays_per_s": round(value * (1 - culled / rays_rank), 2),
             "walked_rays_note": "Mrays/s of the rays that walk the DAG (value x (1 - culled_frac)); the "

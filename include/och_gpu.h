@@ -190,7 +190,7 @@ typedef enum och_option {
                                   2, block 64, packed layout): the planned tiles whose cost reaches this % of the
                                   costliest one's walk each ray over OCH_OPT_SPLIT_SEGS lanes, a lane entering
                                   only every S-th present cell of level OCH_OPT_SPLIT_LEVEL along the ray, the
-                                  lowest one's hit kept -- the same records (DESIGN.md section 4e), a lone
+                                  lowest one's hit kept -- the same records (DESIGN.md section 4d), a lone
                                   frame no longer waiting on its few longest rays.  0 = off */
     OCH_OPT_SPLIT_SEGS = 15,   /* lanes per ray of a split tile: 2, 4 (default), 8 or 16 */
     OCH_OPT_SPLIT_LEVEL = 16,  /* the level whose cells are the split's segments (default 6) */

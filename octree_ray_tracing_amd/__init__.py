@@ -11,9 +11,9 @@ from .builder import NodePool, build_terrain, occupied_box, pack_pool
 from .editor import Editor
 from .frame import FrameGroup, RcclComm, ShardedFrame, ShardedSteps
 from .tracer import (Direction, GpuPool, HOctree, Octree, camera, deal_chunks, display_weight, device_count, device_list, host_rcp_lut,
-                     rcp_from_lut, rcp_lut_error, shard_rows)
+                     rcp_from_lut, rcp_lut_error, shard_rows, split_defaults)
 from .voxels import VoxelData, VoxelDataError
 
 __all__ = ["OchError", "library_path", "load", "NodePool", "build_terrain", "occupied_box", "pack_pool", "Editor", "FrameGroup", "RcclComm", "ShardedFrame", "ShardedSteps", "Direction", "GpuPool",
-           "HOctree", "Octree", "camera", "deal_chunks", "display_weight", "device_count", "device_list", "host_rcp_lut", "rcp_from_lut", "rcp_lut_error", "shard_rows",
+           "HOctree", "Octree", "camera", "deal_chunks", "display_weight", "device_count", "device_list", "host_rcp_lut", "rcp_from_lut", "rcp_lut_error", "shard_rows", "split_defaults",
            "VoxelData", "VoxelDataError"]

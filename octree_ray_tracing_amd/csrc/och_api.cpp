@@ -1447,7 +1447,7 @@ void plan_shape(std::vector<uint32_t> &order, int mode)
 // and adds almost no work).
 constexpr int kSplitRayPct = 30;
 
-// The split form of a primary plan (OCH_OPT_SPLIT; DESIGN.md §4e).  The tiles
+// The split form of a primary plan (OCH_OPT_SPLIT; DESIGN.md §4d).  The tiles
 // whose planning cost reaches opt_split % of the costliest one's are split:
 // one counting render gives every pixel's walked PUSHes, a tile's rays longer
 // than kSplitRayPct % of its longest get opt_split_segs lanes each (segment

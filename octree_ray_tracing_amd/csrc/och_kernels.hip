@@ -495,7 +495,7 @@ __device__ __forceinline__ void ray_push_descend(Ray &r, const DevPool &P, uint3
         // A present cell of the split level due to PUSH is segment ord of the
         // walk; another lane's segment counts as empty here (the walk above
         // the split level does not depend on what happens inside a segment,
-        // DESIGN.md §4e).
+        // DESIGN.md §4d).
         if (r.mode != kStepping && present && r.dim == r.split_dim) {
             const bool mine = (r.ord & r.split_mask) == r.split_seg;
             r.hit_ord = mine ? r.ord : r.hit_ord;
@@ -1083,7 +1083,7 @@ __device__ __forceinline__ void stamp(uint64_t *stamps, uint32_t cap, uint64_t t
 // ---------------------------------------------------------------- kernels
 
 // A heavy tile's rays, the long ones walked by S lanes each (kSplit launches,
-// OCH_OPT_SPLIT; DESIGN.md §4e).  The workgroup is one wave of lane tasks from
+// OCH_OPT_SPLIT; DESIGN.md §4d).  The workgroup is one wave of lane tasks from
 // the plan's task table (och_api.cpp plan_split): word 0 the tile, then per
 // lane pixel | seg << 6 | log2(S) << 10, or ~0 for an idle lane.  A lane walks
 // its ray's whole walk above the split level but enters only the present

@@ -412,6 +412,22 @@ def display_weight(world: int, exchange: str = "all_gather") -> float:
     return max(0.5, 1.0 - (0.0625 if exchange == "gather" else 0.05) * world)
 
 
+# The heavy-tile split (OCH_OPT_SPLIT) by world size: a lone
+# launch no longer waits on its longest rays, but the split waves cost
+# throughput, so it pays where a rank's launches are small and end on their
+# tails (tools/split_sweep.sh, profiles/r06/).  World sizes not listed: off.
+SPLIT_DEFAULTS = {8: {"split": 60, "split_segs": 4, "split_level": 6}}
+
+
+def split_defaults(world: int) -> dict:
+    """Pool options of the heavy-tile split at this world size ({"split": 0} = off)."""
+    best = {"split": 0}
+    for w, opts in sorted(SPLIT_DEFAULTS.items()):
+        if world >= w:
+            best = dict(opts)
+    return best
+
+
 class HOctree(GpuPool):
     """och::h_octree's table on the GPU: 1-based, miss t = +INF (ORT/och_h_octree.h:429)."""
 

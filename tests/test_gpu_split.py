@@ -1,4 +1,4 @@
-"""Heavy-tile split (OCH_OPT_SPLIT, DESIGN.md §4e): the planned costliest
+"""Heavy-tile split (OCH_OPT_SPLIT, DESIGN.md §4d): the planned costliest
 tiles walk their long rays over S lanes each, a lane entering only every S-th
 present cell of the split level along the ray, and the ray keeps the hit of
 the lowest such cell.  The records must be the full walk's (ORT/och_h_octree.h:292-447) bit
