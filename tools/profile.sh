@@ -12,7 +12,7 @@ OUT=gpurun_out/prof_$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
 export OCH_TREE_CACHE=${OCH_TREE_CACHE:-/tmp/och_tree_d12.npz}
-BARGS="--steps 20 --no-cpu-baseline --no-parity --sustain 0 --no-other-configs --no-bounce --no-cull-off $*"
+BARGS="--steps 20 --no-cpu-baseline --no-parity --sustain 0 --no-other-configs --no-bounce --no-cull-off --no-split-arm $*"
 step() {   # step <name> <rocprofv3 args...>
     local name=$1; shift
     echo "[profile] $name" >&2
