@@ -31,3 +31,49 @@ def test_design_roofline_quotes_the_committed_profile():
     # the fraction over the serialised launch, recomputed from the same two numbers
     frac = pmc["SQ_INSTS_VALU"] / (pmc["pmc_mean_ms"] * 1e-3) / 1e9 / (256 * 4 * 2.4 / 2)
     assert f"{frac:.3f}" in para
+
+
+def _bench_line(path: Path) -> dict:
+    """The JSON line of a committed bench.py output (the last line that parses)."""
+    for line in reversed(path.read_text().splitlines()):
+        line = line.strip()
+        if line.startswith("{"):
+            return json.loads(line)
+    raise AssertionError(f"no JSON line in {path}")
+
+
+def test_readme_headline_quotes_the_committed_runs():
+    """README's headline ranges (20-step window, sustained, the lone launch with
+    and without the split) are the min-max over the bench runs that
+    profiles/r06/headline.json lists -- committed bench.py outputs."""
+    spec = json.loads((ROOT / "profiles" / "r06" / "headline.json").read_text())
+    lines = [_bench_line(ROOT / f) for f in spec["n1_runs"]]
+    readme = (ROOT / "README.md").read_text()
+    win = [l["value"] / 1e3 for l in lines]
+    sus = [l["sustained"]["value"] / 1e3 for l in lines]
+    assert f"{min(sus):.1f}–{max(sus):.1f} G rays/s sustained" in readme
+    assert f"{min(win):.1f}–{max(win):.1f} G over the driver's 20-step" in readme
+    lone = [l["roofline"]["kernel_ms_serial"] for l in lines]
+    split = [l["split"]["kernel_ms_serial"] for l in lines if l.get("split")]
+    assert f"one two-view frame in {min(lone):.2f}–{max(lone):.2f} ms" in readme
+    assert split and f"or {min(split):.2f}–{max(split):.2f} ms with the" in readme
+
+
+def test_n8_projection_quotes_the_committed_proxy():
+    """The N = 8 numbers README and DESIGN §4d quote (the proxy's slowest shard
+    over 20 steps, without and with the split) are the min-max over the
+    committed proxy runs profiles/r06/headline.json lists."""
+    spec = json.loads((ROOT / "profiles" / "r06" / "headline.json").read_text())
+    readme = (ROOT / "README.md").read_text()
+    design = (ROOT / "DESIGN.md").read_text()
+
+    def slowest(files):
+        out = []
+        for f in files:
+            rows = json.loads((ROOT / f).read_text())
+            out.append(max(r["ms_per_step_20"] for r in rows if "shard" in r))
+        return min(out), max(out)
+    b, s = slowest(spec["n8_base"]), slowest(spec["n8_split"])
+    quote = f"{b[0]:.4f}–{b[1]:.4f} → {s[0]:.4f}–{s[1]:.4f} ms"
+    assert quote in readme, quote
+    assert quote in design, quote

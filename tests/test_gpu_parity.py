@@ -690,10 +690,12 @@ def test_retired_options_refused(ort, gpu_device):
         assert "retired" in lib.och_last_error().decode()
         assert lib.och_gpu_get_option(pool._h, opt, C.byref(v)) != 0
     for name, value in (("block", 128), ("layout", 0), ("tile_order", 1), ("bounce_compact", 2), ("cull", 0),
-                        ("timing", 2), ("plan", 0)):
+                        ("timing", 2), ("plan", 0), ("split", 60), ("split_segs", 8), ("split_level", 5)):
         pool.set_option(name, value)
         assert pool.get_option(name) == value
-    assert set(pool.OPTIONS) == {"block", "layout", "tile_order", "bounce_compact", "cull", "timing", "plan"}
+    assert set(pool.OPTIONS) == {"block", "layout", "tile_order", "bounce_compact", "cull", "timing", "plan",
+                                 "split", "split_segs", "split_level"}
+    assert pool.get_option("split_tiles") == 0                # read only: no plan made
     pool.close()
 
 
