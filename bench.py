@@ -1557,30 +1557,44 @@ def main():
     # headline's.
     split_arm = None
     if world == 1 and direct and not a.no_split_arm and pool.get_option("split") == 0:
+        # Interleaved with the split off, in the same state of the GPU: by now it
+        # has rendered for seconds, and windows this late run faster than the
+        # headline's (the warm-up ramp) -- compare the arms here,
+        # not with the headline.
         sopts = ort.split_defaults(8)
-        for k, v in sopts.items():
-            pool.set_option(k, v)
-        pool.plan_views(cams, a.row_chunk, 0, 1)
-        lat_split = lone_latency()
-        warm(a.warmup, events=False)
-        el_s = timed(a.steps, stage="window (split)")
-        last_s = sfs[(a.steps - 1) % len(sfs)].frames.cpu().numpy()
-        sus_s = None
-        if sustained is not None:
-            sus_s = round(statistics.median([W * H * len(cams) * sustained["steps_per_run"] /
-                                             timed(sustained["steps_per_run"], stage="window (split sustained)") / 1e6
-                                             for _ in range(3)]), 2)
-        split_arm = {"options": sopts, "tiles_split": pool.get_option("split_tiles"),
-                     "kernel_ms_serial": round(lat_split, 4), "value": round(total_rays / el_s / 1e6, 2),
-                     "ms_per_step": round(el_s / a.steps * 1e3, 4), "sustained": sus_s,
-                     "frames_equal_headline": None if frames_host is None else bool(np.array_equal(last_s, frames_host)),
-                     "note": "heavy-tile split on (the N >= 8 default): the planned costliest tiles walk their long "
-                             "rays over 4 lanes each; kernel_ms_serial = a lone two-view launch"}
-        if split_arm["frames_equal_headline"] is False:
-            raise SystemExit("split frames differ from the headline's")
+        arms = {"off": {"split": 0}, "on": sopts}
+        res = {k: {"lone": [], "window": [], "sustained": []} for k in arms}
+        last_s = None
+        for rnd in range(2):
+            for name, opts in arms.items():
+                for k, v in opts.items():
+                    pool.set_option(k, v)
+                pool.plan_views(cams, a.row_chunk, 0, 1)
+                res[name]["lone"].append(lone_latency())
+                warm(a.warmup, events=False)
+                res[name]["window"].append(total_rays / timed(a.steps, stage=f"window (split {name})") / 1e6)
+                if name == "on":
+                    res[name]["tiles"] = pool.get_option("split_tiles")
+                    last_s = sfs[(a.steps - 1) % len(sfs)].frames.cpu().numpy()
+                if sustained is not None and rnd == 0:
+                    res[name]["sustained"].append(W * H * len(cams) * sustained["steps_per_run"] /
+                                                  timed(sustained["steps_per_run"], stage=f"window (split {name})") / 1e6)
         pool.set_option("split", 0)
         pool.plan_views(cams, a.row_chunk, 0, 1)
         pool.set_stream(stream)
+
+        def summ(r):
+            return {"kernel_ms_serial": [round(x, 4) for x in r["lone"]], "value": [round(x, 2) for x in r["window"]],
+                    "sustained": [round(x, 2) for x in r["sustained"]] or None}
+        split_arm = {"options": sopts, "tiles_split": res["on"].get("tiles"), "on": summ(res["on"]),
+                     "off": summ(res["off"]),
+                     "frames_equal_headline": None if frames_host is None else bool(np.array_equal(last_s, frames_host)),
+                     "note": "heavy-tile split on (the N >= 8 default) against off, interleaved twice in the same GPU "
+                             "state after the headline: lone two-view launch (kernel_ms_serial), 20-step window "
+                             "(value) and one sustained run each; the planned costliest tiles walk their long rays "
+                             "over 4 lanes each"}
+        if split_arm["frames_equal_headline"] is False:
+            raise SystemExit("split frames differ from the headline's")
 
     # A moving camera (N = 1): the bench's cameras pan by dyaw per step, so no
     # step's launch order was planned from its own cameras -- the plan is made
