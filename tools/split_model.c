@@ -16,8 +16,9 @@
  * levels <= L, enters its own segments in the same state as the full walk,
  * and finds the same hit there if the hit lies there.  The ray's record is
  * then the hit of the lowest segment ordinal any lane found, or the MISS.
- * This tool checks that claim ray by ray against the full walk, and prices
- * the split with the lockstep model (a wave costs its longest lane's PUSH
+ * This tool checks that claim ray by ray against the full walk (also for the
+ * dynamic variant: a ray's lanes claim segments first come, first served), and
+ * prices the split with the lockstep model (a wave costs its longest lane's PUSH
  * tests, one per iteration of the render loop).
  *
  * Build: gcc -O2 -msse2 -o /tmp/split_model tools/split_model.c -lm -lpthread
@@ -117,6 +118,115 @@ static void walk(const float *o, const float *d, int seg, int stop_ord, Rec *out
     }
 }
 
+/* Dynamic claiming (the alternative to ordinal % S): every lane of a ray walks
+ * the levels <= L and claims each present level-L cell it reaches that no lane
+ * of the ray has claimed yet (claimed = the next unclaimed ordinal), so a lane
+ * busy inside a segment leaves the next ones to the others; a lane also stops
+ * at a cell past the lowest HIT found so far (hitmin).  Lanes step in lockstep,
+ * one PUSH test per iteration, as the render loop does. */
+typedef struct { int claimed, hitmin; } Shared;
+typedef struct {
+    float c[3], b[3];
+    uint32_t p[3], stack[32], dim, node, t_min;
+    int inv, idx, sp, level, axis, ord, push, cur_ord, st, done;
+    Rec rec;
+} Lane;
+
+static void lane_init(Lane *L, const float *o, const float *d)
+{
+    memset(L, 0, sizeof *L);
+    for (int a = 0; a < 3; ++a) {
+        const int pos = 0.0F < d[a];
+        L->inv |= pos << a;
+        const float refl = fabsf((pos ? 3.0F : 0.0F) - o[a]);
+        L->c[a] = _mm_cvtss_f32(_mm_rcp_ss(_mm_set_ss(u2f(f2u(d[a]) | 0x80000000u))));
+        L->b[a] = u2f(f2u(L->c[a] * refl) ^ 0x80000000u);
+        L->p[a] = f2u(refl) & 0x3FC00000u;
+        if (L->p[a] == 0x3FC00000u) L->idx |= 1 << a;
+    }
+    L->dim = 1u << 22; L->node = 1; L->level = 1; L->axis = 8; L->cur_ord = -1; L->st = 0;
+}
+
+static void lane_finish(Lane *L, int hit, uint32_t voxel)
+{
+    L->done = 1;
+    if (hit) { L->rec = (Rec){(L->axis >> 1) + 3 * ((L->inv & L->axis) == 0), voxel, L->t_min, L->cur_ord, L->push}; }
+    else L->rec = (Rec){6, 0, 0x7F800000u, -1, L->push};
+}
+
+/* run until one PUSH test is done (or the lane finishes) */
+static void lane_iter(Lane *L, Shared *sh)
+{
+    for (;;) {
+        if (L->st == 0) {                                   /* PUSH */
+            ++L->push;
+            const uint32_t ch = N[(size_t)(L->node - 1) * 8 + ((L->idx ^ L->inv) & 7)];
+            if (!ch) { L->st = 1; return; }
+            if (L->level == LEVEL) {
+                const int k = L->ord++;
+                if (sh->hitmin >= 0 && k > sh->hitmin) { lane_finish(L, 0, 0); return; }
+                if (sh->claimed > k) { L->st = 1; return; }   /* another lane's */
+                sh->claimed = k + 1;
+                L->cur_ord = k;
+            }
+            if (L->level++ == DEPTH) {
+                lane_finish(L, 1, ch);
+                if (sh->hitmin < 0 || L->cur_ord < sh->hitmin) sh->hitmin = L->cur_ord;
+                return;
+            }
+            L->stack[L->sp++] = L->node;
+            L->node = ch;
+            L->dim >>= 1;
+            L->idx = 0;
+            for (int a = 0; a < 3; ++a)
+                if (fmaf(u2f(L->p[a] | L->dim), L->c[a], L->b[a]) >= u2f(L->t_min)) { L->idx |= 1 << a; L->p[a] |= L->dim; }
+            return;
+        } else if (L->st == 1) {                            /* STEP */
+            uint32_t t[3];
+            for (int a = 0; a < 3; ++a) t[a] = f2u(fmaf(u2f(L->p[a]), L->c[a], L->b[a]));
+            const int a = (t[0] <= t[1] && t[0] <= t[2]) ? 0 : (t[1] < t[0] && t[1] <= t[2]) ? 1 : 2;
+            L->axis = 1 << a;
+            L->t_min = t[a];
+            if (!(L->idx & L->axis)) { L->st = 2; continue; }
+            L->p[a] &= ~L->dim;
+            L->idx ^= L->axis;
+            L->st = 0;
+        } else {                                            /* POP */
+            if (--L->level == 0) { lane_finish(L, 0, 0); return; }
+            L->node = L->stack[--L->sp];
+            for (int a = 0; a < 3; ++a) L->p[a] &= ~L->dim;
+            L->dim <<= 1;
+            L->idx = 0;
+            for (int a = 0; a < 3; ++a)
+                if (u2f(L->dim) == u2f(L->p[a] & L->dim)) L->idx |= 1 << a;
+            L->st = 1;
+        }
+    }
+}
+
+/* S lanes of one ray in lockstep: returns the iterations of the slowest (the
+ * ray's critical path), the merged record in *m and the lanes' summed iterations. */
+static int ray_dynamic(const float *o, const float *d, int S, Rec *m, int *lane_sum)
+{
+    Lane L[16];
+    Shared sh = {0, -1};
+    for (int s = 0; s < S; ++s) lane_init(&L[s], o, d);
+    int rounds = 0, left = S;
+    while (left) {
+        ++rounds;
+        for (int s = 0; s < S; ++s)
+            if (!L[s].done) { lane_iter(&L[s], &sh); if (L[s].done) --left; }
+    }
+    int best = -1, sum = 0;
+    for (int s = 0; s < S; ++s) {
+        sum += L[s].push;
+        if (L[s].rec.ord >= 0 && (best < 0 || L[s].rec.ord < L[best].rec.ord)) best = s;
+    }
+    *m = best < 0 ? (Rec){6, 0, 0x7F800000u, -1, 0} : L[best].rec;
+    *lane_sum = sum;
+    return rounds;
+}
+
 static void camera(float yaw, float pitch, int W, int H, int col, int row, float *d)
 {
     const float aspect = (float)W / (float)H, fov = 1.25F;
@@ -137,6 +247,8 @@ static int *FULL, *SPLIT;        /* per tile: longest lane, full walk / split (m
 static long *SPLIT_WORK;         /* per tile: sum over the S waves of their longest lane */
 static int *RSPLIT;              /* per tile, per-ray split: longest task */
 static long *RSPLIT_WORK;        /* per tile, per-ray split: waves' longest tasks summed (tasks packed longest first) */
+static int *DSPLIT;              /* per tile, per-ray split with dynamic claiming: longest task */
+static long *DSPLIT_WORK;
 static long BAD, RAYS;
 static int NEXT;
 static pthread_mutex_t MU = PTHREAD_MUTEX_INITIALIZER;
@@ -146,7 +258,7 @@ static void *worker(void *arg)
     (void)arg;
     const float o[3] = {1.5F, 1.5F, 1.5F};
     Rec seg[64];
-    int full_push[64], seg_push[64][16];
+    int full_push[64], seg_push[64][16], dyn_rounds[64];
     for (;;) {
         const int tile = __atomic_fetch_add(&NEXT, 1, __ATOMIC_RELAXED);
         if (tile >= TX * TY) return NULL;
@@ -172,6 +284,10 @@ static void *worker(void *arg)
             }
             const Rec m = best < 0 ? (Rec){6, 0, 0x7F800000u, -1, 0} : seg[best];
             if (m.dir != full.dir || m.voxel != full.voxel || m.t != full.t) ++bad;
+            Rec md;
+            int lsum;
+            dyn_rounds[l] = ray_dynamic(o, d, SEGS, &md, &lsum);
+            if (md.dir != full.dir || md.voxel != full.voxel || md.t != full.t) ++bad;
         }
         long work = 0;
         for (int w = 0; w < SEGS; ++w) work += wave_max[w];
@@ -191,6 +307,19 @@ static void *worker(void *arg)
             lmax = task[0];
             RSPLIT[tile] = lmax;
             RSPLIT_WORK[tile] = rw;
+            /* the same with dynamic claiming: a long ray's S lanes each cost its lockstep rounds */
+            nt = 0;
+            for (int l = 0; l < 64; ++l) {
+                if (full_push[l] * 100 > THETA * full_max) {
+                    for (int s = 0; s < SEGS; ++s) task[nt++] = dyn_rounds[l];
+                } else
+                    task[nt++] = full_push[l];
+            }
+            for (int i = 1; i < nt; ++i) { int v = task[i], j = i; while (j > 0 && task[j - 1] < v) { task[j] = task[j - 1]; --j; } task[j] = v; }
+            rw = 0;
+            for (int i = 0; i < nt; i += 64) rw += task[i];
+            DSPLIT[tile] = task[0];
+            DSPLIT_WORK[tile] = rw;
         }
         FULL[tile] = full_max;
         SPLIT[tile] = split_max;
@@ -229,6 +358,8 @@ int main(int argc, char **argv)
     SPLIT_WORK = calloc(TX * TY, sizeof *SPLIT_WORK);
     RSPLIT = calloc(TX * TY, sizeof *RSPLIT);
     RSPLIT_WORK = calloc(TX * TY, sizeof *RSPLIT_WORK);
+    DSPLIT = calloc(TX * TY, sizeof *DSPLIT);
+    DSPLIT_WORK = calloc(TX * TY, sizeof *DSPLIT_WORK);
     pthread_t th[256];
     for (int k = 0; k < threads; ++k) pthread_create(&th[k], NULL, worker, NULL);
     for (int k = 0; k < threads; ++k) pthread_join(th[k], NULL);
@@ -257,15 +388,17 @@ int main(int argc, char **argv)
                 if (FULL[t] > crit) crit = FULL[t];
             }
         }
-        long rwork = 0;
-        int rcrit = 0;
+        long rwork = 0, dwork = 0;
+        int rcrit = 0, dcrit = 0;
         for (int t = 0; t < TX * TY; ++t) {
-            if (FULL[t] > Ts[k]) { rwork += RSPLIT_WORK[t]; if (RSPLIT[t] > rcrit) rcrit = RSPLIT[t]; }
-            else { rwork += FULL[t]; if (FULL[t] > rcrit) rcrit = FULL[t]; }
+            if (FULL[t] > Ts[k]) { rwork += RSPLIT_WORK[t]; if (RSPLIT[t] > rcrit) rcrit = RSPLIT[t];
+                                   dwork += DSPLIT_WORK[t]; if (DSPLIT[t] > dcrit) dcrit = DSPLIT[t]; }
+            else { rwork += FULL[t]; if (FULL[t] > rcrit) rcrit = FULL[t]; dwork += FULL[t]; if (FULL[t] > dcrit) dcrit = FULL[t]; }
         }
         printf("%s{\"T\": %d, \"tiles_split\": %d, \"critical_path\": %d, \"work_vs_unsplit\": %.4f, "
-               "\"per_ray_critical_path\": %d, \"per_ray_work_vs_unsplit\": %.4f}", k ? ", " : "",
-               Ts[k], n, crit, (double)work / base, rcrit, (double)rwork / base);
+               "\"per_ray_critical_path\": %d, \"per_ray_work_vs_unsplit\": %.4f, "
+               "\"dynamic_critical_path\": %d, \"dynamic_work_vs_unsplit\": %.4f}", k ? ", " : "",
+               Ts[k], n, crit, (double)work / base, rcrit, (double)rwork / base, dcrit, (double)dwork / base);
     }
     printf("]}\n");
     return BAD != 0;
