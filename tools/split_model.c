@@ -124,7 +124,7 @@ static void walk(const float *o, const float *d, int seg, int stop_ord, Rec *out
  * busy inside a segment leaves the next ones to the others; a lane also stops
  * at a cell past the lowest HIT found so far (hitmin).  Lanes step in lockstep,
  * one PUSH test per iteration, as the render loop does. */
-typedef struct { int claimed, hitmin; } Shared;
+typedef struct { int claimed, hitmin, closed; } Shared;   /* closed: no segment left to claim */
 typedef struct {
     float c[3], b[3];
     uint32_t p[3], stack[32], dim, node, t_min;
@@ -157,6 +157,8 @@ static void lane_finish(Lane *L, int hit, uint32_t voxel)
 /* run until one PUSH test is done (or the lane finishes) */
 static void lane_iter(Lane *L, Shared *sh)
 {
+    /* inside a segment past the ray's lowest HIT so far: nothing it finds can win */
+    if (sh->hitmin >= 0 && L->cur_ord > sh->hitmin && L->level > LEVEL) { lane_finish(L, 0, 0); return; }
     for (;;) {
         if (L->st == 0) {                                   /* PUSH */
             ++L->push;
@@ -164,7 +166,7 @@ static void lane_iter(Lane *L, Shared *sh)
             if (!ch) { L->st = 1; return; }
             if (L->level == LEVEL) {
                 const int k = L->ord++;
-                if (sh->hitmin >= 0 && k > sh->hitmin) { lane_finish(L, 0, 0); return; }
+                if ((sh->hitmin >= 0 && k > sh->hitmin) || sh->closed) { lane_finish(L, 0, 0); return; }
                 if (sh->claimed > k) { L->st = 1; return; }   /* another lane's */
                 sh->claimed = k + 1;
                 L->cur_ord = k;
@@ -209,7 +211,7 @@ static void lane_iter(Lane *L, Shared *sh)
 static int ray_dynamic(const float *o, const float *d, int S, Rec *m, int *lane_sum)
 {
     Lane L[16];
-    Shared sh = {0, -1};
+    Shared sh = {0, -1, 0};
     for (int s = 0; s < S; ++s) lane_init(&L[s], o, d);
     int rounds = 0, left = S;
     while (left) {
@@ -333,6 +335,7 @@ static void *worker(void *arg)
 
 static int cmp_desc(const void *a, const void *b) { return *(const int *)b - *(const int *)a; }
 
+#ifndef SPLIT_MODEL_NO_MAIN
 int main(int argc, char **argv)
 {
     if (argc < 6) { fprintf(stderr, "usage: split_model nodes.bin depth pitch L S [threads]\n"); return 2; }
@@ -403,3 +406,4 @@ int main(int argc, char **argv)
     printf("]}\n");
     return BAD != 0;
 }
+#endif
