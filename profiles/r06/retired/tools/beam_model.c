@@ -13,11 +13,11 @@
  * longest lane's PUSH tests and descents with and without it, and checks every
  * record against the full walk.  If the ideal does not pay, no beam does.
  *
- * Build: gcc -O2 -msse2 -o /tmp/beam_model tools/beam_model.c -lm -lpthread
+ * Build: gcc -O2 -msse2 -o /tmp/beam_model profiles/r06/retired/tools/beam_model.c -lm -lpthread
  * Usage: beam_model nodes.bin depth pitch [threads [margin_ulps]]
  *   margin_ulps: t_b lowered by this many float ulps (0 = the ideal bound). */
 #define SPLIT_MODEL_NO_MAIN
-#include "split_model.c"
+#include "../../../../tools/split_model.c"
 
 static int MARGIN;
 

@@ -9,10 +9,10 @@
  * as free (their lanes walk nothing), and the spread of a wave's rays (the
  * bounding box of its pixels, a proxy for how many cache lines its loads touch).
  *
- * Build: gcc -O2 -msse2 -o /tmp/group_model tools/group_model.c -lm -lpthread
+ * Build: gcc -O2 -msse2 -o /tmp/group_model profiles/r06/retired/tools/group_model.c -lm -lpthread
  * Usage: group_model nodes.bin depth pitch [threads] */
 #define SPLIT_MODEL_NO_MAIN
-#include "split_model.c"
+#include "../../../../tools/split_model.c"
 
 static int *COST;                  /* per pixel: PUSH tests of the full walk (0: culled sky ray) */
 static int G_NEXT;

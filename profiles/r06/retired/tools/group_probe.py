@@ -1,5 +1,5 @@
 """Measures cost-sorted wave assembly on the GPU (design probe, not product;
-tools/group_model.c prices it in the lockstep model: -13 % / -19 % of the
+group_model.c (beside this file) prices it in the lockstep model: -13 % / -19 % of the
 waves' work for 16x16 / 32x32 blocks).
 
 The bench's two depth-12 1080p views as resident rays (och_gpu_raygen_dev),
@@ -12,7 +12,7 @@ The records must not depend on the order (checked); the question is whether the
 waves' shorter lockstep walks beat the lost coherence of their loads.  Timed
 lone (one launch, idle GPU) and pipelined (launches round-robin over 3 streams).
 
-Usage (GPU box): python tools/group_probe.py [--blocks 16,32] [--launches 60]"""
+Usage (GPU box): python profiles/r06/retired/tools/group_probe.py [--blocks 16,32] [--launches 60]"""
 from __future__ import annotations
 
 import argparse
@@ -23,7 +23,7 @@ from pathlib import Path
 
 import numpy as np
 
-sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+sys.path.insert(0, str(Path(__file__).resolve().parents[4]))
 
 
 def main() -> int:

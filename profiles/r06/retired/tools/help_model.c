@@ -10,10 +10,10 @@
  * iterations first.  Output: iterations per wave against the plain walk, and
  * the lane utilisation.
  *
- * Build: gcc -O2 -msse2 -o /tmp/help_model tools/help_model.c -lm -lpthread
+ * Build: gcc -O2 -msse2 -o /tmp/help_model profiles/r06/retired/tools/help_model.c -lm -lpthread
  * Usage: help_model nodes.bin depth pitch L setup [threads [tile_stride]] */
 #define SPLIT_MODEL_NO_MAIN
-#include "split_model.c"
+#include "../../../../tools/split_model.c"
 
 static int SETUP, STRIDE = 1;
 static long BASE_IT, HELP_IT, RAY_IT;
