@@ -1,0 +1,225 @@
+"""Randomised parity campaign (GPU box): random scenes, rays and launch options
+through the C ABI against the CPU oracle, bit for bit, for a fixed time.
+
+Each case draws a depth (2..16), a voxel set (uniform scatter, solid boxes,
+one-voxel slabs, checkerboards, clusters around dyadic corners), voxel ids up
+to 2^32 - 1, and rays (origins inside the root, on dyadic planes of the
+scene's depth, at the centre, outside the root; directions uniform, exactly
+axis-aligned, with zero / denormal / tiny components, aimed at voxel centres,
+corners and edges); then one launch path with random options:
+  trace     och_gpu_trace_batch_dev, layout 0/1, cull 0/1/2, block 64/128/256
+            (PUSH counts compared where the launch counts: cull 0 and 1)
+  tiled     och_gpu_trace_batch_tiled_dev (rays as an image of random width)
+  bounce    och_gpu_trace_bounce_batch_dev, compaction 0/1/2
+  octree    the same scene as och::octree (0-based, miss t = 0.0F)
+and compares direction, voxel id, t bits (and secondary records) with
+oracle/och_oracle.c.  The oracle is the checker here, as in tests/.
+
+Writes one JSON line per case and a summary to --out; exit 1 on any mismatch.
+Usage: python tools/fuzz_parity.py --seconds 300 --out gpurun_out/fuzz.jsonl   (or --cases N;
+tests/test_gpu_fuzz.py runs a fixed-seed slice of it)"""
+from __future__ import annotations
+
+import argparse
+import json
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT))
+sys.path.insert(0, str(ROOT / "tests"))
+
+
+def voxels_for(rng, depth):
+    """A random voxel set (x, y, z, id) at this depth and its kind."""
+    side = 1 << depth
+    kind = rng.choice(["scatter", "boxes", "slab", "checker", "corners"])
+    pts = []
+    if kind == "scatter":
+        k = int(rng.integers(1, min(side ** 3, 30000) + 1))
+        pts = rng.integers(0, side, (k, 3))
+    elif kind == "boxes":
+        for _ in range(int(rng.integers(1, 4))):
+            lo = rng.integers(0, side, 3)
+            ext = np.minimum(rng.integers(1, max(2, min(side, 48)), 3), side - lo)
+            g = np.stack(np.meshgrid(*[np.arange(lo[a], lo[a] + ext[a]) for a in range(3)], indexing="ij"), -1)
+            pts.append(g.reshape(-1, 3))
+        pts = np.concatenate(pts)
+    elif kind == "slab":
+        a = int(rng.integers(0, 3))
+        q = int(rng.integers(0, side))
+        n = min(side, 64)
+        u, v = np.meshgrid(np.arange(n), np.arange(n), indexing="ij")
+        u, v = u.ravel() * (side // n), v.ravel() * (side // n)
+        pts = np.zeros((u.size, 3), np.int64)
+        pts[:, a], pts[:, (a + 1) % 3], pts[:, (a + 2) % 3] = q, u, v
+    elif kind == "checker":
+        n = min(side, 24)
+        lo = rng.integers(0, side - n + 1, 3)
+        g = np.stack(np.meshgrid(*[np.arange(n)] * 3, indexing="ij"), -1).reshape(-1, 3)
+        g = g[(g.sum(1) % 2) == 0]
+        pts = g + lo
+    else:
+        for k in range(1, depth):
+            c = (rng.integers(0, 1 << k, 3) * (side >> k))
+            off = rng.integers(-2, 3, (12, 3))
+            pts.append(np.clip(c + off, 0, side - 1))
+        pts = np.concatenate(pts) if pts else rng.integers(0, side, (1, 3))
+    pts = np.unique(np.asarray(pts, np.int64).reshape(-1, 3), axis=0)
+    big = rng.random() < 0.3
+    ids = rng.integers(1, 2 ** 32 if big else 256, pts.shape[0], dtype=np.uint64)
+    return kind, [(int(x), int(y), int(z), int(i)) for (x, y, z), i in zip(pts, ids)]
+
+
+def rays_for(rng, depth, vox, n):
+    side = 1 << depth
+    o = rng.uniform(1.0, 2.0, (n, 3))
+    kinds = rng.integers(0, 4, n)
+    dy = (rng.integers(0, side + 1, (n, 3)) / side) + 1.0            # dyadic planes of this depth
+    pick = rng.random((n, 3)) < 0.5
+    o = np.where((kinds == 1)[:, None] & pick, dy, o)
+    o[kinds == 2] = 1.5
+    out = kinds == 3
+    o[out] = rng.uniform(0.5, 2.5, (out.sum(), 3))
+    tgt = np.array([v[:3] for v in vox], np.float64)[rng.integers(0, len(vox), n)]
+    tgt = tgt + rng.choice([0.0, 0.5, 1.0], (n, 3))                   # corners, centres, edges
+    d = (1.0 + tgt / side) - o
+    r = rng.random(n)
+    d[r < 0.25] = rng.normal(size=((r < 0.25).sum(), 3))
+    ax = (r >= 0.25) & (r < 0.32)
+    d[ax] = 0.0
+    d[ax, rng.integers(0, 3, ax.sum())] = rng.choice([-1.0, 1.0], ax.sum())
+    zc = (r >= 0.32) & (r < 0.40)
+    d[zc, rng.integers(0, 3, zc.sum())] = rng.choice([0.0, 1e-40, -1e-30, 1e-12], zc.sum())
+    norm = np.linalg.norm(d, axis=1, keepdims=True)
+    scale = np.where(rng.random((n, 1)) < 0.8, norm, 1.0)             # most normalised, some not
+    d = np.where(norm > 0, d / np.where(scale > 0, scale, 1.0), [[0.6, 0.0, -0.8]])
+    return o.astype(np.float32), d.astype(np.float32)
+
+
+def to_octree(nodes, root, depth):
+    """The 1-based DAG as och::octree's 0-based table: root first, 0 = empty."""
+    n = nodes.shape[0]
+    order = [root] + [i for i in range(1, n + 1) if i != root]
+    new = {old: k for k, old in enumerate(order)}
+    out = np.zeros_like(nodes)
+    # interior levels hold node indices, the last level voxel ids: tell them apart by level
+    level = {root: 0}
+    stack = [root]
+    while stack:
+        i = stack.pop()
+        if level[i] == depth - 1:
+            continue
+        for c in nodes[i - 1]:
+            if c and int(c) not in level:
+                level[int(c)] = level[i] + 1
+                stack.append(int(c))
+    for old, k in new.items():
+        row = nodes[old - 1]
+        if level.get(old, depth - 1) == depth - 1:
+            out[k] = row
+        else:
+            out[k] = [new[int(c)] if c else 0 for c in row]
+    return out
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--seconds", type=float, default=300)
+    ap.add_argument("--seed", type=int, default=2026)
+    ap.add_argument("--rays", type=int, default=60000)
+    ap.add_argument("--cases", type=int, default=0, help="stop after this many cases (0: run for --seconds)")
+    ap.add_argument("--out", default="gpurun_out/fuzz.jsonl")
+    a = ap.parse_args(argv)
+    import torch
+    import octree_ray_tracing_amd as ort
+    import oracle.oracle as O
+    from conftest import sparse_dag
+
+    dev = torch.device("cuda", 0)
+    rng = np.random.default_rng(a.seed)
+    Path(a.out).parent.mkdir(parents=True, exist_ok=True)
+    fout = open(a.out, "w")
+    t_end = time.time() + a.seconds
+    cases = bad = rays_total = 0
+    by_path = {}
+
+    def dt(x, dtype=torch.int32):
+        return torch.from_numpy(np.ascontiguousarray(x)).to(dev) if x is not None else None
+
+    while time.time() < t_end and not (a.cases and cases >= a.cases):
+        depth = int(rng.choice(np.arange(2, 17), p=np.r_[[1, 2, 3, 4, 4, 4, 4, 4, 3, 2, 2, 1, 1, 1, 1]] / 37))
+        kind, vox = voxels_for(rng, depth)
+        nodes, root = sparse_dag(depth, vox)
+        o, d = rays_for(rng, depth, vox, a.rays)
+        n = o.shape[0]
+        path = str(rng.choice(["trace", "trace", "tiled", "bounce", "octree"]))
+        opts = {"layout": int(rng.integers(0, 2)), "cull": int(rng.integers(0, 3)),
+                "block": int(rng.choice([64, 128, 256]))}
+        if path == "octree":
+            onodes = to_octree(nodes, root, depth)
+            pool = ort.Octree(onodes, depth, device=0)
+            ref_pool = O.OraclePool(onodes, 0, depth, 0)
+        else:
+            pool = ort.HOctree(nodes, root, depth, device=0)
+            ref_pool = O.OraclePool(nodes, root, depth, 1)
+        for k, v in opts.items():
+            pool.set_option(k, v)
+        pool.set_stream(torch.cuda.current_stream())
+        od, dd = dt(o.reshape(-1)), dt(d.reshape(-1))
+        hd, hv, ht, hp = (torch.empty(n, dtype=torch.int32, device=dev) for _ in range(4))
+        counts = opts["cull"] != 2
+        if path == "bounce":
+            pool.set_option("bounce_compact", int(rng.integers(0, 3)))
+            bd, bv, bt = (torch.empty(n, dtype=torch.int32, device=dev) for _ in range(3))
+            pool.trace_bounce_batch_dev(od, dd, hd, hv, ht, bd, bv, bt, hp if counts else None, n=n)
+            ref = O.trace_bounce_batch(ref_pool, O.Rcp(None), o, d, nthreads=16, want_push=True)
+        elif path == "tiled":
+            width = int(rng.integers(1, 700))
+            pool.trace_batch_tiled_dev(od, dd, width, hd, hv, ht, hp if counts else None, n=n)
+            ref = O.trace_batch(ref_pool, O.Rcp(None), o, d, nthreads=16, want_push=True)
+            opts["width"] = width
+        else:
+            pool.trace_batch_dev(od, dd, hd, hv, ht, hp if counts else None, n=n)
+            ref = O.trace_batch(ref_pool, O.Rcp(None), o, d, nthreads=16, want_push=True)
+        torch.cuda.synchronize()
+        got = {"dir": hd.cpu().numpy(), "voxel": hv.cpu().numpy().view(np.uint32), "t": ht.cpu().numpy().view(np.uint32)}
+        miss = int((got["dir"] != ref["dir"]).sum() + (got["voxel"] != ref["voxel"].view(np.uint32)).sum()
+                   + (got["t"] != ref["t"].view(np.uint32)).sum())
+        # PUSH counts: launches that count cull only at cull 2 (a culled ray counts 0)
+        if counts and path != "bounce":
+            miss += int((hp.cpu().numpy().view(np.uint32) != ref["push"]).sum())
+        if path == "bounce":
+            for k, b in (("dir2", bd), ("voxel2", bv), ("t2", bt)):
+                g = b.cpu().numpy()
+                r = ref[k]
+                if k == "t2":
+                    g, r = g.view(np.uint32), r.view(np.uint32)
+                elif k == "voxel2":
+                    g, r = g.view(np.uint32), r.view(np.uint32)
+                miss += int((g != r).sum())
+        pool.close()
+        cases += 1
+        rays_total += n
+        bad += miss != 0
+        by_path[path] = by_path.get(path, 0) + 1
+        hits = int((ref["dir"] < 6).sum())
+        rec = {"case": cases, "path": path, "depth": depth, "scene": kind, "voxels": len(vox), "nodes": int(nodes.shape[0]),
+               "rays": n, "hits": hits, "opts": opts, "mismatches": miss}
+        fout.write(json.dumps(rec) + "\n")
+        fout.flush()
+        print(f"[fuzz] {cases} {path} d{depth} {kind} vox {len(vox)} hits {hits} opts {opts} -> {miss}",
+              file=sys.stderr, flush=True)
+    summary = {"summary": True, "cases": cases, "rays": rays_total, "cases_with_mismatches": bad, "by_path": by_path,
+               "seed": a.seed, "seconds": a.seconds}
+    fout.write(json.dumps(summary) + "\n")
+    fout.close()
+    print(json.dumps(summary))
+    return 1 if bad else 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())
