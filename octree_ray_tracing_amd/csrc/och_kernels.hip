@@ -605,6 +605,15 @@ __device__ __forceinline__ void ray_trace(Ray &r, const DevPool &P, const float 
                                           uint32_t stride, bool exact = true)
 {
     if (!ray_setup<kCount, kCull>(r, P, o, d, stack, stride, exact)) return;
+    // A split walk is exact only where a POP restores the child index the
+    // descent took: in waves whose rays all start inside the
+    // root.  Elsewhere a POP rebuilds idx from the position bits (:440-444),
+    // which can differ from what a lane that skipped the segment holds, so
+    // every lane of such a wave enters every segment (the whole walk).
+    if (kSplit && !r.inside) {
+        r.split_mask = 0;
+        r.split_seg = 0;
+    }
     if (kPacked && r.inside)
         ray_walk<kPacked, kCount, kAsm, true, kSplit>(r, P, stride);
     else

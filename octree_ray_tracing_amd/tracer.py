@@ -58,6 +58,16 @@ def _dev_ptr(t) -> int:
     return t.data_ptr()
 
 
+def _need(t, nbytes: int, what: str):
+    """A device buffer passed as a tensor must hold what the launch writes or
+    reads: the C ABI takes bare pointers (as the reference's interface takes
+    references), so the sizes are checked here.  Raw pointers pass unchecked."""
+    if hasattr(t, "numel") and hasattr(t, "element_size"):
+        have = t.numel() * t.element_size()
+        if have < nbytes:
+            raise ValueError(f"{what}: the buffer holds {have} B, the launch needs {nbytes} B")
+
+
 def host_rcp_lut() -> np.ndarray:
     """This host's RCPPS (_mm_rcp_ps, ORT/och_h_octree.h:316) as a 2^k table."""
     buf = np.empty(1 << 23, np.uint32)
@@ -235,6 +245,7 @@ class GpuPool:
         if n is None:
             n = dirs.numel() // 3
         stride = 0 if origins.numel() == 3 else 3
+        self._need_batch(origins, dirs, n, stride, (hit_dir, hit_voxel, hit_time, push))
         call("och_gpu_trace_batch_dev", self._h, _dev_ptr(origins), stride, _dev_ptr(dirs), int(n),
              _dev_ptr(hit_dir), _dev_ptr(hit_voxel), _dev_ptr(hit_time),
              None if push is None else _dev_ptr(push))
@@ -245,6 +256,7 @@ class GpuPool:
         if n is None:
             n = dirs.numel() // 3
         stride = 0 if origins.numel() == 3 else 3
+        self._need_batch(origins, dirs, n, stride, (hit_dir, hit_voxel, hit_time, push))
         call("och_gpu_trace_batch_tiled_dev", self._h, _dev_ptr(origins), stride, _dev_ptr(dirs), int(n), int(width),
              _dev_ptr(hit_dir), _dev_ptr(hit_voxel), _dev_ptr(hit_time), None if push is None else _dev_ptr(push))
 
@@ -262,12 +274,28 @@ class GpuPool:
         if n is None:
             n = dirs.numel() // 3
         stride = 0 if origins.numel() == 3 else 3
+        self._need_batch(origins, dirs, n, stride, (hit_dir, hit_voxel, hit_time, bounce_dir, bounce_voxel,
+                                                    bounce_time, push))
         call("och_gpu_trace_bounce_batch_dev", self._h, _dev_ptr(origins), stride, _dev_ptr(dirs), int(n),
              _dev_ptr(hit_dir), _dev_ptr(hit_voxel), _dev_ptr(hit_time), _dev_ptr(bounce_dir),
              _dev_ptr(bounce_voxel), _dev_ptr(bounce_time), None if push is None else _dev_ptr(push))
 
+    @staticmethod
+    def _need_batch(origins, dirs, n, stride, outs):
+        _need(origins, 12 * (int(n) if stride else 1), "origins")
+        _need(dirs, 12 * int(n), "dirs")
+        for o in outs:
+            if o is not None:
+                _need(o, 4 * int(n), "hit records")
+
+    def _need_frames(self, buf, cams, row_chunk, shard, n_shards, bytes_per_pixel, what):
+        cams = cams if isinstance(cams, (list, tuple)) else [cams]
+        rows = self.slice_rows(cams[0].height, int(row_chunk), int(n_shards))
+        _need(buf, len(cams) * rows * cams[0].width * bytes_per_pixel, what)
+
     # -- frame path
     def raygen_dev(self, cam: Camera, dirs):
+        _need(dirs, 12 * cam.width * cam.height, "dirs")
         call("och_gpu_raygen_dev", self._h, C.byref(cam), _dev_ptr(dirs))
 
     def render(self, cam: Camera) -> np.ndarray:
@@ -280,6 +308,7 @@ class GpuPool:
                    n_shards: int = 1):
         if row_chunk is None:
             row_chunk = cam.height
+        self._need_frames(rgba_slice, cam, row_chunk, shard, n_shards, 4, "rgba_slice")
         call("och_gpu_render_dev", self._h, C.byref(cam), _dev_ptr(rgba_slice), int(row_chunk),
              int(shard), int(n_shards))
 
@@ -288,6 +317,7 @@ class GpuPool:
         arr = (Camera * len(cams))(*cams)
         if row_chunk is None:
             row_chunk = cams[0].height
+        self._need_frames(rgba_slices, cams, row_chunk, shard, n_shards, 4, "rgba_slices")
         call("och_gpu_render_views_dev", self._h, C.cast(arr, C.c_void_p), len(cams), _dev_ptr(rgba_slices),
              int(row_chunk), int(shard), int(n_shards))
 
@@ -303,6 +333,8 @@ class GpuPool:
         if row_chunk is None:
             row_chunk = cams[0].height
         sp = (C.c_void_p * len(streams))(*[getattr(s_, "cuda_stream", s_) for s_ in streams])
+        for f in frames:
+            self._need_frames(f, list(cams), row_chunk, 0, 1, 4, "frames")
         fp = (C.c_void_p * len(frames))(*[_dev_ptr(f) for f in frames])
         e0 = e1 = None
         if events is not None:
@@ -328,6 +360,7 @@ class GpuPool:
         arr = (Camera * len(cams))(*cams)
         if row_chunk is None:
             row_chunk = cams[0].height
+        self._need_frames(rgba_slices, cams, row_chunk, shard, n_shards, 4, "rgba_slices")
         call("och_gpu_render_bounce_views_dev", self._h, C.cast(arr, C.c_void_p), len(cams), _dev_ptr(rgba_slices),
              int(row_chunk), int(shard), int(n_shards))
 
@@ -357,6 +390,9 @@ class GpuPool:
         return out
 
     def unshard_dev(self, gathered, frame, width: int, height: int, row_chunk: int, n_shards: int, n_views: int = 1):
+        rows = self.slice_rows(height, row_chunk, n_shards)
+        _need(gathered, 4 * n_shards * n_views * rows * width, "gathered")
+        _need(frame, 4 * n_views * height * width, "frame")
         call("och_gpu_unshard_views_dev", self._h, _dev_ptr(gathered), _dev_ptr(frame), int(width), int(height),
              int(row_chunk), int(n_shards), int(n_views))
 
@@ -369,11 +405,15 @@ class GpuPool:
         arr = (Camera * len(cams))(*cams)
         if row_chunk is None:
             row_chunk = cams[0].height
+        self._need_frames(code_slices, cams, row_chunk, shard, n_shards, 1, "code_slices")
         call("och_gpu_render_codes_views_dev", self._h, C.cast(arr, C.c_void_p), len(cams), _dev_ptr(code_slices),
              int(row_chunk), int(shard), int(n_shards), int(bool(bounce)))
 
     def shade_unshard_dev(self, gathered_codes, frames, width: int, height: int, row_chunk: int, n_shards: int,
                           n_views: int = 1):
+        rows = self.slice_rows(height, row_chunk, n_shards)
+        _need(gathered_codes, n_shards * n_views * rows * width, "gathered_codes")
+        _need(frames, 4 * n_views * height * width, "frames")
         call("och_gpu_shade_unshard_views_dev", self._h, _dev_ptr(gathered_codes), _dev_ptr(frames), int(width),
              int(height), int(row_chunk), int(n_shards), int(n_views))
 

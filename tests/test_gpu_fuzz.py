@@ -1,9 +1,10 @@
 """A fixed-seed slice of the randomised parity campaign (tools/fuzz_parity.py):
 random scenes (scatter, boxes, slabs, checkerboards, dyadic-corner clusters;
 depths 2-16; voxel ids up to 2^32 - 1), random edge-case rays and random
-launch options through four C-ABI paths (trace, tiled trace, bounce,
-och::octree), each against the oracle bit for bit.  The round-6 campaign ran
-5 920 such cases (355 M rays) with no mismatch (profiles/r06/r06n/)."""
+launch options through five C-ABI paths (trace, tiled trace, bounce,
+och::octree, camera frames in natural or planned order with the heavy-tile
+split), each against the oracle bit for bit.  Round 6's campaigns ran 8 934
+such cases with no mismatch (profiles/r06/r06n/, r06o/)."""
 import json
 import sys
 from pathlib import Path
@@ -24,4 +25,4 @@ def test_fuzz_slice(tmp_path, ort, O, gpu_device):
     summary = rows[-1]
     bad = [r for r in rows[:-1] if r["mismatches"]]
     assert rc == 0 and not bad, bad[:3]
-    assert summary["cases"] >= 60 and len(summary["by_path"]) == 4, summary
+    assert summary["cases"] >= 60 and len(summary["by_path"]) == 5, summary

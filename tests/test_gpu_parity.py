@@ -620,7 +620,7 @@ def test_planned_launch_order(ort, O, gpu_device, order, shape):
                 assert np.array_equal(full[v].cpu().numpy().view(np.uint32), want[v]), (yaw, n, rc, v)
     # config 5 frames in their planned order (the bounce kernel's own plan)
     cams = [ort.camera((1.5, 1.5, 1.5), 0.3, p, 1.25, W, H) for p in (0.0, -0.6)]
-    gathered = torch.full((1, 2, H, W), 255, dtype=torch.uint8, device="cuda")
+    gathered = torch.full((1, 2, ort.shard_rows(H, 8, 1), W), 255, dtype=torch.uint8, device="cuda")
     pool.render_codes_views_dev(cams, gathered[0], 8, 0, 1, bounce=True)
     full = torch.empty((2, H, W), dtype=torch.int32, device="cuda")
     pool.shade_unshard_dev(gathered, full, W, H, 8, 1, 2)

@@ -11,6 +11,8 @@ layout, a split level at the leaves)."""
 import numpy as np
 import pytest
 
+from conftest import GOLD
+
 pytestmark = pytest.mark.gpu
 
 ORIGIN = (1.5, 1.5, 1.5)
@@ -36,11 +38,12 @@ def frames_of(pool, cams, split=None, row_chunk=8, plan=True):
     pool.set_option("tile_order", 2 if plan else 0)
     if plan:
         pool.plan_views(cams, row_chunk)
-    out = torch.full((len(cams) * W * H,), 7, dtype=torch.int32, device="cuda")
+    rows = pool.slice_rows(H, row_chunk, 1)       # a view's slice holds whole row chunks
+    out = torch.full((len(cams) * rows * W,), 7, dtype=torch.int32, device="cuda")
     pool.set_stream(torch.cuda.current_stream())
     pool.render_views_dev(cams, out, row_chunk)
     torch.cuda.synchronize()
-    return out.cpu().numpy().view(np.uint32).reshape(len(cams), H, W)
+    return out.cpu().numpy().view(np.uint32).reshape(len(cams), rows, W)[:, :H]
 
 
 def test_split_bench_instance_d12_against_oracle(ort, O, d12):
@@ -147,3 +150,39 @@ def test_split_not_taken(ort, d10):
         from octree_ray_tracing_amd._lib import call
         call("och_gpu_set_option", pool._h, 17, 1)          # split_tiles is read-only
     pool.close()
+
+
+def test_split_camera_outside_root(ort, O):
+    """A camera outside the root (tools/fuzz_parity.py seed 4242, case 2483:
+    depth 3, y = 2.10): a POP there rebuilds the child index from the position
+    bits (:440-444), which can differ from the index a lane that skipped the
+    segment still holds, so such waves walk every segment on every lane
+    (och_kernels.hip ray_trace).  Before that guard this case lost 152-216
+    pixels at split level 1.  Also the depth-10 terrain seen from outside."""
+    z = np.load(GOLD / "split_outside_camera.npz")
+    depth, W, H, rc = int(z["depth"]), int(z["W"]), int(z["H"]), int(z["row_chunk"])
+    pal = ort.VoxelData().get_colours()
+    for nodes, root, depth, pos, views, fov in (
+            (z["nodes"], int(z["root"]), depth, tuple(float(v) for v in z["pos"]), z["views"], float(z["fov"])),
+            (None, None, 10, (1.82, 2.1, 1.64), [(2.0, -0.8), (0.3, -0.6)], 1.25)):
+        if nodes is None:
+            tree = ort.build_terrain(10)
+            nodes, root = tree.nodes, tree.root
+        pool = ort.HOctree(nodes, root, depth, device=0)
+        pool.set_palette(pal)
+        ref_pool = O.OraclePool(nodes, root, depth, 1)
+        cams = [ort.camera(pos, float(y), float(p), fov, W, H) for y, p in views]
+        want = []
+        for y, p in views:
+            r = O.trace_batch(ref_pool, O.Rcp(None), np.array(pos, np.float32), O.raygen(float(y), float(p), fov, W, H),
+                              nthreads=16)
+            want.append(O.shade_fast(r["dir"], r["voxel"], pal).reshape(H, W))
+        split_tiles = 0
+        for level in range(1, depth):
+            for segs in (4, 16):
+                got = frames_of(pool, cams, {"split": 66, "split_segs": segs, "split_level": level}, row_chunk=rc)
+                split_tiles = max(split_tiles, pool.get_option("split_tiles"))
+                for v in range(len(cams)):
+                    assert np.array_equal(got[v], want[v]), (depth, level, segs, v, int((got[v] != want[v]).sum()))
+        assert split_tiles > 0
+        pool.close()

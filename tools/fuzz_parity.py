@@ -12,6 +12,9 @@ corners and edges); then one launch path with random options:
   tiled     och_gpu_trace_batch_tiled_dev (rays as an image of random width)
   bounce    och_gpu_trace_bounce_batch_dev, compaction 0/1/2
   octree    the same scene as och::octree (0-based, miss t = 0.0F)
+  render    camera frames (RGBA8) of 1-2 random views, sizes, positions, fields
+            of view and palettes, natural or planned order, the heavy-tile
+            split at random thresholds / segment counts / levels
 and compares direction, voxel id, t bits (and secondary records) with
 oracle/och_oracle.c.  The oracle is the checker here, as in tests/.
 
@@ -126,6 +129,49 @@ def to_octree(nodes, root, depth):
     return out
 
 
+def render_case(rng, ort, O, torch, dev, pool, ref_pool, depth, opts):
+    """Camera frames (och_gpu_render_views_dev, RGBA8) of random views, sizes and
+    palettes, in natural or planned launch order, with the heavy-tile split at
+    random thresholds, segment counts and levels; against the oracle's raygen,
+    trace and trace_pixel shading.  Returns (mismatching pixels, rays, hits)."""
+    W, H, nv = int(rng.integers(1, 321)), int(rng.integers(1, 201)), int(rng.integers(1, 3))
+    pos = rng.uniform(1.0, 2.0, 3) if rng.random() < 0.85 else rng.uniform(0.6, 2.4, 3)
+    if rng.random() < 0.3:                                             # on dyadic planes of the scene
+        pos = np.where(rng.random(3) < 0.5, 1.0 + rng.integers(0, (1 << depth) + 1, 3) / (1 << depth), pos)
+    pos = tuple(float(np.float32(v)) for v in pos)
+    fov = float(rng.choice([1.25, float(rng.uniform(0.2, 2.5))]))
+    views = [(float(rng.uniform(-3.2, 3.2)), float(rng.uniform(-1.5, 1.5))) for _ in range(nv)]
+    pal = rng.integers(0, 2 ** 32, 6 * int(rng.integers(1, 300)), dtype=np.uint64).astype(np.uint32)
+    pool.set_palette(pal)
+    row_chunk = int(rng.choice([1, 2, 4, 8, 16]))
+    plan = rng.random() < 0.6
+    pool.set_option("tile_order", 2 if plan else 0)
+    if plan and opts["block"] == 64 and opts["layout"] == 1 and depth > 1 and rng.random() < 0.6:
+        split = {"split": int(rng.integers(1, 101)), "split_segs": int(rng.choice([2, 4, 8, 16])),
+                 "split_level": int(rng.integers(1, depth))}
+    else:
+        split = {"split": 0}
+    for k, v in split.items():
+        pool.set_option(k, v)
+    opts.update({"W": W, "H": H, "views": nv, "row_chunk": row_chunk, "plan": plan, **split})
+    cams = [ort.camera(pos, y, p, fov, W, H) for y, p in views]
+    if plan:
+        pool.plan_views(cams, row_chunk)
+        opts["split_tiles"] = pool.get_option("split_tiles")
+    rows = pool.slice_rows(H, row_chunk, 1)                            # a view's slice: whole row chunks
+    out = torch.full((nv * rows * W,), 7, dtype=torch.int32, device=dev)
+    pool.set_stream(torch.cuda.current_stream())
+    pool.render_views_dev(cams, out, row_chunk)
+    torch.cuda.synchronize()
+    got = out.cpu().numpy().view(np.uint32).reshape(nv, rows * W)[:, :H * W]
+    miss = hits = 0
+    for v, (y, p) in enumerate(views):
+        r = O.trace_batch(ref_pool, O.Rcp(None), np.array(pos, np.float32), O.raygen(y, p, fov, W, H), nthreads=16)
+        miss += int((got[v] != O.shade_fast(r["dir"], r["voxel"], pal)).sum())
+        hits += int((r["dir"] < 6).sum())
+    return miss, nv * W * H, hits
+
+
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--seconds", type=float, default=300)
@@ -156,7 +202,7 @@ def main(argv=None) -> int:
         nodes, root = sparse_dag(depth, vox)
         o, d = rays_for(rng, depth, vox, a.rays)
         n = o.shape[0]
-        path = str(rng.choice(["trace", "trace", "tiled", "bounce", "octree"]))
+        path = str(rng.choice(["trace", "trace", "tiled", "bounce", "octree", "render", "render"]))
         opts = {"layout": int(rng.integers(0, 2)), "cull": int(rng.integers(0, 3)),
                 "block": int(rng.choice([64, 128, 256]))}
         if path == "octree":
@@ -169,6 +215,20 @@ def main(argv=None) -> int:
         for k, v in opts.items():
             pool.set_option(k, v)
         pool.set_stream(torch.cuda.current_stream())
+        if path == "render":
+            miss, n, hits = render_case(rng, ort, O, torch, dev, pool, ref_pool, depth, opts)
+            pool.close()
+            cases += 1
+            rays_total += n
+            bad += miss != 0
+            by_path[path] = by_path.get(path, 0) + 1
+            rec = {"case": cases, "path": path, "depth": depth, "scene": kind, "voxels": len(vox),
+                   "nodes": int(nodes.shape[0]), "rays": n, "hits": hits, "opts": opts, "mismatches": miss}
+            fout.write(json.dumps(rec) + "\n")
+            fout.flush()
+            print(f"[fuzz] {cases} {path} d{depth} {kind} vox {len(vox)} hits {hits} opts {opts} -> {miss}",
+                  file=sys.stderr, flush=True)
+            continue
         od, dd = dt(o.reshape(-1)), dt(d.reshape(-1))
         hd, hv, ht, hp = (torch.empty(n, dtype=torch.int32, device=dev) for _ in range(4))
         counts = opts["cull"] != 2
