@@ -1,10 +1,11 @@
 """A fixed-seed slice of the randomised parity campaign (tools/fuzz_parity.py):
 random scenes (scatter, boxes, slabs, checkerboards, dyadic-corner clusters;
 depths 2-16; voxel ids up to 2^32 - 1), random edge-case rays and random
-launch options through five C-ABI paths (trace, tiled trace, bounce,
+launch options through nine C-ABI paths (trace, tiled trace, bounce,
 och::octree, camera frames in natural or planned order with the heavy-tile
-split), each against the oracle bit for bit.  Round 6's campaigns ran 8 934
-such cases with no mismatch (profiles/r06/r06n/, r06o/)."""
+split, sharded colour codes + shade, config-5 frames, the host image entry,
+editor flushes), each against the oracle bit for bit.  Round 6's campaigns:
+profiles/r06/INDEX.md (r06n-r06r, prof_r06q)."""
 import json
 import sys
 from pathlib import Path
@@ -25,4 +26,4 @@ def test_fuzz_slice(tmp_path, ort, O, gpu_device):
     summary = rows[-1]
     bad = [r for r in rows[:-1] if r["mismatches"]]
     assert rc == 0 and not bad, bad[:3]
-    assert summary["cases"] >= 60 and len(summary["by_path"]) == 5, summary
+    assert summary["cases"] >= 60 and len(summary["by_path"]) == 9, summary

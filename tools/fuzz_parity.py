@@ -15,6 +15,11 @@ corners and edges); then one launch path with random options:
   render    camera frames (RGBA8) of 1-2 random views, sizes, positions, fields
             of view and palettes, natural or planned order, the heavy-tile
             split at random thresholds / segment counts / levels
+  codes     every shard's indexed-colour slice (1-8 shards, round-robin or
+            weighted row deals, primary or config 5) + shade_unshard
+  bounce_frames  config 5 RGBA8 frames, every compaction mode
+  image     och_gpu_trace_batch_image (host rays, x + y * W, 8x8 tiles)
+  editor    h_octree::set edits flushed to the device pool in 1-3 windows
 and compares direction, voxel id, t bits (and secondary records) with
 oracle/och_oracle.c.  The oracle is the checker here, as in tests/.
 
@@ -172,6 +177,143 @@ def render_case(rng, ort, O, torch, dev, pool, ref_pool, depth, opts):
     return miss, nv * W * H, hits
 
 
+def random_views(rng, ort, depth, W, H, nv):
+    pos = rng.uniform(1.0, 2.0, 3) if rng.random() < 0.85 else rng.uniform(0.6, 2.4, 3)
+    pos = tuple(float(np.float32(v)) for v in pos)
+    fov = float(rng.choice([1.25, float(rng.uniform(0.2, 2.5))]))
+    views = [(float(rng.uniform(-3.2, 3.2)), float(rng.uniform(-1.5, 1.5))) for _ in range(nv)]
+    return pos, fov, views, [ort.camera(pos, y, p, fov, W, H) for y, p in views]
+
+
+def codes_case(rng, ort, O, torch, dev, pool, ref_pool, depth, opts):
+    """The multi-GPU frame path on one device: every shard's indexed-colour slice
+    (och_gpu_render_codes_views_dev, primary or config 5) under a round-robin or
+    weighted row deal, then och_gpu_shade_unshard_views_dev into RGBA8 frames."""
+    W, H, nv = int(rng.integers(1, 257)), int(rng.integers(1, 161)), int(rng.integers(1, 3))
+    n, rc = int(rng.integers(1, 9)), int(rng.choice([1, 2, 5, 8, 16]))
+    bounce = bool(rng.random() < 0.4)
+    pos, fov, views, cams = random_views(rng, ort, depth, W, H, nv)
+    pal = rng.integers(0, 2 ** 32, 6 * int(rng.integers(1, 21)), dtype=np.uint64).astype(np.uint32)
+    pool.set_palette(pal)
+    chunks = -(-H // rc)
+    if rng.random() < 0.5:
+        deal = ort.deal_chunks(rng.uniform(0.1, 2.0, chunks), n, rng.uniform(0.3, 1.0, n))
+        pool.set_row_deal(H, rc, n, deal)
+    else:
+        pool.set_row_deal(H, rc, n, None)
+    opts.update({"W": W, "H": H, "views": nv, "n_shards": n, "row_chunk": rc, "bounce": bounce})
+    rows = pool.slice_rows(H, rc, n)
+    gathered = torch.full((n, nv, rows, W), 255, dtype=torch.uint8, device=dev)
+    pool.set_stream(torch.cuda.current_stream())
+    for s_ in range(n):
+        pool.render_codes_views_dev(cams, gathered[s_], rc, s_, n, bounce)
+    full = torch.empty((nv, H, W), dtype=torch.int32, device=dev)
+    pool.shade_unshard_dev(gathered, full, W, H, rc, n, nv)
+    torch.cuda.synchronize()
+    got = full.cpu().numpy().view(np.uint32).reshape(nv, H * W)
+    return compare_frames(O, ref_pool, got, pos, fov, views, W, H, pal, bounce)
+
+
+def bounce_frames_case(rng, ort, O, torch, dev, pool, ref_pool, depth, opts):
+    """Config 5 RGBA8 frames (och_gpu_render_bounce_views_dev), every compaction mode."""
+    W, H, nv = int(rng.integers(1, 257)), int(rng.integers(1, 161)), int(rng.integers(1, 3))
+    rc = int(rng.choice([1, 4, 8, 16]))
+    pos, fov, views, cams = random_views(rng, ort, depth, W, H, nv)
+    pal = rng.integers(0, 2 ** 32, 6 * int(rng.integers(1, 300)), dtype=np.uint64).astype(np.uint32)
+    pool.set_palette(pal)
+    pool.set_option("bounce_compact", int(rng.integers(0, 3)))
+    plan = rng.random() < 0.5
+    pool.set_option("tile_order", 2 if plan else 0)
+    if plan:
+        pool.plan_views(cams, rc)
+    opts.update({"W": W, "H": H, "views": nv, "row_chunk": rc, "plan": plan})
+    rows = pool.slice_rows(H, rc, 1)
+    out = torch.full((nv * rows * W,), 7, dtype=torch.int32, device=dev)
+    pool.set_stream(torch.cuda.current_stream())
+    pool.render_bounce_views_dev(cams, out, rc)
+    torch.cuda.synchronize()
+    got = out.cpu().numpy().view(np.uint32).reshape(nv, rows * W)[:, :H * W]
+    return compare_frames(O, ref_pool, got, pos, fov, views, W, H, pal, True)
+
+
+def compare_frames(O, ref_pool, got, pos, fov, views, W, H, pal, bounce):
+    miss = hits = 0
+    for v, (y, p) in enumerate(views):
+        rays = O.raygen(y, p, fov, W, H)
+        if bounce:
+            r = O.trace_bounce_batch(ref_pool, O.Rcp(None), np.array(pos, np.float32), rays, nthreads=16)
+            want = O.shade_bounce(r["dir"], r["voxel"], r["dir2"], pal)
+        else:
+            r = O.trace_batch(ref_pool, O.Rcp(None), np.array(pos, np.float32), rays, nthreads=16)
+            want = O.shade_fast(r["dir"], r["voxel"], pal)
+        miss += int((got[v] != want).sum())
+        hits += int((r["dir"] < 6).sum())
+    return miss, len(views) * W * H, hits
+
+
+def image_case(rng, ort, O, torch, dev, pool, ref_pool, depth, opts, o, d):
+    """och_gpu_trace_batch_image: host rays in x + y * W order, traced as 8x8 tiles."""
+    width = int(rng.integers(1, 600))
+    opts["width"] = width
+    hd, hv, ht = pool.trace_batch(o, d, width=width)
+    r = O.trace_batch(ref_pool, O.Rcp(None), o, d, nthreads=16)
+    miss = int((hd != r["dir"]).sum() + (hv != r["voxel"].view(np.uint32)).sum()
+               + (ht.view(np.uint32) != r["t"].view(np.uint32)).sum())
+    return miss, o.shape[0], int((r["dir"] < 6).sum())
+
+
+def editor_case(rng, ort, O, torch, dev, scene, depth, opts, o, d):
+    """h_octree::set edits through the editor (och_editor_*), flushed to the
+    device pool in one to three windows, traced; against the oracle on a DAG
+    built afresh from the edited voxel set."""
+    from conftest import sparse_dag
+    nodes, root, vox = scene
+    if depth > 16:
+        return 0, 0, 0
+    ed = ort.Editor(nodes, root, depth, capacity=int(nodes.shape[0] + 700 * depth + 64))   # <= 597 edits
+    pool = ed.make_pool(device=0)
+    for k, v in (("layout", opts["layout"]), ("cull", opts["cull"]), ("block", opts["block"])):
+        pool.set_option(k, v)
+    cells = {(x, y, z): v for x, y, z, v in vox}
+    side = 1 << depth
+    flushes = int(rng.integers(1, 4))
+    n_edits = 0
+    for _ in range(flushes):
+        for _ in range(int(rng.integers(1, 200))):
+            if cells and rng.random() < 0.4:                      # remove or recolour an existing voxel
+                x, y, z = list(cells)[int(rng.integers(0, len(cells)))]
+            else:
+                x, y, z = (int(c) for c in rng.integers(0, side, 3))
+            v = 0 if rng.random() < 0.3 else int(rng.integers(1, 2 ** 32, dtype=np.uint64))
+            ed.set(x, y, z, v)
+            n_edits += 1
+            if v:
+                cells[(x, y, z)] = v
+            else:
+                cells.pop((x, y, z), None)
+        ed.flush(pool)
+    opts.update({"edits": n_edits, "flushes": flushes})
+    if not cells:
+        ed.close()
+        pool.close()
+        return 0, 0, 0
+    ref_nodes, ref_root = sparse_dag(depth, [(x, y, z, v) for (x, y, z), v in cells.items()])
+    ref_pool = O.OraclePool(ref_nodes, ref_root, depth, 1)
+    n = o.shape[0]
+    od = torch.from_numpy(np.ascontiguousarray(o.reshape(-1))).to(dev)
+    dd = torch.from_numpy(np.ascontiguousarray(d.reshape(-1))).to(dev)
+    hd, hv, ht = (torch.empty(n, dtype=torch.int32, device=dev) for _ in range(3))
+    pool.set_stream(torch.cuda.current_stream())
+    pool.trace_batch_dev(od, dd, hd, hv, ht, None, n=n)
+    torch.cuda.synchronize()
+    r = O.trace_batch(ref_pool, O.Rcp(None), o, d, nthreads=16)
+    miss = int((hd.cpu().numpy() != r["dir"]).sum() + (hv.cpu().numpy().view(np.uint32) != r["voxel"].view(np.uint32)).sum()
+               + (ht.cpu().numpy().view(np.uint32) != r["t"].view(np.uint32)).sum())
+    ed.close()
+    pool.close()
+    return miss, n, int((r["dir"] < 6).sum())
+
+
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--seconds", type=float, default=300)
@@ -202,7 +344,8 @@ def main(argv=None) -> int:
         nodes, root = sparse_dag(depth, vox)
         o, d = rays_for(rng, depth, vox, a.rays)
         n = o.shape[0]
-        path = str(rng.choice(["trace", "trace", "tiled", "bounce", "octree", "render", "render"]))
+        path = str(rng.choice(["trace", "trace", "tiled", "bounce", "octree", "render", "render", "codes",
+                               "bounce_frames", "image", "editor"]))
         opts = {"layout": int(rng.integers(0, 2)), "cull": int(rng.integers(0, 3)),
                 "block": int(rng.choice([64, 128, 256]))}
         if path == "octree":
@@ -215,9 +358,20 @@ def main(argv=None) -> int:
         for k, v in opts.items():
             pool.set_option(k, v)
         pool.set_stream(torch.cuda.current_stream())
-        if path == "render":
-            miss, n, hits = render_case(rng, ort, O, torch, dev, pool, ref_pool, depth, opts)
-            pool.close()
+        if path in ("render", "codes", "bounce_frames", "image", "editor"):
+            case = {"render": render_case, "codes": codes_case, "bounce_frames": bounce_frames_case,
+                    "image": image_case, "editor": editor_case}[path]
+            if path == "editor":
+                pool.close()
+                pool = None
+                miss, n, hits = editor_case(rng, ort, O, torch, dev, (nodes, root, vox), depth, opts, o, d)
+            elif path == "image":
+                miss, n, hits = image_case(rng, ort, O, torch, dev, pool, ref_pool, depth, opts, o, d)
+            else:
+                miss, n, hits = case(rng, ort, O, torch, dev, pool, ref_pool, depth, opts)
+            if pool is not None:
+                pool.close()
+            pool = None
             cases += 1
             rays_total += n
             bad += miss != 0
