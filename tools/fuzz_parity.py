@@ -20,6 +20,8 @@ corners and edges); then one launch path with random options:
   bounce_frames  config 5 RGBA8 frames, every compaction mode
   image     och_gpu_trace_batch_image (host rays, x + y * W, 8x8 tiles)
   editor    h_octree::set edits flushed to the device pool in 1-3 windows
+  steps     the N = 1 frame loop issued by the library (och_gpu_render_steps_dev)
+  sharded_steps  the N > 1 window at world size 1: codes, RCCL exchange, shade
 and compares direction, voxel id, t bits (and secondary records) with
 oracle/och_oracle.c.  The oracle is the checker here, as in tests/.
 
@@ -139,13 +141,9 @@ def render_case(rng, ort, O, torch, dev, pool, ref_pool, depth, opts):
     palettes, in natural or planned launch order, with the heavy-tile split at
     random thresholds, segment counts and levels; against the oracle's raygen,
     trace and trace_pixel shading.  Returns (mismatching pixels, rays, hits)."""
-    W, H, nv = int(rng.integers(1, 321)), int(rng.integers(1, 201)), int(rng.integers(1, 3))
-    pos = rng.uniform(1.0, 2.0, 3) if rng.random() < 0.85 else rng.uniform(0.6, 2.4, 3)
-    if rng.random() < 0.3:                                             # on dyadic planes of the scene
-        pos = np.where(rng.random(3) < 0.5, 1.0 + rng.integers(0, (1 << depth) + 1, 3) / (1 << depth), pos)
-    pos = tuple(float(np.float32(v)) for v in pos)
-    fov = float(rng.choice([1.25, float(rng.uniform(0.2, 2.5))]))
-    views = [(float(rng.uniform(-3.2, 3.2)), float(rng.uniform(-1.5, 1.5))) for _ in range(nv)]
+    W, H = int(rng.integers(1, 321)), int(rng.integers(1, 201))
+    nv = int(rng.integers(1, 3)) if rng.random() < 0.7 else int(rng.integers(3, 9))
+    views, cams = random_views(rng, ort, depth, W, H, nv)
     pal = rng.integers(0, 2 ** 32, 6 * int(rng.integers(1, 300)), dtype=np.uint64).astype(np.uint32)
     pool.set_palette(pal)
     row_chunk = int(rng.choice([1, 2, 4, 8, 16]))
@@ -159,7 +157,6 @@ def render_case(rng, ort, O, torch, dev, pool, ref_pool, depth, opts):
     for k, v in split.items():
         pool.set_option(k, v)
     opts.update({"W": W, "H": H, "views": nv, "row_chunk": row_chunk, "plan": plan, **split})
-    cams = [ort.camera(pos, y, p, fov, W, H) for y, p in views]
     if plan:
         pool.plan_views(cams, row_chunk)
         opts["split_tiles"] = pool.get_option("split_tiles")
@@ -169,30 +166,30 @@ def render_case(rng, ort, O, torch, dev, pool, ref_pool, depth, opts):
     pool.render_views_dev(cams, out, row_chunk)
     torch.cuda.synchronize()
     got = out.cpu().numpy().view(np.uint32).reshape(nv, rows * W)[:, :H * W]
-    miss = hits = 0
-    for v, (y, p) in enumerate(views):
-        r = O.trace_batch(ref_pool, O.Rcp(None), np.array(pos, np.float32), O.raygen(y, p, fov, W, H), nthreads=16)
-        miss += int((got[v] != O.shade_fast(r["dir"], r["voxel"], pal)).sum())
-        hits += int((r["dir"] < 6).sum())
-    return miss, nv * W * H, hits
+    return compare_frames(O, ref_pool, got, views, W, H, pal, False)
 
 
 def random_views(rng, ort, depth, W, H, nv):
-    pos = rng.uniform(1.0, 2.0, 3) if rng.random() < 0.85 else rng.uniform(0.6, 2.4, 3)
-    pos = tuple(float(np.float32(v)) for v in pos)
-    fov = float(rng.choice([1.25, float(rng.uniform(0.2, 2.5))]))
-    views = [(float(rng.uniform(-3.2, 3.2)), float(rng.uniform(-1.5, 1.5))) for _ in range(nv)]
-    return pos, fov, views, [ort.camera(pos, y, p, fov, W, H) for y, p in views]
+    """nv views of one size, each with its own position (outside the root now
+    and then), field of view, yaw and pitch: views = [(pos, fov, yaw, pitch)]."""
+    views = []
+    for _ in range(nv):
+        pos = rng.uniform(1.0, 2.0, 3) if rng.random() < 0.85 else rng.uniform(0.6, 2.4, 3)
+        if rng.random() < 0.3:                                         # on dyadic planes of the scene
+            pos = np.where(rng.random(3) < 0.5, 1.0 + rng.integers(0, (1 << depth) + 1, 3) / (1 << depth), pos)
+        views.append((tuple(float(np.float32(v)) for v in pos), float(rng.choice([1.25, float(rng.uniform(0.2, 2.5))])),
+                      float(rng.uniform(-3.2, 3.2)), float(rng.uniform(-1.5, 1.5))))
+    return views, [ort.camera(pos, y, p, fov, W, H) for pos, fov, y, p in views]
 
 
 def codes_case(rng, ort, O, torch, dev, pool, ref_pool, depth, opts):
     """The multi-GPU frame path on one device: every shard's indexed-colour slice
     (och_gpu_render_codes_views_dev, primary or config 5) under a round-robin or
     weighted row deal, then och_gpu_shade_unshard_views_dev into RGBA8 frames."""
-    W, H, nv = int(rng.integers(1, 257)), int(rng.integers(1, 161)), int(rng.integers(1, 3))
+    W, H, nv = int(rng.integers(1, 193)), int(rng.integers(1, 121)), int(rng.integers(1, 9))
     n, rc = int(rng.integers(1, 9)), int(rng.choice([1, 2, 5, 8, 16]))
     bounce = bool(rng.random() < 0.4)
-    pos, fov, views, cams = random_views(rng, ort, depth, W, H, nv)
+    views, cams = random_views(rng, ort, depth, W, H, nv)
     pal = rng.integers(0, 2 ** 32, 6 * int(rng.integers(1, 21)), dtype=np.uint64).astype(np.uint32)
     pool.set_palette(pal)
     chunks = -(-H // rc)
@@ -211,14 +208,14 @@ def codes_case(rng, ort, O, torch, dev, pool, ref_pool, depth, opts):
     pool.shade_unshard_dev(gathered, full, W, H, rc, n, nv)
     torch.cuda.synchronize()
     got = full.cpu().numpy().view(np.uint32).reshape(nv, H * W)
-    return compare_frames(O, ref_pool, got, pos, fov, views, W, H, pal, bounce)
+    return compare_frames(O, ref_pool, got, views, W, H, pal, bounce)
 
 
 def bounce_frames_case(rng, ort, O, torch, dev, pool, ref_pool, depth, opts):
     """Config 5 RGBA8 frames (och_gpu_render_bounce_views_dev), every compaction mode."""
-    W, H, nv = int(rng.integers(1, 257)), int(rng.integers(1, 161)), int(rng.integers(1, 3))
+    W, H, nv = int(rng.integers(1, 193)), int(rng.integers(1, 121)), int(rng.integers(1, 9))
     rc = int(rng.choice([1, 4, 8, 16]))
-    pos, fov, views, cams = random_views(rng, ort, depth, W, H, nv)
+    views, cams = random_views(rng, ort, depth, W, H, nv)
     pal = rng.integers(0, 2 ** 32, 6 * int(rng.integers(1, 300)), dtype=np.uint64).astype(np.uint32)
     pool.set_palette(pal)
     pool.set_option("bounce_compact", int(rng.integers(0, 3)))
@@ -233,12 +230,81 @@ def bounce_frames_case(rng, ort, O, torch, dev, pool, ref_pool, depth, opts):
     pool.render_bounce_views_dev(cams, out, rc)
     torch.cuda.synchronize()
     got = out.cpu().numpy().view(np.uint32).reshape(nv, rows * W)[:, :H * W]
-    return compare_frames(O, ref_pool, got, pos, fov, views, W, H, pal, True)
+    return compare_frames(O, ref_pool, got, views, W, H, pal, True)
 
 
-def compare_frames(O, ref_pool, got, pos, fov, views, W, H, pal, bounce):
+def steps_case(rng, ort, O, torch, dev, pool, ref_pool, depth, opts):
+    """The N = 1 frame loop issued by the library (och_gpu_render_steps_dev):
+    n frames round-robin over B streams and frame buffers, primary or config 5."""
+    W, H, nv = int(rng.integers(1, 193)), int(rng.integers(1, 121)), int(rng.integers(1, 9))
+    rc, B, n = int(rng.choice([1, 4, 8, 16])), int(rng.integers(1, 4)), int(rng.integers(1, 7))
+    bounce = bool(rng.random() < 0.4)
+    views, cams = random_views(rng, ort, depth, W, H, nv)
+    pal = rng.integers(0, 2 ** 32, 6 * int(rng.integers(1, 300)), dtype=np.uint64).astype(np.uint32)
+    pool.set_palette(pal)
+    opts.update({"W": W, "H": H, "views": nv, "row_chunk": rc, "buffers": B, "steps": n, "bounce": bounce})
+    rows = pool.slice_rows(H, rc, 1)
+    streams = [torch.cuda.current_stream()] + [torch.cuda.Stream(device=dev) for _ in range(B - 1)]
+    frames = [torch.full((nv * rows * W,), 7, dtype=torch.int32, device=dev) for _ in range(B)]
+    pool.render_steps_dev(cams, frames, streams, n, row_chunk=rc, bounce=bounce)
+    torch.cuda.synchronize()
     miss = hits = 0
-    for v, (y, p) in enumerate(views):
+    for b in range(min(B, n)):                                         # buffers no frame reached stay 7
+        got = frames[b].cpu().numpy().view(np.uint32).reshape(nv, rows * W)[:, :H * W]
+        m, _, hits = compare_frames(O, ref_pool, got, views, W, H, pal, bounce)
+        miss += m
+    pool.set_stream(torch.cuda.current_stream())
+    return miss, n * nv * W * H, hits
+
+
+COMM = []
+
+
+def sharded_steps_case(rng, ort, O, torch, dev, pool, ref_pool, depth, opts):
+    """The N > 1 window at world size 1 (och_gpu_render_sharded_steps_dev on the
+    library's RCCL communicator): colour codes, the exchange (all-gather, display
+    rank, gather), the shade; several frames over B streams and buffer sets."""
+    from octree_ray_tracing_amd.frame import ShardedFrame, ShardedSteps
+    if not COMM:
+        COMM.append(ort.RcclComm.local(0))
+    comm = COMM[0]
+    W, H, nv = int(rng.integers(1, 193)), int(rng.integers(1, 121)), int(rng.integers(1, 9))
+    rc, B, n = int(rng.choice([1, 2, 5, 8, 16])), int(rng.integers(1, 4)), int(rng.integers(1, 6))
+    bounce = bool(rng.random() < 0.4)
+    exchange = str(rng.choice(["all_gather", "display", "gather"]))
+    views, cams = random_views(rng, ort, depth, W, H, nv)
+    pal = rng.integers(0, 2 ** 32, 6 * int(rng.integers(1, 21)), dtype=np.uint64).astype(np.uint32)
+    pool.set_palette(pal)
+    plan = rng.random() < 0.5
+    pool.set_option("tile_order", 2 if plan else 0)
+    if plan:
+        pool.plan_views(cams, rc, 0, 1)
+    opts.update({"W": W, "H": H, "views": nv, "row_chunk": rc, "buffers": B, "steps": n, "bounce": bounce,
+                 "exchange": exchange, "plan": plan})
+    streams = [torch.cuda.current_stream()] + [torch.cuda.Stream(device=dev) for _ in range(B - 1)]
+    shade = "all" if exchange == "all_gather" else "display"
+    mode = "gather" if exchange == "gather" else "all_gather"
+    sfs = []
+    for s_ in streams:
+        with torch.cuda.stream(s_):
+            sfs.append(ShardedFrame(pool, W, H, rc, n_views=nv, indexed=True, shade=shade, comm=comm,
+                                    sharded=True, exchange=mode))
+    for f in sfs:
+        f.frames.fill_(7)
+    ShardedSteps(sfs, streams, comm, cams, bounce=bounce).run(n)
+    torch.cuda.synchronize()
+    miss = hits = 0
+    for b in range(min(B, n)):
+        got = sfs[b].frames.cpu().numpy().view(np.uint32).reshape(nv, H * W)
+        m, _, hits = compare_frames(O, ref_pool, got, views, W, H, pal, bounce)
+        miss += m
+    pool.set_stream(torch.cuda.current_stream())
+    return miss, n * nv * W * H, hits
+
+
+def compare_frames(O, ref_pool, got, views, W, H, pal, bounce):
+    miss = hits = 0
+    for v, (pos, fov, y, p) in enumerate(views):
         rays = O.raygen(y, p, fov, W, H)
         if bounce:
             r = O.trace_bounce_batch(ref_pool, O.Rcp(None), np.array(pos, np.float32), rays, nthreads=16)
@@ -345,7 +411,7 @@ def main(argv=None) -> int:
         o, d = rays_for(rng, depth, vox, a.rays)
         n = o.shape[0]
         path = str(rng.choice(["trace", "trace", "tiled", "bounce", "octree", "render", "render", "codes",
-                               "bounce_frames", "image", "editor"]))
+                               "bounce_frames", "image", "editor", "steps", "sharded_steps"]))
         opts = {"layout": int(rng.integers(0, 2)), "cull": int(rng.integers(0, 3)),
                 "block": int(rng.choice([64, 128, 256]))}
         if path == "octree":
@@ -358,9 +424,10 @@ def main(argv=None) -> int:
         for k, v in opts.items():
             pool.set_option(k, v)
         pool.set_stream(torch.cuda.current_stream())
-        if path in ("render", "codes", "bounce_frames", "image", "editor"):
+        if path in ("render", "codes", "bounce_frames", "image", "editor", "steps", "sharded_steps"):
             case = {"render": render_case, "codes": codes_case, "bounce_frames": bounce_frames_case,
-                    "image": image_case, "editor": editor_case}[path]
+                    "image": image_case, "editor": editor_case, "steps": steps_case,
+                    "sharded_steps": sharded_steps_case}[path]
             if path == "editor":
                 pool.close()
                 pool = None
@@ -427,6 +494,9 @@ def main(argv=None) -> int:
         fout.flush()
         print(f"[fuzz] {cases} {path} d{depth} {kind} vox {len(vox)} hits {hits} opts {opts} -> {miss}",
               file=sys.stderr, flush=True)
+    for c in COMM:
+        c.close()
+    COMM.clear()
     summary = {"summary": True, "cases": cases, "rays": rays_total, "cases_with_mismatches": bad, "by_path": by_path,
                "seed": a.seed, "seconds": a.seconds}
     fout.write(json.dumps(summary) + "\n")
