@@ -16,7 +16,8 @@ corners and edges); then one launch path with random options:
             of view and palettes, natural or planned order, the heavy-tile
             split at random thresholds / segment counts / levels
   codes     every shard's indexed-colour slice (1-8 shards, round-robin or
-            weighted row deals, primary or config 5) + shade_unshard
+            weighted row deals, primary or config 5; each shard planned, with
+            the split, as each rank of the N = 8 bench) + shade_unshard
   bounce_frames  config 5 RGBA8 frames, every compaction mode
   image     och_gpu_trace_batch_image (host rays, x + y * W, 8x8 tiles)
   editor    h_octree::set edits flushed to the device pool in 1-3 windows
@@ -147,16 +148,10 @@ def render_case(rng, ort, O, torch, dev, pool, ref_pool, depth, opts):
     pal = rng.integers(0, 2 ** 32, 6 * int(rng.integers(1, 300)), dtype=np.uint64).astype(np.uint32)
     pool.set_palette(pal)
     row_chunk = int(rng.choice([1, 2, 4, 8, 16]))
-    plan = rng.random() < 0.6
+    plan = FORCE_SPLIT[0] or rng.random() < 0.6
     pool.set_option("tile_order", 2 if plan else 0)
-    if plan and opts["block"] == 64 and opts["layout"] == 1 and depth > 1 and rng.random() < 0.6:
-        split = {"split": int(rng.integers(1, 101)), "split_segs": int(rng.choice([2, 4, 8, 16])),
-                 "split_level": int(rng.integers(1, depth))}
-    else:
-        split = {"split": 0}
-    for k, v in split.items():
-        pool.set_option(k, v)
-    opts.update({"W": W, "H": H, "views": nv, "row_chunk": row_chunk, "plan": plan, **split})
+    random_split(rng, pool, opts, depth, plan)
+    opts.update({"W": W, "H": H, "views": nv, "row_chunk": row_chunk, "plan": plan})
     if plan:
         pool.plan_views(cams, row_chunk)
         opts["split_tiles"] = pool.get_option("split_tiles")
@@ -198,11 +193,16 @@ def codes_case(rng, ort, O, torch, dev, pool, ref_pool, depth, opts):
         pool.set_row_deal(H, rc, n, deal)
     else:
         pool.set_row_deal(H, rc, n, None)
-    opts.update({"W": W, "H": H, "views": nv, "n_shards": n, "row_chunk": rc, "bounce": bounce})
+    plan = not bounce and (FORCE_SPLIT[0] or rng.random() < 0.5)
+    pool.set_option("tile_order", 2 if plan else 0)
+    random_split(rng, pool, opts, depth, plan)
+    opts.update({"W": W, "H": H, "views": nv, "n_shards": n, "row_chunk": rc, "bounce": bounce, "plan": plan})
     rows = pool.slice_rows(H, rc, n)
     gathered = torch.full((n, nv, rows, W), 255, dtype=torch.uint8, device=dev)
     pool.set_stream(torch.cuda.current_stream())
     for s_ in range(n):
+        if plan:                                   # each shard's own plan, as each rank makes it
+            pool.plan_views(cams, rc, s_, n)
         pool.render_codes_views_dev(cams, gathered[s_], rc, s_, n, bounce)
     full = torch.empty((nv, H, W), dtype=torch.int32, device=dev)
     pool.shade_unshard_dev(gathered, full, W, H, rc, n, nv)
@@ -231,6 +231,22 @@ def bounce_frames_case(rng, ort, O, torch, dev, pool, ref_pool, depth, opts):
     torch.cuda.synchronize()
     got = out.cpu().numpy().view(np.uint32).reshape(nv, rows * W)[:, :H * W]
     return compare_frames(O, ref_pool, got, views, W, H, pal, True)
+
+
+FORCE_SPLIT = [False]
+
+
+def random_split(rng, pool, opts, depth, plan):
+    """The heavy-tile split's options where a launch can take it (planned order,
+    block 64, the packed layout), at random thresholds, segment counts, levels."""
+    if plan and opts["block"] == 64 and opts["layout"] == 1 and depth > 1 and (FORCE_SPLIT[0] or rng.random() < 0.6):
+        split = {"split": int(rng.integers(1, 101)), "split_segs": int(rng.choice([2, 4, 8, 16])),
+                 "split_level": int(rng.integers(1, depth))}
+    else:
+        split = {"split": 0}
+    for k, v in split.items():
+        pool.set_option(k, v)
+    opts.update(split)
 
 
 def steps_case(rng, ort, O, torch, dev, pool, ref_pool, depth, opts):
@@ -275,8 +291,9 @@ def sharded_steps_case(rng, ort, O, torch, dev, pool, ref_pool, depth, opts):
     views, cams = random_views(rng, ort, depth, W, H, nv)
     pal = rng.integers(0, 2 ** 32, 6 * int(rng.integers(1, 21)), dtype=np.uint64).astype(np.uint32)
     pool.set_palette(pal)
-    plan = rng.random() < 0.5
+    plan = FORCE_SPLIT[0] or rng.random() < 0.5
     pool.set_option("tile_order", 2 if plan else 0)
+    random_split(rng, pool, opts, depth, plan and not bounce)
     if plan:
         pool.plan_views(cams, rc, 0, 1)
     opts.update({"W": W, "H": H, "views": nv, "row_chunk": rc, "buffers": B, "steps": n, "bounce": bounce,
@@ -387,6 +404,9 @@ def main(argv=None) -> int:
     ap.add_argument("--rays", type=int, default=60000)
     ap.add_argument("--cases", type=int, default=0, help="stop after this many cases (0: run for --seconds)")
     ap.add_argument("--out", default="gpurun_out/fuzz.jsonl")
+    ap.add_argument("--paths", default="", help="comma list: only these paths (default: all)")
+    ap.add_argument("--force-split", action="store_true",
+                    help="frame paths always planned, block 64, packed layout and split (the split's own campaign)")
     a = ap.parse_args(argv)
     import torch
     import octree_ray_tracing_amd as ort
@@ -404,16 +424,22 @@ def main(argv=None) -> int:
     def dt(x, dtype=torch.int32):
         return torch.from_numpy(np.ascontiguousarray(x)).to(dev) if x is not None else None
 
+    paths = ["trace", "trace", "tiled", "bounce", "octree", "render", "render", "codes", "bounce_frames", "image",
+             "editor", "steps", "sharded_steps"]
+    if a.paths:
+        paths = [p for p in a.paths.split(",") if p]
+    FORCE_SPLIT[:] = [a.force_split]
     while time.time() < t_end and not (a.cases and cases >= a.cases):
         depth = int(rng.choice(np.arange(2, 17), p=np.r_[[1, 2, 3, 4, 4, 4, 4, 4, 3, 2, 2, 1, 1, 1, 1]] / 37))
         kind, vox = voxels_for(rng, depth)
         nodes, root = sparse_dag(depth, vox)
         o, d = rays_for(rng, depth, vox, a.rays)
         n = o.shape[0]
-        path = str(rng.choice(["trace", "trace", "tiled", "bounce", "octree", "render", "render", "codes",
-                               "bounce_frames", "image", "editor", "steps", "sharded_steps"]))
+        path = str(rng.choice(paths))
         opts = {"layout": int(rng.integers(0, 2)), "cull": int(rng.integers(0, 3)),
                 "block": int(rng.choice([64, 128, 256]))}
+        if a.force_split:
+            opts.update({"layout": 1, "block": 64})
         if path == "octree":
             onodes = to_octree(nodes, root, depth)
             pool = ort.Octree(onodes, depth, device=0)
