@@ -137,7 +137,7 @@ def to_octree(nodes, root, depth):
     return out
 
 
-def render_case(rng, ort, O, torch, dev, pool, ref_pool, depth, opts):
+def render_case(rng, ort, O, torch, dev, pool, ref_pool, depth, opts, scene, o, d):
     """Camera frames (och_gpu_render_views_dev, RGBA8) of random views, sizes and
     palettes, in natural or planned launch order, with the heavy-tile split at
     random thresholds, segment counts and levels; against the oracle's raygen,
@@ -177,7 +177,7 @@ def random_views(rng, ort, depth, W, H, nv):
     return views, [ort.camera(pos, y, p, fov, W, H) for pos, fov, y, p in views]
 
 
-def codes_case(rng, ort, O, torch, dev, pool, ref_pool, depth, opts):
+def codes_case(rng, ort, O, torch, dev, pool, ref_pool, depth, opts, scene, o, d):
     """The multi-GPU frame path on one device: every shard's indexed-colour slice
     (och_gpu_render_codes_views_dev, primary or config 5) under a round-robin or
     weighted row deal, then och_gpu_shade_unshard_views_dev into RGBA8 frames."""
@@ -211,7 +211,7 @@ def codes_case(rng, ort, O, torch, dev, pool, ref_pool, depth, opts):
     return compare_frames(O, ref_pool, got, views, W, H, pal, bounce)
 
 
-def bounce_frames_case(rng, ort, O, torch, dev, pool, ref_pool, depth, opts):
+def bounce_frames_case(rng, ort, O, torch, dev, pool, ref_pool, depth, opts, scene, o, d):
     """Config 5 RGBA8 frames (och_gpu_render_bounce_views_dev), every compaction mode."""
     W, H, nv = int(rng.integers(1, 193)), int(rng.integers(1, 121)), int(rng.integers(1, 9))
     rc = int(rng.choice([1, 4, 8, 16]))
@@ -249,7 +249,7 @@ def random_split(rng, pool, opts, depth, plan):
     opts.update(split)
 
 
-def steps_case(rng, ort, O, torch, dev, pool, ref_pool, depth, opts):
+def steps_case(rng, ort, O, torch, dev, pool, ref_pool, depth, opts, scene, o, d):
     """The N = 1 frame loop issued by the library (och_gpu_render_steps_dev):
     n frames round-robin over B streams and frame buffers, primary or config 5."""
     W, H, nv = int(rng.integers(1, 193)), int(rng.integers(1, 121)), int(rng.integers(1, 9))
@@ -276,7 +276,7 @@ def steps_case(rng, ort, O, torch, dev, pool, ref_pool, depth, opts):
 COMM = []
 
 
-def sharded_steps_case(rng, ort, O, torch, dev, pool, ref_pool, depth, opts):
+def sharded_steps_case(rng, ort, O, torch, dev, pool, ref_pool, depth, opts, scene, o, d):
     """The N > 1 window at world size 1 (och_gpu_render_sharded_steps_dev on the
     library's RCCL communicator): colour codes, the exchange (all-gather, display
     rank, gather), the shade; several frames over B streams and buffer sets."""
@@ -334,7 +334,7 @@ def compare_frames(O, ref_pool, got, views, W, H, pal, bounce):
     return miss, len(views) * W * H, hits
 
 
-def image_case(rng, ort, O, torch, dev, pool, ref_pool, depth, opts, o, d):
+def image_case(rng, ort, O, torch, dev, pool, ref_pool, depth, opts, scene, o, d):
     """och_gpu_trace_batch_image: host rays in x + y * W order, traced as 8x8 tiles."""
     width = int(rng.integers(1, 600))
     opts["width"] = width
@@ -345,7 +345,7 @@ def image_case(rng, ort, O, torch, dev, pool, ref_pool, depth, opts, o, d):
     return miss, o.shape[0], int((r["dir"] < 6).sum())
 
 
-def editor_case(rng, ort, O, torch, dev, scene, depth, opts, o, d):
+def editor_case(rng, ort, O, torch, dev, pool, ref_pool, depth, opts, scene, o, d):
     """h_octree::set edits through the editor (och_editor_*), flushed to the
     device pool in one to three windows, traced; against the oracle on a DAG
     built afresh from the edited voxel set."""
@@ -395,6 +395,10 @@ def editor_case(rng, ort, O, torch, dev, scene, depth, opts, o, d):
     ed.close()
     pool.close()
     return miss, n, int((r["dir"] < 6).sum())
+
+
+CASES = {"render": render_case, "codes": codes_case, "bounce_frames": bounce_frames_case, "image": image_case,
+         "editor": editor_case, "steps": steps_case, "sharded_steps": sharded_steps_case}
 
 
 def main(argv=None) -> int:
@@ -450,21 +454,13 @@ def main(argv=None) -> int:
         for k, v in opts.items():
             pool.set_option(k, v)
         pool.set_stream(torch.cuda.current_stream())
-        if path in ("render", "codes", "bounce_frames", "image", "editor", "steps", "sharded_steps"):
-            case = {"render": render_case, "codes": codes_case, "bounce_frames": bounce_frames_case,
-                    "image": image_case, "editor": editor_case, "steps": steps_case,
-                    "sharded_steps": sharded_steps_case}[path]
-            if path == "editor":
+        if path in CASES:
+            if path == "editor":                   # the editor makes its own pool
                 pool.close()
                 pool = None
-                miss, n, hits = editor_case(rng, ort, O, torch, dev, (nodes, root, vox), depth, opts, o, d)
-            elif path == "image":
-                miss, n, hits = image_case(rng, ort, O, torch, dev, pool, ref_pool, depth, opts, o, d)
-            else:
-                miss, n, hits = case(rng, ort, O, torch, dev, pool, ref_pool, depth, opts)
+            miss, n, hits = CASES[path](rng, ort, O, torch, dev, pool, ref_pool, depth, opts, (nodes, root, vox), o, d)
             if pool is not None:
                 pool.close()
-            pool = None
             cases += 1
             rays_total += n
             bad += miss != 0
