@@ -151,9 +151,10 @@ def render_case(rng, ort, O, torch, dev, pool, ref_pool, depth, opts, scene, o, 
     plan = FORCE_SPLIT[0] or rng.random() < 0.6
     pool.set_option("tile_order", 2 if plan else 0)
     random_split(rng, pool, opts, depth, plan)
-    opts.update({"W": W, "H": H, "views": nv, "row_chunk": row_chunk, "plan": plan})
+    moved = plan and rng.random() < 0.3           # planned on other cameras (bench.py's moving camera)
+    opts.update({"W": W, "H": H, "views": nv, "row_chunk": row_chunk, "plan": plan, "moved": moved})
     if plan:
-        pool.plan_views(cams, row_chunk)
+        pool.plan_views(random_views(rng, ort, depth, W, H, nv)[1] if moved else cams, row_chunk)
         opts["split_tiles"] = pool.get_option("split_tiles")
     rows = pool.slice_rows(H, row_chunk, 1)                            # a view's slice: whole row chunks
     out = torch.full((nv * rows * W,), 7, dtype=torch.int32, device=dev)
