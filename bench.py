@@ -130,6 +130,16 @@ def pipeline_defaults(world: int, inflight=None, hw_queues=None):
     return inflight, hw_queues
 
 
+def plan_label(pool) -> str:
+    """The render launches' workgroup order (OCH_OPT_TILE_ORDER, OCH_OPT_PLAN)."""
+    if pool.get_option("tile_order") < 2:
+        return "natural"
+    p = pool.get_option("plan")
+    shape = ("every workgroup costliest first" if p == 0 else "costliest and cheapest alternating" if p == 100
+             else f"the costliest {p} % first, the rest in natural order")
+    return f"planned from a timed planning frame: {shape}"
+
+
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
@@ -1040,6 +1050,11 @@ def main():
         # 204-210 G over 20 steps against 200-202 G for the 10 % shape (sustained
         # 238-243 against 244-247 G); the driver times 20 steps
         pool.set_option("plan", 0)
+    elif world == 1 and not any(kv.startswith("plan=") for kv in a.opt):
+        # N = 1 (profiles/r06/r06x/, 9-12 interleaved runs per shape): the costliest
+        # 3 % first gives 38.87 G over the driver's 20 steps against 38.61 G for the
+        # library's 10 % (2 %: 39.01, 5 %: 39.06); sustained the same (45.8 G)
+        pool.set_option("plan", 3)
     if a.pool_timing is not None:
         pool.set_option("timing", a.pool_timing)
     if pool.get_option("tile_order") >= 2:
@@ -1856,6 +1871,7 @@ def main():
                        "parallelism": f"rows{world}",
                        "frames_in_flight": len(streams),
                        "hw_queues": int(os.environ.get("GPU_MAX_HW_QUEUES", "4")),
+                       "launch_order": plan_label(pool),
                        "issue": ("one och_gpu_render_sharded_steps_dev call per timed window and rank (the "
                                  "library issues each step's render, RCCL exchange and shade)" if sharded_steps
                                  else "one och_gpu_render_steps_dev call per timed window (the library issues each "
