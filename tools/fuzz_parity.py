@@ -111,6 +111,27 @@ def rays_for(rng, depth, vox, n):
     return o.astype(np.float32), d.astype(np.float32)
 
 
+TERRAIN = {}
+
+
+def terrain_rays(rng, n):
+    """Rays for the terrain DAG: origins inside the cube (the camera's 1.5 among
+    them), on its mid-planes, outside it; directions mostly downward (the
+    ground fills z < 1.31), some axis-aligned or with zero components."""
+    o = rng.uniform(1.0, 2.0, (n, 3))
+    o[rng.random(n) < 0.2] = 1.5
+    mid = rng.random((n, 3)) < 0.1
+    o[mid] = rng.choice([1.25, 1.5, 1.75], mid.sum())
+    out = rng.random(n) < 0.1
+    o[out] = rng.uniform(0.6, 2.4, (out.sum(), 3))
+    d = rng.normal(size=(n, 3))
+    d[:, 2] -= np.abs(rng.normal(1.0, 0.5, n))
+    zc = rng.random(n) < 0.08
+    d[zc, rng.integers(0, 3, zc.sum())] = 0.0
+    d /= np.maximum(np.linalg.norm(d, axis=1, keepdims=True), 1e-30)
+    return o.astype(np.float32), d.astype(np.float32)
+
+
 def to_octree(nodes, root, depth):
     """The 1-based DAG as och::octree's 0-based table: root first, 0 = empty."""
     n = nodes.shape[0]
@@ -410,6 +431,9 @@ def main(argv=None) -> int:
     ap.add_argument("--cases", type=int, default=0, help="stop after this many cases (0: run for --seconds)")
     ap.add_argument("--out", default="gpurun_out/fuzz.jsonl")
     ap.add_argument("--paths", default="", help="comma list: only these paths (default: all)")
+    ap.add_argument("--terrain", type=float, default=0.0,
+                    help="probability of a case on the reference's terrain at depth 10 or 12 (the bench's DAG) "
+                         "instead of a random scene")
     ap.add_argument("--force-split", action="store_true",
                     help="frame paths always planned, block 64, packed layout and split (the split's own campaign)")
     a = ap.parse_args(argv)
@@ -435,12 +459,21 @@ def main(argv=None) -> int:
         paths = [p for p in a.paths.split(",") if p]
     FORCE_SPLIT[:] = [a.force_split]
     while time.time() < t_end and not (a.cases and cases >= a.cases):
-        depth = int(rng.choice(np.arange(2, 17), p=np.r_[[1, 2, 3, 4, 4, 4, 4, 4, 3, 2, 2, 1, 1, 1, 1]] / 37))
-        kind, vox = voxels_for(rng, depth)
-        nodes, root = sparse_dag(depth, vox)
-        o, d = rays_for(rng, depth, vox, a.rays)
+        if a.terrain and rng.random() < a.terrain:
+            depth, kind, vox = int(rng.choice([10, 12])), "terrain", []
+            if depth not in TERRAIN:
+                t = ort.build_terrain(depth, use_gpu=True)
+                TERRAIN[depth] = (t.nodes, t.root)
+            nodes, root = TERRAIN[depth]
+            o, d = terrain_rays(rng, a.rays)
+            path = str(rng.choice([p for p in paths if p not in ("editor", "octree")] or ["trace"]))
+        else:
+            depth = int(rng.choice(np.arange(2, 17), p=np.r_[[1, 2, 3, 4, 4, 4, 4, 4, 3, 2, 2, 1, 1, 1, 1]] / 37))
+            kind, vox = voxels_for(rng, depth)
+            nodes, root = sparse_dag(depth, vox)
+            o, d = rays_for(rng, depth, vox, a.rays)
+            path = str(rng.choice(paths))
         n = o.shape[0]
-        path = str(rng.choice(paths))
         opts = {"layout": int(rng.integers(0, 2)), "cull": int(rng.integers(0, 3)),
                 "block": int(rng.choice([64, 128, 256]))}
         if a.force_split:
