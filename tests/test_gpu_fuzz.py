@@ -22,7 +22,8 @@ def test_fuzz_slice(tmp_path, ort, O, gpu_device):
     sys.path.insert(0, str(ROOT / "tools"))
     import fuzz_parity
     out = tmp_path / "fuzz.jsonl"
-    rc = fuzz_parity.main(["--cases", "160", "--seed", "7", "--rays", "20000", "--seconds", "90", "--out", str(out)])
+    rc = fuzz_parity.main(["--cases", "160", "--seed", "7", "--rays", "20000", "--seconds", "90",
+                           "--terrain", "0.1", "--out", str(out)])
     rows = [json.loads(l) for l in out.read_text().splitlines()]
     summary = rows[-1]
     bad = [r for r in rows[:-1] if r["mismatches"]]
