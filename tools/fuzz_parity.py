@@ -12,9 +12,10 @@ corners and edges); then one launch path with random options:
   tiled     och_gpu_trace_batch_tiled_dev (rays as an image of random width)
   bounce    och_gpu_trace_bounce_batch_dev, compaction 0/1/2
   octree    the same scene as och::octree (0-based, miss t = 0.0F)
-  render    camera frames (RGBA8) of 1-2 random views, sizes, positions, fields
-            of view and palettes, natural or planned order, the heavy-tile
-            split at random thresholds / segment counts / levels
+  render    camera frames (RGBA8) of 1-8 views of one random size, each with its
+            own position, field of view, yaw and pitch; random palettes;
+            natural or planned order (sometimes planned on other cameras); the
+            heavy-tile split at random thresholds / segment counts / levels
   codes     every shard's indexed-colour slice (1-8 shards, round-robin or
             weighted row deals, primary or config 5; each shard planned, with
             the split, as each rank of the N = 8 bench) + shade_unshard
@@ -23,12 +24,15 @@ corners and edges); then one launch path with random options:
   editor    h_octree::set edits flushed to the device pool in 1-3 windows
   steps     the N = 1 frame loop issued by the library (och_gpu_render_steps_dev)
   sharded_steps  the N > 1 window at world size 1: codes, RCCL exchange, shade
-and compares direction, voxel id, t bits (and secondary records) with
-oracle/och_oracle.c.  The oracle is the checker here, as in tests/.
+and compares direction, voxel id, t bits (and secondary records), or every
+frame's pixels, with oracle/och_oracle.c.  The oracle is the checker here, as
+in tests/.  --terrain P puts a fraction P of the cases on the reference's
+terrain DAG at depth 10 or 12 (the bench's); --paths and --force-split narrow a
+campaign (the split's own: --paths render,codes,sharded_steps --force-split).
 
 Writes one JSON line per case and a summary to --out; exit 1 on any mismatch.
-Usage: python tools/fuzz_parity.py --seconds 300 --out gpurun_out/fuzz.jsonl   (or --cases N;
-tests/test_gpu_fuzz.py runs a fixed-seed slice of it)"""
+Usage: python tools/fuzz_parity.py --seconds 300 --out gpurun_out/fuzz.jsonl
+(or --cases N; tests/test_gpu_fuzz.py runs a fixed-seed slice of it)"""
 from __future__ import annotations
 
 import argparse
