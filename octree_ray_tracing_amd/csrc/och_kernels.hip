@@ -589,8 +589,11 @@ __device__ __forceinline__ void ray_walk(Ray &r, const DevPool &P, uint32_t stri
         ray_push_raw<kCount>(r, P);
     // the activity test's two constants in VGPRs: as SGPRs the compiler re-loads
     // them from the kernel arguments in every iteration when the kernel's SGPR
-    // budget (80, for 8 waves per SIMD) is tight
-    uint32_t lo = P.dim_lo, span = P.dim_span;
+    // budget (80, for 8 waves per SIMD) is tight.  Derived from depth (which
+    // setup has loaded) rather than read as dim_lo / dim_span: those two share
+    // one scalar load with the cull box, and in the split kernel that load was
+    // hoisted to the entry, live across setup, and spilled to VGPR lanes
+    uint32_t lo = 1u << (23 - P.depth), span = (1u << 22) - lo;
     asm volatile("" : "+v"(lo), "+v"(span));
     if (r.dim - lo <= span) do {
         ray_iterate<kPacked, kCount, kAsm, kIdxPlane, kSplit>(r, P, stride);
