@@ -1565,18 +1565,19 @@ def main():
             pool.plan_views(cams, a.row_chunk, rank, world)
         pool.set_stream(stream)
 
-    # The heavy-tile split beside the headline at N = 1, where it
-    # is off by default: a lone frame no longer waits on its few longest rays,
-    # at a cost in throughput (the split waves walk the coarse levels once per
-    # lane).  Same cameras, the same window; its last frames must equal the
-    # headline's.
+    # The heavy-tile split against off at N = 1: with it a lone
+    # frame no longer waits on its few longest rays, for a little throughput
+    # (the split waves walk the coarse levels once per lane).  Same cameras,
+    # the same window; its last frames must equal the headline's.
     split_arm = None
-    if world == 1 and direct and not a.no_split_arm and pool.get_option("split") == 0:
-        # Interleaved with the split off, in the same state of the GPU: by now it
-        # has rendered for seconds, and windows this late run faster than the
-        # headline's (the warm-up ramp) -- compare the arms here,
-        # not with the headline.
-        sopts = ort.split_defaults(8)
+    if world == 1 and direct and not a.no_split_arm:
+        # Interleaved, in the same state of the GPU: by now it has rendered for
+        # seconds, and windows this late run faster than the headline's (the
+        # warm-up ramp) -- compare the arms here, not with the
+        # headline.  "on" is the headline's split, or the N = 8 default when the
+        # headline ran without one.
+        headline_split = {k: pool.get_option(k) for k in ("split", "split_segs", "split_level")}
+        sopts = headline_split if headline_split["split"] else ort.split_defaults(8)
         arms = {"off": {"split": 0}, "on": sopts}
         res = {k: {"lone": [], "window": [], "sustained": []} for k in arms}
         last_s = None
@@ -1594,7 +1595,8 @@ def main():
                 if sustained is not None and rnd == 0:
                     res[name]["sustained"].append(W * H * len(cams) * sustained["steps_per_run"] /
                                                   timed(sustained["steps_per_run"], stage=f"window (split {name})") / 1e6)
-        pool.set_option("split", 0)
+        for k, v in headline_split.items():        # back to the headline's options and plan
+            pool.set_option(k, v)
         pool.plan_views(cams, a.row_chunk, 0, 1)
         pool.set_stream(stream)
 
@@ -1604,10 +1606,10 @@ def main():
         split_arm = {"options": sopts, "tiles_split": res["on"].get("tiles"), "on": summ(res["on"]),
                      "off": summ(res["off"]),
                      "frames_equal_headline": None if frames_host is None else bool(np.array_equal(last_s, frames_host)),
-                     "note": "heavy-tile split on (the N >= 8 default) against off, interleaved twice in the same GPU "
-                             "state after the headline: lone two-view launch (kernel_ms_serial), 20-step window "
-                             "(value) and one sustained run each; the planned costliest tiles walk their long rays "
-                             "over 4 lanes each"}
+                     "note": "heavy-tile split on (the headline's options, or the N >= 8 default when the headline "
+                             "ran without) against off, interleaved twice in the same GPU state after the headline: "
+                             "lone two-view launch (kernel_ms_serial), 20-step window (value) and one sustained run "
+                             "each; the planned costliest tiles walk their long rays over 4 lanes each"}
         if split_arm["frames_equal_headline"] is False:
             raise SystemExit("split frames differ from the headline's")
 
@@ -1872,6 +1874,8 @@ def main():
                        "frames_in_flight": len(streams),
                        "hw_queues": int(os.environ.get("GPU_MAX_HW_QUEUES", "4")),
                        "launch_order": plan_label(pool),
+                       "heavy_tile_split": ({k: pool.get_option(k) for k in ("split", "split_segs", "split_level")}
+                                            if pool.get_option("split") else "off"),
                        "issue": ("one och_gpu_render_sharded_steps_dev call per timed window and rank (the "
                                  "library issues each step's render, RCCL exchange and shade)" if sharded_steps
                                  else "one och_gpu_render_steps_dev call per timed window (the library issues each "

@@ -456,7 +456,12 @@ def display_weight(world: int, exchange: str = "all_gather") -> float:
 # launch no longer waits on its longest rays, but the split waves cost
 # throughput, so it pays where a rank's launches are small and end on their
 # tails (tools/split_sweep.sh, profiles/r06/).  World sizes not listed: off.
-SPLIT_DEFAULTS = {8: {"split": 60, "split_segs": 4, "split_level": 6}}
+# The heavy-tile split by world size (bench.py sweeps): at N = 1
+# the costliest tiles only (T 80: +1.2 % over the 20-step window, -0.4 %
+# sustained, a lone frame 0.19 -> 0.16 ms; profiles/r06/r06ah/), off at N = 2 and
+# 4 (a tie), T 60 from N = 8, whose half-size launches end on their tails.
+SPLIT_DEFAULTS = {1: {"split": 80, "split_segs": 4, "split_level": 6}, 2: {"split": 0},
+                  8: {"split": 60, "split_segs": 4, "split_level": 6}}
 
 
 def split_defaults(world: int) -> dict:

@@ -44,7 +44,7 @@ def _bench_line(path: Path) -> dict:
 
 def test_readme_headline_quotes_the_committed_runs():
     """README's headline ranges (20-step window, sustained, the lone launch with
-    and without the split) are the min-max over the bench runs that
+    the headline's split and, from the split arm, without it) are the min-max over the bench runs that
     profiles/r06/headline.json lists -- committed bench.py outputs."""
     spec = json.loads((ROOT / "profiles" / "r06" / "headline.json").read_text())
     lines = [_bench_line(ROOT / f) for f in spec["n1_runs"]]
@@ -53,14 +53,13 @@ def test_readme_headline_quotes_the_committed_runs():
     sus = [l["sustained"]["value"] / 1e3 for l in lines]
     assert f"{min(sus):.1f}–{max(sus):.1f} G rays/s sustained" in readme
     assert f"{min(win):.1f}–{max(win):.1f} G over the driver's 20-step" in readme
-    lone = [l["roofline"]["kernel_ms_serial"] for l in lines]
-    split = []
-    for l in lines:                 # the split arm: one lone launch, or one per interleaved round
-        if l.get("split"):
-            v = l["split"]["on"]["kernel_ms_serial"] if "on" in l["split"] else l["split"]["kernel_ms_serial"]
-            split += v if isinstance(v, list) else [v]
+    lone = [l["roofline"]["kernel_ms_serial"] for l in lines]          # the headline's launch
+    off = []
+    for l in lines:                 # the split arm's launches without the split, one per interleaved round
+        off += l["split"]["off"]["kernel_ms_serial"]
+    assert all(l["config"]["heavy_tile_split"] != "off" for l in lines)
     assert f"one two-view frame in {min(lone):.3f}–{max(lone):.3f} ms" in readme
-    assert split and f"or {min(split):.3f}–{max(split):.3f} ms with the" in readme
+    assert off and f"{min(off):.3f}–{max(off):.3f} ms without it" in readme
 
 
 def test_n8_projection_quotes_the_committed_proxy():
