@@ -26,6 +26,8 @@ with the product's flags and checks, in every function that issues the load
   4. every traversal kernel (k_trace_grid, k_trace_bounce) admits 8 waves per
      SIMD by its SGPR and VGPR counts (above 80 SGPRs a SIMD takes 7, although
      the compiler's occupancy note still says 8).
+  5. no grid kernel spills SGPRs to VGPR lanes (the config-5 kernels' spills are
+     counted in the summary).
 Exit status 0 and a one-line summary when every kernel passes; 1 with the
 offending instruction otherwise.  Run by the csrc Makefile (`make isa-check`),
 __graft_entry__.build() and tests/test_isa_check.py.
@@ -315,6 +317,17 @@ def main(argv=None) -> int:
     for n, w in occ.items():
         if w < 8:
             problems.append(f"{n}: {res[n][0]} SGPRs / {res[n][1]} VGPRs admit {w} waves per SIMD, not 8")
+    # 5. no grid kernel spills SGPRs to VGPR lanes: under the 80-SGPR cap the
+    #    compiler spills rather than drop to 7 waves, and a spill reloaded in every
+    #    wave cost the split kernel 2 %.  The config-5 kernels
+    #    spill in their per-ray setup (counted, not refused).
+    spills = {n: sum(1 for l in lines if re.match(r"\s*v_(writelane|readlane)_b32", l))
+              for n, lines in fns.items() if "k_trace_grid" in n or "k_trace_bounce" in n}
+    summary["grid_spill_lanes"] = sum(v for n, v in spills.items() if "k_trace_grid" in n)
+    summary["bounce_spill_lanes"] = sum(v for n, v in spills.items() if "k_trace_bounce" in n)
+    for n, v in spills.items():
+        if v and "k_trace_grid" in n:
+            problems.append(f"{n}: {v} SGPR spill lanes (v_writelane / v_readlane)")
     if problems:
         print("isa_check: FAILED " + json.dumps(summary))
         for p in problems[:20]:
