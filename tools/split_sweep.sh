@@ -10,7 +10,7 @@ mkdir -p "$out"
 BA="--steps 20 --warmup 5 --no-other-configs --no-cpu-baseline --no-bounce --moving-steps 0 --no-cull-off"
 for r in $(seq "$rounds"); do
   for t in $arms; do
-    opt=""; [[ "$t" != 0 ]] && opt="--opt split=$t --opt split_segs=4 --opt split_level=6"
+    opt="--opt split=0"; [[ "$t" != 0 ]] && opt="--opt split=$t --opt split_segs=4 --opt split_level=6"
     for w in $worlds; do
       if [[ "$w" == 1 ]]; then
         timeout -k 10 200 python -u bench.py $BA $opt > "$out/n1_t${t}_r$r.json" 2> "$out/n1_t${t}_r$r.err" \
